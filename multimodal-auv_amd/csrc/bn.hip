@@ -1,0 +1,375 @@
+// Training-mode BatchNorm (+ residual add + ReLU), forward and backward, per MC group.
+//
+// The reference keeps every model in .train() for training, evaluation AND prediction
+// (train/multimodal.py:60,232; inference/predictors.py:27), so every MC pass normalises with
+// the batch statistics of THAT pass (torchvision BatchNorm2d, eps 1e-5, momentum 0.1).  With
+// the MC loop collapsed into G groups the statistics are taken per group g over its own
+// (B,H,W) rows, and the running statistics are updated G times in sample order —
+// bit-for-bit the sequence of G sequential forward calls.
+//
+// Layout: y/out/dout [G][M][C] (NHWC rows, M = B*H*W), per-group stats [G][C].
+// Statistics: per-thread Welford over a row slab, Chan merges across threads and blocks
+// (double in the final merge) — no E[x^2]-E[x]^2 cancellation.
+#include "mauv_common.h"
+
+using namespace mauv;
+
+namespace mauv {
+
+struct RowMap {
+  int tpr, rp, cpt;  // threads per row (float4 each), rows in parallel, float4 per thread
+};
+static inline RowMap row_map(int C) {
+  RowMap r;
+  const int c4 = C / 4;
+  r.tpr = c4 < 256 ? c4 : 256;
+  r.rp = 256 / r.tpr;
+  r.cpt = c4 / r.tpr;
+  return r;
+}
+
+constexpr int MAXCPT = 2;  // C <= 2048
+
+// Stage 1: per (group, block) partial (count, mean, M2) per channel.
+__global__ __launch_bounds__(256) void bn_stats_partial(const float* __restrict__ y, long long M,
+                                                        int C, int rpb, RowMap rm,
+                                                        float* __restrict__ pmean,
+                                                        float* __restrict__ pm2,
+                                                        float* __restrict__ pcnt) {
+  const int g = blockIdx.y, blk = blockIdx.x, nblk = gridDim.x;
+  const int tid = threadIdx.x;
+  const int t_c = tid % rm.tpr, t_r = tid / rm.tpr;
+  const long long r0 = (long long)blk * rpb;
+  const long long r1 = min(M, r0 + rpb);
+  const float* yg = y + (long long)g * M * C;
+  float mean[MAXCPT][4], m2[MAXCPT][4];
+#pragma unroll
+  for (int j = 0; j < MAXCPT; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { mean[j][e] = 0.f; m2[j][e] = 0.f; }
+  float n = 0.f;
+  for (long long r = r0 + t_r; r < r1; r += rm.rp) {
+    n += 1.f;
+    const float inv = 1.0f / n;
+#pragma unroll
+    for (int j = 0; j < MAXCPT; ++j) {
+      if (j >= rm.cpt) break;
+      const floatx4 v = *(const floatx4*)(yg + r * C + 4 * (t_c + j * rm.tpr));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[e] - mean[j][e];
+        mean[j][e] += d * inv;
+        m2[j][e] += d * (v[e] - mean[j][e]);
+      }
+    }
+  }
+  // merge the rp row-threads of every channel through LDS
+  __shared__ float s_mean[2048 * 2], s_m2[2048 * 2];  // rp * C <= 4096
+  __shared__ float s_n[256];
+  if (t_c == 0) s_n[t_r] = n;
+#pragma unroll
+  for (int j = 0; j < MAXCPT; ++j) {
+    if (j >= rm.cpt) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = 4 * (t_c + j * rm.tpr) + e;
+      s_mean[t_r * C + c] = mean[j][e];
+      s_m2[t_r * C + c] = m2[j][e];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float nn = 0.f, mu = 0.f, mm = 0.f;
+    for (int r = 0; r < rm.rp; ++r) {
+      const float nb = s_n[r];
+      if (nb == 0.f) continue;
+      const float mb = s_mean[r * C + c], m2b = s_m2[r * C + c];
+      const float nt = nn + nb;
+      const float d = mb - mu;
+      mu += d * (nb / nt);
+      mm += m2b + d * d * (nn * nb / nt);
+      nn = nt;
+    }
+    const long long o = ((long long)g * nblk + blk) * C + c;
+    pmean[o] = mu;
+    pm2[o] = mm;
+    if (c == 0) pcnt[(long long)g * nblk + blk] = nn;
+  }
+}
+
+// Stage 2: per channel, merge blocks (double), then the G running-stat updates in order.
+__global__ void bn_stats_final(int G, int nblk, int C, const float* __restrict__ pmean,
+                               const float* __restrict__ pm2, const float* __restrict__ pcnt,
+                               const float* __restrict__ gamma, const float* __restrict__ beta,
+                               float* __restrict__ run_mean, float* __restrict__ run_var,
+                               float momentum, float eps, float* __restrict__ mean_out,
+                               float* __restrict__ invstd_out, float* __restrict__ scale_out,
+                               float* __restrict__ shift_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float rmean = run_mean ? run_mean[c] : 0.f, rvar = run_var ? run_var[c] : 0.f;
+  for (int g = 0; g < G; ++g) {
+    double nn = 0.0, mu = 0.0, mm = 0.0;
+    for (int b = 0; b < nblk; ++b) {
+      const double nb = pcnt[(long long)g * nblk + b];
+      if (nb == 0.0) continue;
+      const long long o = ((long long)g * nblk + b) * C + c;
+      const double mb = pmean[o], m2b = pm2[o];
+      const double nt = nn + nb, d = mb - mu;
+      mu += d * (nb / nt);
+      mm += m2b + d * d * (nn * nb / nt);
+      nn = nt;
+    }
+    const double var = mm / nn;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * invstd;
+    mean_out[g * C + c] = (float)mu;
+    invstd_out[g * C + c] = invstd;
+    scale_out[g * C + c] = sc;
+    shift_out[g * C + c] = beta[c] - (float)mu * sc;
+    if (run_mean) {
+      const double uvar = nn > 1.0 ? mm / (nn - 1.0) : var;
+      rmean = (1.f - momentum) * rmean + momentum * (float)mu;
+      rvar = (1.f - momentum) * rvar + momentum * (float)uvar;
+    }
+  }
+  if (run_mean) { run_mean[c] = rmean; run_var[c] = rvar; }
+}
+
+// out = [relu]( y * scale[g][c] + shift[g][c] (+ res) )
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ y,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const float* __restrict__ res, int relu,
+                                                       float* __restrict__ out, long long M,
+                                                       int C) {
+  const int c4n = C / 4;
+  const long long per_g = M * c4n;
+  const int g = blockIdx.y;
+  const float* yg = y + (long long)g * M * C;
+  float* og = out + (long long)g * M * C;
+  const float* rg = res ? res + (long long)g * M * C : nullptr;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < per_g; i += (long long)gridDim.x * 256) {
+    const int c = 4 * (int)(i % c4n);
+    floatx4 v = *(const floatx4*)(yg + 4 * i);
+    const floatx4 sc = *(const floatx4*)(scale + g * C + c);
+    const floatx4 sh = *(const floatx4*)(shift + g * C + c);
+    v = v * sc + sh;
+    if (rg) v += *(const floatx4*)(rg + 4 * i);
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+    }
+    *(floatx4*)(og + 4 * i) = v;
+  }
+}
+
+// Backward stage 1: per (g, block) partial sums of dz and dz*xhat per channel,
+// dz = dout * (relu ? out > 0 : 1), xhat = (y - mean) * invstd.
+__global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ y,
+                                                      const float* __restrict__ out,
+                                                      const float* __restrict__ dout, int relu,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ invstd,
+                                                      long long M, int C, int rpb, RowMap rm,
+                                                      float* __restrict__ p1,
+                                                      float* __restrict__ p2) {
+  const int g = blockIdx.y, blk = blockIdx.x, nblk = gridDim.x;
+  const int tid = threadIdx.x;
+  const int t_c = tid % rm.tpr, t_r = tid / rm.tpr;
+  const long long r0 = (long long)blk * rpb;
+  const long long r1 = min(M, r0 + rpb);
+  const long long go = (long long)g * M * C;
+  float s1[MAXCPT][4], s2[MAXCPT][4], mu[MAXCPT][4], is[MAXCPT][4];
+#pragma unroll
+  for (int j = 0; j < MAXCPT; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s1[j][e] = 0.f; s2[j][e] = 0.f;
+      const int c = 4 * (t_c + j * rm.tpr) + e;
+      mu[j][e] = j < rm.cpt ? mean[g * C + c] : 0.f;
+      is[j][e] = j < rm.cpt ? invstd[g * C + c] : 0.f;
+    }
+  for (long long r = r0 + t_r; r < r1; r += rm.rp) {
+#pragma unroll
+    for (int j = 0; j < MAXCPT; ++j) {
+      if (j >= rm.cpt) break;
+      const long long o = go + r * C + 4 * (t_c + j * rm.tpr);
+      const floatx4 yv = *(const floatx4*)(y + o);
+      floatx4 dz = *(const floatx4*)(dout + o);
+      if (relu) {
+        const floatx4 ov = *(const floatx4*)(out + o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dz[e] = ov[e] > 0.f ? dz[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s1[j][e] += dz[e];
+        s2[j][e] += dz[e] * (yv[e] - mu[j][e]) * is[j][e];
+      }
+    }
+  }
+  __shared__ float sh1[4096], sh2[4096];
+#pragma unroll
+  for (int j = 0; j < MAXCPT; ++j) {
+    if (j >= rm.cpt) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = 4 * (t_c + j * rm.tpr) + e;
+      sh1[t_r * C + c] = s1[j][e];
+      sh2[t_r * C + c] = s2[j][e];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rm.rp; ++r) { a += sh1[r * C + c]; b += sh2[r * C + c]; }
+    const long long o = ((long long)g * nblk + blk) * C + c;
+    p1[o] = a;
+    p2[o] = b;
+  }
+}
+
+// Backward stage 2: k1 = sum dz / M, k2 = sum dz*xhat / M per (g,c); dgamma/dbeta += over g.
+__global__ void bn_bwd_final(int G, int nblk, int C, long long M, const float* __restrict__ p1,
+                             const float* __restrict__ p2, float* __restrict__ k1,
+                             float* __restrict__ k2, float* __restrict__ dgamma,
+                             float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double tg = 0.0, tb = 0.0;
+  for (int g = 0; g < G; ++g) {
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < nblk; ++k) {
+      const long long o = ((long long)g * nblk + k) * C + c;
+      a += p1[o];
+      b += p2[o];
+    }
+    k1[g * C + c] = (float)(a / (double)M);
+    k2[g * C + c] = (float)(b / (double)M);
+    tb += a;
+    tg += b;
+  }
+  if (dgamma) dgamma[c] += (float)tg;
+  if (dbeta) dbeta[c] += (float)tb;
+}
+
+// dy = gamma*invstd * (dz - k1 - xhat*k2); dres = dz (optional)
+__global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ y,
+                                                    const float* __restrict__ out,
+                                                    const float* __restrict__ dout, int relu,
+                                                    const float* __restrict__ mean,
+                                                    const float* __restrict__ invstd,
+                                                    const float* __restrict__ scale,
+                                                    const float* __restrict__ k1,
+                                                    const float* __restrict__ k2,
+                                                    float* __restrict__ dy,
+                                                    float* __restrict__ dres, long long M, int C) {
+  const int c4n = C / 4;
+  const long long per_g = M * c4n;
+  const int g = blockIdx.y;
+  const long long go = (long long)g * M * C;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < per_g; i += (long long)gridDim.x * 256) {
+    const int c = 4 * (int)(i % c4n);
+    const long long o = go + 4 * i;
+    floatx4 dz = *(const floatx4*)(dout + o);
+    if (relu) {
+      const floatx4 ov = *(const floatx4*)(out + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dz[e] = ov[e] > 0.f ? dz[e] : 0.f;
+    }
+    const floatx4 yv = *(const floatx4*)(y + o);
+    const floatx4 mu = *(const floatx4*)(mean + g * C + c);
+    const floatx4 is = *(const floatx4*)(invstd + g * C + c);
+    const floatx4 sc = *(const floatx4*)(scale + g * C + c);
+    const floatx4 a = *(const floatx4*)(k1 + g * C + c);
+    const floatx4 b = *(const floatx4*)(k2 + g * C + c);
+    const floatx4 xh = (yv - mu) * is;
+    *(floatx4*)(dy + o) = sc * (dz - a - xh * b);
+    if (dres) *(floatx4*)(dres + o) = dz;
+  }
+}
+
+static void reduce_geometry(long long M, int C, int& nblk, int& rpb) {
+  const RowMap rm = row_map(C);
+  long long target = (M + 255) / 256;  // ~256 rows per block
+  if (target > 1024) target = 1024;
+  if (target < 1) target = 1;
+  rpb = (int)((M + target - 1) / target);
+  if (rpb < rm.rp) rpb = rm.rp;
+  nblk = (int)((M + rpb - 1) / rpb);
+}
+
+static int ew_grid(long long n4) {
+  long long b = (n4 + 255) / 256;
+  if (b > 4096) b = 4096;
+  return (int)(b < 1 ? 1 : b);
+}
+
+}  // namespace mauv
+
+// Workspace floats needed by mauv_bn_fwd_train / mauv_bn_bwd for (G, M, C).
+MAUV_API long long mauv_bn_workspace_floats(int G, long long M, int C) {
+  int nblk, rpb;
+  reduce_geometry(M, C, nblk, rpb);
+  return (long long)G * nblk * (2LL * C + 1) + 2LL * G * C;
+}
+
+// Training-mode BN forward for G groups: statistics (mean/invstd/scale/shift out, [G][C]),
+// sequential running-stat updates (run_* nullable), then out = [relu](bn(y) (+ res)).
+MAUV_API int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const float* gamma,
+                               const float* beta, float* run_mean, float* run_var,
+                               float momentum, float eps, float* workspace, float* mean,
+                               float* invstd, float* scale, float* shift, const float* res,
+                               int relu, float* out, hipStream_t stream) {
+  if (C % 4 != 0 || C > 2048 || G <= 0 || M <= 0) { set_error("bn_fwd: unsupported C/G/M"); return kErrArg; }
+  int nblk, rpb;
+  reduce_geometry(M, C, nblk, rpb);
+  const RowMap rm = row_map(C);
+  float* pmean = workspace;
+  float* pm2 = pmean + (long long)G * nblk * C;
+  float* pcnt = pm2 + (long long)G * nblk * C;
+  hipLaunchKernelGGL(bn_stats_partial, dim3(nblk, G), dim3(256), 0, stream, y, M, C, rpb, rm,
+                     pmean, pm2, pcnt);
+  hipLaunchKernelGGL(bn_stats_final, dim3((C + 255) / 256), dim3(256), 0, stream, G, nblk, C,
+                     pmean, pm2, pcnt, gamma, beta, run_mean, run_var, momentum, eps, mean,
+                     invstd, scale, shift);
+  if (out) {
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C / 4 / 1), G), dim3(256), 0, stream,
+                       y, scale, shift, res, relu, out, M, C);
+  }
+  return check_launch("bn_fwd_train");
+}
+
+// out = [relu](y * scale + shift (+ res)) with precomputed per-group scale/shift.
+MAUV_API int mauv_bn_apply(const float* y, const float* scale, const float* shift,
+                           const float* res, int relu, float* out, int G, long long M, int C,
+                           hipStream_t stream) {
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C / 4), G), dim3(256), 0, stream, y,
+                     scale, shift, res, relu, out, M, C);
+  return check_launch("bn_apply");
+}
+
+// Training-mode BN backward (+ReLU mask from `out`, + residual split):
+//   dy = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)),  dres = dz (nullable),
+//   dgamma += sum dz*xhat, dbeta += sum dz (over all groups; nullable).
+MAUV_API int mauv_bn_bwd(const float* y, const float* out, const float* dout, int relu,
+                         const float* mean, const float* invstd, const float* scale, int G,
+                         long long M, int C, float* workspace, float* dy, float* dres,
+                         float* dgamma, float* dbeta, hipStream_t stream) {
+  if (C % 4 != 0 || C > 2048) { set_error("bn_bwd: unsupported C"); return kErrArg; }
+  int nblk, rpb;
+  reduce_geometry(M, C, nblk, rpb);
+  const RowMap rm = row_map(C);
+  float* p1 = workspace;
+  float* p2 = p1 + (long long)G * nblk * C;
+  float* k1 = p2 + (long long)G * nblk * C;
+  float* k2 = k1 + (long long)G * C;
+  hipLaunchKernelGGL(bn_bwd_partial, dim3(nblk, G), dim3(256), 0, stream, y, out, dout, relu,
+                     mean, invstd, M, C, rpb, rm, p1, p2);
+  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 255) / 256), dim3(256), 0, stream, G, nblk, C, M,
+                     p1, p2, k1, k2, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_bwd_apply, dim3(ew_grid(M * C / 4), G), dim3(256), 0, stream, y, out,
+                     dout, relu, mean, invstd, scale, k1, k2, dy, dres, M, C);
+  return check_launch("bn_bwd");
+}

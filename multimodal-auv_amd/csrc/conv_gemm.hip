@@ -1,0 +1,468 @@
+// Implicit-GEMM convolution (forward, data-gradient, weight-gradient) on CDNA4 MFMA, fp32.
+//
+// Replaces F.conv2d inside bayesian-torch Conv2dReparameterization.forward (called for every
+// ResNet-50 conv of the three trunks, reference models/base_models.py:15-18 and
+// models/model_utils.py:57-61) and its cuDNN backward (train/multimodal.py:138).  The MC
+// loop of train/multimodal.py:107-112 is collapsed into the grid: blockIdx.z = MC sample g,
+// each with its own sampled weight set W_g and its own activations.
+//
+// Layouts (all NHWC, channel-last, per MC group g):
+//   x   [G][B][H][W][Cin]   (arbitrary element strides; group stride 0 = shared input,
+//                            used by the stems which read the caller's NCHW images directly)
+//   W_g [G][Cout][R][S][Cin]  sampled weights (written by mauv_reparam_sample_conv)
+//   y   [G][B][Ho][Wo][Cout]
+// GEMM views:
+//   FWD   y [B*Ho*Wo][Cout]   = im2col(x)[B*Ho*Wo][R*S*Cin] . W_g^T
+//   DGRAD dx[B*H*W][Cin]      = gather(dy)[B*H*W][R*S*Cout] . W_g[(r,s,n)][c]
+//   WGRAD dW[Cout][R*S*Cin]   = dy^T[Cout][B*Ho*Wo] . im2col(x)[B*Ho*Wo][R*S*Cin]
+//                               (split-K over pixels; fp32 partial slabs, reduced
+//                                deterministically by mauv_reparam_bwd)
+// Tiles: 256 threads = 4 waves (2x2), block tile BM x BN x 16, double-buffered LDS stored
+// k-major ([k][row], rows contiguous) so each MFMA operand is one conflict-free ds_read_b32;
+// MFMA v_mfma_f32_32x32x2_f32 (exact fp32, fmaf-chain numerics).
+#include "mauv_common.h"
+
+namespace mauv {
+
+enum { FWD = 0, DGRAD = 1, WGRAD = 2 };
+
+struct ConvArgs {
+  int B, H, W, Cin, Ho, Wo, Cout, R, S, stride, pad;
+  long long xs_g, xs_b, xs_h, xs_w, xs_c;  // x element strides
+  const float* x;
+  const float* w;
+  long long ws_g;
+  const float* dy;  // [G][B*Ho*Wo][Cout]
+  float* out;
+  long long out_sg;
+  const float* bias;
+  long long bias_sg;
+  const float* addend;
+  int accumulate;
+  int G, splits, kchunk;
+  int M, N, K;  // GEMM dims (per group)
+};
+
+constexpr int BK = 16;
+constexpr int PAD = 4;
+
+template <int MODE, int BM, int BN, bool VA, bool VB>
+__global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 32, NI = WN / 32;
+  constexpr int NVA = BM * BK / 4 / 256, NVB = BN * BK / 4 / 256;
+  __shared__ float As[2][BK][BM + PAD];
+  __shared__ float Bs[2][BK][BN + PAD];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int g, sp = 0;
+  if constexpr (MODE == WGRAD) { g = blockIdx.z / a.splits; sp = blockIdx.z % a.splits; }
+  else g = blockIdx.z;
+  int kbeg = 0, kend = a.K;
+  if constexpr (MODE == WGRAD) { kbeg = sp * a.kchunk; kend = min(a.K, kbeg + a.kchunk); }
+
+  // ---------------- per-thread loader state ----------------
+  // A (FWD/DGRAD: k-contiguous rows; WGRAD: row-contiguous, rows = Cout)
+  long long a_off[NVA];
+  int a_p0[NVA], a_p1[NVA];
+  bool a_ok[NVA];
+  // B (FWD: k-contiguous rows = Cout; DGRAD: rows = Cin contiguous; WGRAD: rows=(r,s,c))
+  int b_r[NVB], b_s[NVB], b_c[NVB];
+  bool b_ok[NVB];
+  const float* xg = a.x + (long long)g * a.xs_g;
+  const float* dyg = a.dy + (long long)g * ((long long)a.B * a.Ho * a.Wo * a.Cout);
+  const float* wg = a.w + (long long)g * a.ws_g;
+
+#pragma unroll
+  for (int j = 0; j < NVA; ++j) {
+    const int idx = tid + 256 * j;
+    if constexpr (MODE == FWD || MODE == DGRAD) {
+      const int m = m0 + (idx >> 2);
+      a_ok[j] = m < a.M;
+      const int mm = a_ok[j] ? m : 0;
+      const int HW = (MODE == FWD) ? a.Ho * a.Wo : a.H * a.W;
+      const int WW = (MODE == FWD) ? a.Wo : a.W;
+      const int b = mm / HW, rem = mm - b * HW, oh = rem / WW, ow = rem - oh * WW;
+      if constexpr (MODE == FWD) {
+        a_off[j] = (long long)b * a.xs_b;
+        a_p0[j] = oh * a.stride - a.pad;
+        a_p1[j] = ow * a.stride - a.pad;
+      } else {
+        a_off[j] = (long long)b * a.Ho * a.Wo * a.Cout;
+        a_p0[j] = oh + a.pad;  // ih + pad
+        a_p1[j] = ow + a.pad;
+      }
+    } else {  // WGRAD: row4 fixed
+      const int row = m0 + 4 * (idx % (BM / 4));
+      a_p0[j] = row;
+      a_p1[j] = idx / (BM / 4);  // k offset within tile
+      a_ok[j] = true;
+      a_off[j] = 0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NVB; ++j) {
+    const int idx = tid + 256 * j;
+    if constexpr (MODE == FWD) {
+      const int n = n0 + (idx >> 2);
+      b_ok[j] = n < a.N;
+      b_r[j] = n;
+    } else if constexpr (MODE == DGRAD) {
+      b_c[j] = n0 + 4 * (idx % (BN / 4));
+      b_r[j] = idx / (BN / 4);
+      b_ok[j] = true;
+    } else {  // WGRAD: col=(r,s,c) of 4 consecutive columns
+      const int col = n0 + 4 * (idx % (BN / 4));
+      b_ok[j] = col < a.N;
+      const int cc = b_ok[j] ? col : 0;
+      const int rs = cc / a.Cin;
+      b_c[j] = cc - rs * a.Cin;
+      b_r[j] = rs / a.S;
+      b_s[j] = rs - b_r[j] * a.S;
+    }
+  }
+
+  floatx4 ra[NVA], rb[NVB];
+
+  auto load_a = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < NVA; ++j) {
+      const int idx = tid + 256 * j;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (MODE == FWD) {
+        const int kq = idx & 3;
+        if constexpr (VA) {
+          const int SC = a.S * a.Cin;
+          const int r = k0 / SC, rem = k0 - r * SC, s = rem / a.Cin;
+          const int c = rem - s * a.Cin + 4 * kq;
+          const int ih = a_p0[j] + r, iw = a_p1[j] + s;
+          if (a_ok[j] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+            v = *(const floatx4*)(xg + a_off[j] + (long long)ih * a.xs_h + (long long)iw * a.xs_w + c);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = k0 + 4 * kq + e;
+            if (a_ok[j] && k < kend) {
+              const int rs = k / a.Cin, c = k - rs * a.Cin, r = rs / a.S, s = rs - r * a.S;
+              const int ih = a_p0[j] + r, iw = a_p1[j] + s;
+              if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+                v[e] = xg[a_off[j] + (long long)ih * a.xs_h + (long long)iw * a.xs_w +
+                          (long long)c * a.xs_c];
+            }
+          }
+        }
+      } else if constexpr (MODE == DGRAD) {
+        const int kq = idx & 3;
+        if constexpr (VA) {
+          const int SC = a.S * a.Cout;
+          const int r = k0 / SC, rem = k0 - r * SC, s = rem / a.Cout;
+          const int n = rem - s * a.Cout + 4 * kq;
+          const int ohn = a_p0[j] - r, own = a_p1[j] - s;
+          if (a_ok[j] && ohn >= 0 && own >= 0 && ohn % a.stride == 0 && own % a.stride == 0) {
+            const int oh = ohn / a.stride, ow = own / a.stride;
+            if (oh < a.Ho && ow < a.Wo)
+              v = *(const floatx4*)(dyg + a_off[j] + ((long long)oh * a.Wo + ow) * a.Cout + n);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = k0 + 4 * kq + e;
+            if (a_ok[j] && k < kend) {
+              const int rs = k / a.Cout, n = k - rs * a.Cout, r = rs / a.S, s = rs - r * a.S;
+              const int ohn = a_p0[j] - r, own = a_p1[j] - s;
+              if (ohn >= 0 && own >= 0 && ohn % a.stride == 0 && own % a.stride == 0) {
+                const int oh = ohn / a.stride, ow = own / a.stride;
+                if (oh < a.Ho && ow < a.Wo)
+                  v[e] = dyg[a_off[j] + ((long long)oh * a.Wo + ow) * a.Cout + n];
+              }
+            }
+          }
+        }
+      } else {  // WGRAD A: dy^T, rows = cout, k = pixel
+        const int p = k0 + a_p1[j], co = a_p0[j];
+        if (p < kend) {
+          const float* src = dyg + (long long)p * a.Cout;
+          if constexpr (VA) {
+            if (co < a.Cout) v = *(const floatx4*)(src + co);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (co + e < a.Cout) v[e] = src[co + e];
+          }
+        }
+      }
+      ra[j] = v;
+    }
+  };
+
+  auto load_b = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < NVB; ++j) {
+      const int idx = tid + 256 * j;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (MODE == FWD) {
+        const int kq = idx & 3;
+        const int k = k0 + 4 * kq;
+        const float* src = wg + (long long)b_r[j] * a.K;
+        if constexpr (VB) {
+          if (b_ok[j] && k < kend) v = *(const floatx4*)(src + k);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (b_ok[j] && k + e < kend) v[e] = src[k + e];
+        }
+      } else if constexpr (MODE == DGRAD) {
+        const int k = k0 + b_r[j];
+        const int c = b_c[j];
+        if (k < kend) {
+          const int rs = k / a.Cout, n = k - rs * a.Cout, r = rs / a.S, s = rs - r * a.S;
+          const float* src = wg + (((long long)n * a.R + r) * a.S + s) * a.Cin;
+          if constexpr (VB) {
+            if (c < a.N) v = *(const floatx4*)(src + c);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (c + e < a.N) v[e] = src[c + e];
+          }
+        }
+      } else {  // WGRAD B: im2col(x), rows=(r,s,c), k = pixel
+        const int p = k0 + (idx / (BN / 4));
+        if (p < kend && b_ok[j]) {
+          const int HW = a.Ho * a.Wo;
+          const int b = p / HW, rem = p - b * HW, oh = rem / a.Wo, ow = rem - oh * a.Wo;
+          if constexpr (VB) {
+            const int ih = oh * a.stride - a.pad + b_r[j], iw = ow * a.stride - a.pad + b_s[j];
+            if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+              v = *(const floatx4*)(xg + (long long)b * a.xs_b + (long long)ih * a.xs_h +
+                                    (long long)iw * a.xs_w + b_c[j]);
+          } else {
+            const int col0 = n0 + 4 * (idx % (BN / 4));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int col = col0 + e;
+              if (col < a.N) {
+                const int rs = col / a.Cin, c = col - rs * a.Cin, r = rs / a.S, s = rs - r * a.S;
+                const int ih = oh * a.stride - a.pad + r, iw = ow * a.stride - a.pad + s;
+                if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+                  v[e] = xg[(long long)b * a.xs_b + (long long)ih * a.xs_h +
+                            (long long)iw * a.xs_w + (long long)c * a.xs_c];
+              }
+            }
+          }
+        }
+      }
+      rb[j] = v;
+    }
+  };
+
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < NVA; ++j) {
+      const int idx = tid + 256 * j;
+      if constexpr (MODE == WGRAD) {
+        const int kr = idx / (BM / 4), r4 = idx % (BM / 4);
+        *(floatx4*)&As[buf][kr][4 * r4] = ra[j];
+      } else {
+        const int row = idx >> 2, kq = idx & 3;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) As[buf][4 * kq + e][row] = ra[j][e];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NVB; ++j) {
+      const int idx = tid + 256 * j;
+      if constexpr (MODE == FWD) {
+        const int row = idx >> 2, kq = idx & 3;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Bs[buf][4 * kq + e][row] = rb[j][e];
+      } else {
+        const int kr = idx / (BN / 4), r4 = idx % (BN / 4);
+        *(floatx4*)&Bs[buf][kr][4 * r4] = rb[j];
+      }
+    }
+  };
+
+  floatx16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int ntiles = (kend - kbeg + BK - 1) / BK;
+  if (ntiles > 0) {
+    load_a(kbeg);
+    load_b(kbeg);
+    store_tiles(0);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      load_a(kbeg + (t + 1) * BK);
+      load_b(kbeg + (t + 1) * BK);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      float av[MI], bv[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) av[mi] = As[cur][2 * kk + lh][wm * WM + mi * 32 + li];
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) bv[ni] = Bs[cur][2 * kk + lh][wn * WN + ni * 32 + li];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+    }
+    if (more) store_tiles(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---------------- epilogue ----------------
+  float* outg;
+  if constexpr (MODE == WGRAD)
+    outg = a.out + ((long long)sp * a.G + g) * ((long long)a.M * a.N);
+  else
+    outg = a.out + (long long)g * a.out_sg;
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int col = n0 + wn * WN + ni * 32 + li;
+      if (col >= a.N) continue;
+      float bias = 0.f;
+      if constexpr (MODE == FWD)
+        if (a.bias) bias = a.bias[(long long)g * a.bias_sg + col];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row >= a.M) continue;
+        const long long o = (long long)row * a.N + col;
+        float v = acc[mi][ni][r] + bias;
+        if constexpr (MODE == DGRAD) {
+          if (a.addend) v += a.addend[(long long)g * a.out_sg + o];
+          if (a.accumulate) v += outg[o];
+        }
+        outg[o] = v;
+      }
+    }
+}
+
+template <int MODE, int BM, int BN, bool VA, bool VB>
+static void launch(const ConvArgs& a, hipStream_t st) {
+  dim3 grid(ceil_div(a.M, BM), ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
+  hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, VA, VB>), grid, dim3(256), 0, st, a);
+}
+
+template <int MODE, bool VA, bool VB>
+static void launch_tiles(const ConvArgs& a, hipStream_t st) {
+  // BN = 64 when the N extent is 64 or less (Cout=64 convs / Cin=64 dgrad), else 128.
+  const bool smallN = a.N <= 64;
+  const bool smallM = a.M <= 64;
+  if (smallM && smallN) launch<MODE, 64, 64, VA, VB>(a, st);
+  else if (smallM) launch<MODE, 64, 128, VA, VB>(a, st);
+  else if (smallN) launch<MODE, 128, 64, VA, VB>(a, st);
+  else launch<MODE, 128, 128, VA, VB>(a, st);
+}
+
+}  // namespace mauv
+
+using namespace mauv;
+
+static ConvArgs make_args(int G, int B, int H, int W, int Cin, int Cout, int R, int S,
+                          int stride, int pad, const long long* xs) {
+  ConvArgs a{};
+  a.G = G; a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.R = R; a.S = S;
+  a.stride = stride; a.pad = pad;
+  a.Ho = (H + 2 * pad - R) / stride + 1;
+  a.Wo = (W + 2 * pad - S) / stride + 1;
+  if (xs) { a.xs_g = xs[0]; a.xs_b = xs[1]; a.xs_h = xs[2]; a.xs_w = xs[3]; a.xs_c = xs[4]; }
+  else {
+    a.xs_c = 1; a.xs_w = Cin; a.xs_h = (long long)W * Cin; a.xs_b = (long long)H * W * Cin;
+    a.xs_g = (long long)B * H * W * Cin;
+  }
+  a.ws_g = (long long)Cout * R * S * Cin;
+  a.splits = 1;
+  return a;
+}
+
+// Forward: y[g] = conv(x[g], W_g) (+ bias[g]) — NHWC, fp32.
+// x_strides (nullable): element strides {group, batch, h, w, c} of x; NULL = dense NHWC.
+// Replaces F.conv2d in bayesian-torch Conv2dReparameterization.forward / F.linear in
+// LinearReparameterization.forward (a linear is the 1x1 case with H=W=1).
+MAUV_API int mauv_conv2d_fwd_f32(const float* x, const long long* x_strides, const float* w,
+                                 const float* bias, float* y, int G, int B, int H, int W,
+                                 int Cin, int Cout, int R, int S, int stride, int pad,
+                                 hipStream_t stream) {
+  if (G <= 0 || B <= 0 || Cin <= 0 || Cout <= 0) { set_error("conv2d_fwd: bad shape"); return kErrArg; }
+  ConvArgs a = make_args(G, B, H, W, Cin, Cout, R, S, stride, pad, x_strides);
+  a.x = x; a.w = w; a.out = y; a.bias = bias; a.bias_sg = Cout;
+  a.M = B * a.Ho * a.Wo; a.N = Cout; a.K = R * S * Cin;
+  a.out_sg = (long long)a.M * a.N;
+  const bool va = (Cin % BK == 0) && a.xs_c == 1 && (a.xs_w % 4 == 0) && (a.xs_h % 4 == 0) &&
+                  (a.xs_b % 4 == 0) && (a.xs_g % 4 == 0);
+  const bool vb = (a.K % 4 == 0);
+  if (va && vb) launch_tiles<FWD, true, true>(a, stream);
+  else if (vb) launch_tiles<FWD, false, true>(a, stream);
+  else launch_tiles<FWD, false, false>(a, stream);
+  return check_launch("conv2d_fwd");
+}
+
+// Data gradient: dx[g] = conv_transpose(dy[g], W_g) (+ addend) (+ dx if accumulate).
+MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx,
+                                      const float* addend, int accumulate, int G, int B, int H,
+                                      int W, int Cin, int Cout, int R, int S, int stride,
+                                      int pad, hipStream_t stream) {
+  ConvArgs a = make_args(G, B, H, W, Cin, Cout, R, S, stride, pad, nullptr);
+  a.dy = dy; a.w = w; a.out = dx; a.addend = addend; a.accumulate = accumulate;
+  a.M = B * H * W; a.N = Cin; a.K = R * S * Cout;
+  a.out_sg = (long long)a.M * a.N;
+  const bool va = (Cout % BK == 0), vb = (Cin % 4 == 0);
+  if (va && vb) launch_tiles<DGRAD, true, true>(a, stream);
+  else if (vb) launch_tiles<DGRAD, false, true>(a, stream);
+  else launch_tiles<DGRAD, false, false>(a, stream);
+  return check_launch("conv2d_bwd_data");
+}
+
+// Split count used by mauv_conv2d_bwd_weight for a given problem (host helper so the caller
+// can size the partial-slab workspace: splits * G * Cout * R*S*Cin floats).
+MAUV_API int mauv_conv2d_wgrad_splits(int G, int B, int H, int W, int Cin, int Cout, int R,
+                                      int S, int stride, int pad) {
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  const long long P = (long long)B * Ho * Wo;
+  const int N = R * S * Cin;
+  const long long tiles = (long long)ceil_div(Cout, Cout <= 64 ? 64 : 128) *
+                          ceil_div(N, N <= 64 ? 64 : 128) * G;
+  // target >= ~1024 workgroups, but keep >= 256 pixels per split
+  long long splits = (1024 + tiles - 1) / tiles;
+  const long long maxs = (P + 255) / 256;
+  if (splits > maxs) splits = maxs;
+  if (splits < 1) splits = 1;
+  if (splits > 256) splits = 256;
+  return (int)splits;
+}
+
+// Weight gradient partial slabs: ws[split][g][Cout][R*S*Cin] (reduced by mauv_reparam_bwd).
+MAUV_API int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strides,
+                                        const float* dy, float* ws, int splits, int G, int B,
+                                        int H, int W, int Cin, int Cout, int R, int S,
+                                        int stride, int pad, hipStream_t stream) {
+  ConvArgs a = make_args(G, B, H, W, Cin, Cout, R, S, stride, pad, x_strides);
+  a.x = x; a.dy = dy; a.out = ws;
+  a.M = Cout; a.N = R * S * Cin; a.K = B * a.Ho * a.Wo;
+  a.splits = splits;
+  a.kchunk = ((a.K + splits - 1) / splits + BK - 1) / BK * BK;
+  const bool va = (Cout % 4 == 0);
+  const bool vb = (Cin % 4 == 0) && a.xs_c == 1 && (a.xs_w % 4 == 0) && (a.xs_h % 4 == 0) &&
+                  (a.xs_b % 4 == 0) && (a.xs_g % 4 == 0);
+  if (va && vb) launch_tiles<WGRAD, true, true>(a, stream);
+  else if (va) launch_tiles<WGRAD, true, false>(a, stream);
+  else launch_tiles<WGRAD, false, false>(a, stream);
+  return check_launch("conv2d_bwd_weight");
+}

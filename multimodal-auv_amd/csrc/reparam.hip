@@ -1,0 +1,237 @@
+// Variational weight sampling, its backward, and the KL divergence (bayesian-torch 0.5.0
+// Conv2dReparameterization / LinearReparameterization semantics).
+//
+//   forward  (per MC sample g):  w_g = mu + softplus(rho) * eps_g     eps_g ~ N(0,1)
+//   backward:                    dmu  += sum_g dW_g
+//                                drho += sum_g dW_g * eps_g * sigmoid(rho)
+//   KL       (per tensor):       mean(log s_p - log s + (s^2 + (mu - m_p)^2) / (2 s_p^2) - 1/2)
+//
+// eps_g is never stored: it is regenerated from (seed, sample, layer, element quad) with
+// Philox4x32-10 in both passes, so the MC-batched launch (G samples at once) draws exactly
+// the stream G sequential single-sample forwards would.  An explicit eps pointer
+// ([G][numel], parameter (OIHW) order) replaces the generator for parity tests.
+// Sampled weights are written in the GEMM layout [G][Cout][R][S][Cin] (KRSC) consumed by
+// conv_gemm.hip; parameters / gradients stay in the reference's OIHW layout so state_dicts
+// keep bayesian-torch's shapes.
+#include "mauv_common.h"
+
+using namespace mauv;
+
+struct MauvKlEntry {
+  const float* mu;
+  const float* rho;
+  float* dmu;
+  float* drho;
+  long long numel;
+  float prior_mu;
+  float prior_sigma;
+};
+
+namespace mauv {
+
+__global__ __launch_bounds__(256) void reparam_sample_kernel(
+    const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
+    uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS,
+    float* __restrict__ out) {
+  const long long numel = (long long)Cout * Cin * RS;
+  const long long nq = (numel + 3) / 4;
+  for (long long q = blockIdx.x * 256LL + threadIdx.x; q < nq; q += (long long)gridDim.x * 256) {
+    float m[4], s[4];
+    long long dst[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long i = 4 * q + e;
+      if (i < numel) {
+        m[e] = mu[i];
+        s[e] = softplus(rho[i]);
+        const long long o = i / ((long long)Cin * RS);
+        const long long rem = i - o * Cin * RS;
+        const int c = (int)(rem / RS), rs = (int)(rem - (long long)c * RS);
+        dst[e] = (o * RS + rs) * Cin + c;
+      } else {
+        m[e] = 0.f; s[e] = 0.f; dst[e] = -1;
+      }
+    }
+    for (int g = 0; g < G; ++g) {
+      floatx4 ep;
+      if (eps) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ep[e] = dst[e] >= 0 ? eps[(long long)g * numel + 4 * q + e] : 0.f;
+      } else {
+        ep = normal4(seed, sample0 + g, layer, (uint32_t)q);
+      }
+      float* og = out + (long long)g * numel;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (dst[e] >= 0) og[dst[e]] = m[e] + s[e] * ep[e];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void reparam_bwd_kernel(
+    const float* __restrict__ dw, int splits, const float* __restrict__ mu,
+    const float* __restrict__ rho, const float* __restrict__ eps, uint64_t seed,
+    uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS,
+    float* __restrict__ dmu, float* __restrict__ drho) {
+  const long long numel = (long long)Cout * Cin * RS;
+  const long long nq = (numel + 3) / 4;
+  for (long long q = blockIdx.x * 256LL + threadIdx.x; q < nq; q += (long long)gridDim.x * 256) {
+    long long src[4];
+    float sg[4], gm[4] = {0.f, 0.f, 0.f, 0.f}, gr[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long i = 4 * q + e;
+      if (i < numel) {
+        sg[e] = sigmoidf_(rho[i]);
+        const long long o = i / ((long long)Cin * RS);
+        const long long rem = i - o * Cin * RS;
+        const int c = (int)(rem / RS), rs = (int)(rem - (long long)c * RS);
+        src[e] = (o * RS + rs) * Cin + c;
+      } else {
+        sg[e] = 0.f; src[e] = -1;
+      }
+    }
+    for (int g = 0; g < G; ++g) {
+      floatx4 ep;
+      if (eps) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ep[e] = src[e] >= 0 ? eps[(long long)g * numel + 4 * q + e] : 0.f;
+      } else {
+        ep = normal4(seed, sample0 + g, layer, (uint32_t)q);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (src[e] < 0) continue;
+        float d = 0.f;
+        for (int s = 0; s < splits; ++s) d += dw[((long long)s * G + g) * numel + src[e]];
+        gm[e] += d;
+        gr[e] += d * ep[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long i = 4 * q + e;
+      if (i < numel) {
+        dmu[i] += gm[e];
+        drho[i] += gr[e] * sg[e];
+      }
+    }
+  }
+}
+
+// KL: one block-row of partials per table entry (deterministic, fixed-order finalize).
+constexpr int KL_BLOCKS = 32;
+
+__global__ __launch_bounds__(256) void kl_partial_kernel(const MauvKlEntry* __restrict__ tab,
+                                                         double* __restrict__ partial) {
+  const MauvKlEntry t = tab[blockIdx.y];
+  const float lsp = logf(t.prior_sigma), inv2 = 1.0f / (2.0f * t.prior_sigma * t.prior_sigma);
+  double acc = 0.0;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < t.numel; i += (long long)KL_BLOCKS * 256) {
+    const float s = softplus(t.rho[i]);
+    const float d = t.mu[i] - t.prior_mu;
+    acc += (double)(lsp - logf(s) + (s * s + d * d) * inv2 - 0.5f);
+  }
+  __shared__ double red[4];
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    partial[(long long)blockIdx.y * KL_BLOCKS + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void kl_finalize_kernel(const MauvKlEntry* __restrict__ tab, int n,
+                                   const double* __restrict__ partial, float scale,
+                                   float* __restrict__ out) {
+  // one wave: lane-strided over entries, then fixed-order wave reduction
+  double acc = 0.0;
+  for (int e = threadIdx.x; e < n; e += 64) {
+    double s = 0.0;
+    for (int b = 0; b < KL_BLOCKS; ++b) s += partial[(long long)e * KL_BLOCKS + b];
+    acc += s / (double)tab[e].numel;
+  }
+  acc = wave_sum_d(acc);
+  if (threadIdx.x == 0) out[0] = (float)(acc * scale);
+}
+
+__global__ __launch_bounds__(256) void kl_bwd_kernel(const MauvKlEntry* __restrict__ tab,
+                                                     const float* __restrict__ coef_dev,
+                                                     float scale) {
+  const MauvKlEntry t = tab[blockIdx.y];
+  const float coef = (coef_dev ? coef_dev[0] : 1.0f) * scale / (float)t.numel;
+  const float inv_sp2 = 1.0f / (t.prior_sigma * t.prior_sigma);
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < t.numel; i += (long long)gridDim.x * 256) {
+    const float r = t.rho[i];
+    const float s = softplus(r);
+    t.dmu[i] += coef * (t.mu[i] - t.prior_mu) * inv_sp2;
+    t.drho[i] += coef * (-1.0f / s + s * inv_sp2) * sigmoidf_(r);
+  }
+}
+
+__global__ void philox_raw_kernel(uint64_t seed, uint64_t sample, uint32_t layer, int nq,
+                                  uint4* out, floatx4* nrm) {
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  out[q] = philox4x32_10(make_uint4(q, (uint32_t)sample, layer, (uint32_t)(sample >> 32)),
+                         make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+  nrm[q] = normal4(seed, sample, layer, q);
+}
+
+static int grid_for(long long nq) {
+  long long b = (nq + 255) / 256;
+  if (b > 65536) b = 65536;
+  return (int)(b < 1 ? 1 : b);
+}
+
+}  // namespace mauv
+
+// Sample G weight sets: out[g] (KRSC) = mu + softplus(rho) * eps_g.  mu/rho in OIHW
+// [Cout][Cin][R*S] (linear: [out][in], R*S = 1; bias: Cout = n, Cin = RS = 1).
+MAUV_API int mauv_reparam_sample(const float* mu, const float* rho, const float* eps,
+                                 unsigned long long seed, unsigned long long sample0,
+                                 unsigned int layer, int G, int Cout, int Cin, int RS,
+                                 float* out, hipStream_t stream) {
+  const long long nq = ((long long)Cout * Cin * RS + 3) / 4;
+  hipLaunchKernelGGL(reparam_sample_kernel, dim3(grid_for(nq)), dim3(256), 0, stream, mu, rho,
+                     eps, seed, sample0, layer, G, Cout, Cin, RS, out);
+  return check_launch("reparam_sample");
+}
+
+// dmu += sum_g sum_s dw[s][g];  drho += sum_g (sum_s dw[s][g]) * eps_g * sigmoid(rho).
+MAUV_API int mauv_reparam_bwd(const float* dw, int splits, const float* mu, const float* rho,
+                              const float* eps, unsigned long long seed,
+                              unsigned long long sample0, unsigned int layer, int G, int Cout,
+                              int Cin, int RS, float* dmu, float* drho, hipStream_t stream) {
+  const long long nq = ((long long)Cout * Cin * RS + 3) / 4;
+  hipLaunchKernelGGL(reparam_bwd_kernel, dim3(grid_for(nq)), dim3(256), 0, stream, dw, splits,
+                     mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS, dmu, drho);
+  return check_launch("reparam_bwd");
+}
+
+MAUV_API int mauv_kl_workspace_bytes(int n_entries) { return n_entries * KL_BLOCKS * 8; }
+
+// out[0] = scale * sum_entries mean(KL elementwise) — get_kl_loss over a table of tensors.
+MAUV_API int mauv_kl_fwd(const MauvKlEntry* table, int n, double* workspace, float scale,
+                         float* out, hipStream_t stream) {
+  if (n <= 0 || n > 65535) { set_error("kl_fwd: bad table size"); return kErrArg; }
+  hipLaunchKernelGGL(kl_partial_kernel, dim3(KL_BLOCKS, n), dim3(256), 0, stream, table, workspace);
+  hipLaunchKernelGGL(kl_finalize_kernel, dim3(1), dim3(64), 0, stream, table, n, workspace, scale, out);
+  return check_launch("kl_fwd");
+}
+
+// dmu/drho += (coef_dev ? *coef_dev : 1) * scale * dKL/d(mu,rho) for every table entry.
+MAUV_API int mauv_kl_bwd(const MauvKlEntry* table, int n, const float* coef_dev, float scale,
+                         hipStream_t stream) {
+  if (n <= 0 || n > 65535) { set_error("kl_bwd: bad table size"); return kErrArg; }
+  hipLaunchKernelGGL(kl_bwd_kernel, dim3(64, n), dim3(256), 0, stream, table, coef_dev, scale);
+  return check_launch("kl_bwd");
+}
+
+// Debug/test: raw Philox4x32-10 words and the derived normals for quads [0, nq).
+MAUV_API int mauv_philox_raw(unsigned long long seed, unsigned long long sample,
+                             unsigned int layer, int nq, unsigned int* out_u32x4,
+                             float* out_normal4, hipStream_t stream) {
+  hipLaunchKernelGGL(philox_raw_kernel, dim3((nq + 255) / 256), dim3(256), 0, stream, seed,
+                     sample, layer, nq, (uint4*)out_u32x4, (floatx4*)out_normal4);
+  return check_launch("philox_raw");
+}

@@ -1,0 +1,93 @@
+"""ctypes binding of libmauv_hip.so — the C-ABI declared in include/mauv.h.
+
+The library is the product: there is no fallback.  If it is missing or was built for
+another architecture, importing ``mauv`` raises immediately.  torch is imported first so
+that the HIP runtime the library links against (soname libamdhip64.so.7) resolves to the
+one PyTorch-ROCm already loaded — stream handles are then interchangeable.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must load libamdhip64 before the extension)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MAUV_LIB", os.path.join(_HERE, "libmauv_hip.so"))
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+LL = ctypes.c_longlong
+F = ctypes.c_float
+U64 = ctypes.c_ulonglong
+U32 = ctypes.c_uint
+
+# name -> argtypes (restype is int unless listed in _RESTYPES)
+SIGNATURES = {
+    "mauv_abi_version": [],
+    "mauv_last_error": [],
+    # conv_gemm.hip
+    "mauv_conv2d_fwd_f32": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
+    "mauv_conv2d_bwd_data_f32": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
+    "mauv_conv2d_wgrad_splits": [I, I, I, I, I, I, I, I, I, I],
+    "mauv_conv2d_bwd_weight_f32": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
+    # reparam.hip
+    "mauv_reparam_sample": [P, P, P, U64, U64, U32, I, I, I, I, P, P],
+    "mauv_reparam_bwd": [P, I, P, P, P, U64, U64, U32, I, I, I, I, P, P, P],
+    "mauv_kl_workspace_bytes": [I],
+    "mauv_kl_fwd": [P, I, P, F, P, P],
+    "mauv_kl_bwd": [P, I, P, F, P],
+    "mauv_philox_raw": [U64, U64, U32, I, P, P, P],
+    # bn.hip
+    "mauv_bn_workspace_floats": [I, LL, I],
+    "mauv_bn_fwd_train": [P, I, LL, I, P, P, P, P, F, F, P, P, P, P, P, P, I, P, P],
+    "mauv_bn_apply": [P, P, P, P, I, P, I, LL, I, P],
+    "mauv_bn_bwd": [P, P, P, I, P, P, P, I, LL, I, P, P, P, P, P, P],
+    # pool.hip
+    "mauv_maxpool_fwd": [P, I, I, I, I, P, P, P],
+    "mauv_maxpool_bwd": [P, P, I, I, I, I, P, P],
+    "mauv_avgpool_fwd": [P, I, I, I, P, P],
+    "mauv_avgpool_bwd": [P, I, I, I, P, P],
+    # head.hip
+    "mauv_attn_t": [P, I, P, P],
+    "mauv_attn_t_bwd": [P, P, I, P, P],
+    "mauv_attn_out": [P, P, I, P, I, I, P],
+    "mauv_attn_out_bwd": [P, I, I, P, P, I, P, P, P],
+    "mauv_colsum": [P, I, I, I, P, I, P],
+    "mauv_mc_mean_ce": [P, P, I, I, I, P, P, P],
+    "mauv_mc_mean_bwd": [P, P, P, P, I, I, I, P, P],
+    "mauv_mc_stats": [P, I, I, I, F, P, I, P],
+    "mauv_mc_finalize": [P, I, I, I, F, P, P, P, P, P, P],
+    "mauv_nonfinite_count": [P, LL, P, P],
+}
+_RESTYPES = {"mauv_last_error": ctypes.c_char_p, "mauv_bn_workspace_floats": LL}
+
+
+class MauvError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libmauv_hip.so not found at {LIB_PATH}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
+            "There is no CPU/PyTorch fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argt in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argt
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    return lib
+
+
+lib = _load()
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib.mauv_last_error().decode(errors="replace")
+        raise MauvError(f"{what or 'mauv'} failed ({rc}): {msg}")
+    return rc
+
+
+def exported_symbols():
+    return list(SIGNATURES)

@@ -1,0 +1,185 @@
+"""Thin tensor-level wrappers over the libmauv_hip C-ABI (include/mauv.h).
+
+Every function launches on the current torch stream and is asynchronous; tensors must be
+contiguous device tensors of the documented dtype.  These wrappers do no arithmetic of
+their own — all compute is in the HIP kernels.
+"""
+import ctypes
+
+import torch
+
+from ._lib import lib, check
+
+_LL5 = ctypes.c_longlong * 5
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _f32(*ts):
+    for t in ts:
+        if t is not None:
+            assert t.is_cuda and t.dtype == torch.float32 and t.is_contiguous(), \
+                (t.device, t.dtype, t.is_contiguous(), t.shape)
+
+
+def out_hw(H, R, stride, pad):
+    return (H + 2 * pad - R) // stride + 1
+
+
+# ----------------------------------------------------------------------- convolutions
+def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_strides=None):
+    """y[G][B*Ho*Wo][Cout] = conv(x[g], w[g]) (+ bias[g]); w: [G][Cout][R][R][Cin]."""
+    _f32(w, y, bias)
+    assert x.is_cuda and x.dtype == torch.float32
+    xs = None if x_strides is None else _LL5(*x_strides)
+    check(lib.mauv_conv2d_fwd_f32(_p(x), xs, _p(w), _p(bias), _p(y), G, B, H, W, Cin, Cout,
+                                  R, R, stride, pad, stream()), "conv2d_fwd")
+
+
+def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=None,
+                    accumulate=False):
+    _f32(dy, w, dx, addend)
+    check(lib.mauv_conv2d_bwd_data_f32(_p(dy), _p(w), _p(dx), _p(addend), int(accumulate), G,
+                                       B, H, W, Cin, Cout, R, R, stride, pad, stream()),
+          "conv2d_bwd_data")
+
+
+def wgrad_splits(G, B, H, W, Cin, Cout, R, stride, pad):
+    return lib.mauv_conv2d_wgrad_splits(G, B, H, W, Cin, Cout, R, R, stride, pad)
+
+
+def conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, R, stride, pad,
+                      x_strides=None):
+    """ws[splits][G][Cout][R*R*Cin] partial slabs."""
+    _f32(dy, ws)
+    xs = None if x_strides is None else _LL5(*x_strides)
+    check(lib.mauv_conv2d_bwd_weight_f32(_p(x), xs, _p(dy), _p(ws), splits, G, B, H, W, Cin,
+                                         Cout, R, R, stride, pad, stream()),
+          "conv2d_bwd_weight")
+
+
+# ----------------------------------------------------------------------- reparam / KL
+def reparam_sample(mu, rho, out, G, seed, sample0, layer, Cout, Cin, RS, eps=None):
+    _f32(mu, rho, out, eps)
+    check(lib.mauv_reparam_sample(_p(mu), _p(rho), _p(eps), seed, sample0, layer, G, Cout, Cin,
+                                  RS, _p(out), stream()), "reparam_sample")
+
+
+def reparam_bwd(dw, splits, mu, rho, dmu, drho, G, seed, sample0, layer, Cout, Cin, RS,
+                eps=None):
+    _f32(dw, mu, rho, dmu, drho, eps)
+    check(lib.mauv_reparam_bwd(_p(dw), splits, _p(mu), _p(rho), _p(eps), seed, sample0, layer,
+                               G, Cout, Cin, RS, _p(dmu), _p(drho), stream()), "reparam_bwd")
+
+
+def kl_fwd(table, n, workspace, out, scale=1.0):
+    check(lib.mauv_kl_fwd(_p(table), n, _p(workspace), scale, _p(out), stream()), "kl_fwd")
+
+
+def kl_bwd(table, n, coef=None, scale=1.0):
+    check(lib.mauv_kl_bwd(_p(table), n, _p(coef), scale, stream()), "kl_bwd")
+
+
+def philox_raw(seed, sample, layer, nq, device="cuda"):
+    raw = torch.empty(nq * 4, dtype=torch.int32, device=device)
+    nrm = torch.empty(nq * 4, dtype=torch.float32, device=device)
+    check(lib.mauv_philox_raw(seed, sample, layer, nq, _p(raw), _p(nrm), stream()),
+          "philox_raw")
+    return raw, nrm
+
+
+# ----------------------------------------------------------------------- batch norm
+def bn_workspace_floats(G, M, C):
+    return int(lib.mauv_bn_workspace_floats(G, M, C))
+
+
+def bn_fwd_train(y, G, M, C, gamma, beta, run_mean, run_var, momentum, eps, ws, mean, invstd,
+                 scale, shift, res, relu, out):
+    _f32(y, gamma, beta, run_mean, run_var, ws, mean, invstd, scale, shift, res, out)
+    check(lib.mauv_bn_fwd_train(_p(y), G, M, C, _p(gamma), _p(beta), _p(run_mean),
+                                _p(run_var), momentum, eps, _p(ws), _p(mean), _p(invstd),
+                                _p(scale), _p(shift), _p(res), int(relu), _p(out), stream()),
+          "bn_fwd_train")
+
+
+def bn_apply(y, scale, shift, res, relu, out, G, M, C):
+    check(lib.mauv_bn_apply(_p(y), _p(scale), _p(shift), _p(res), int(relu), _p(out), G, M, C,
+                            stream()), "bn_apply")
+
+
+def bn_bwd(y, out, dout, relu, mean, invstd, scale, G, M, C, ws, dy, dres=None, dgamma=None,
+           dbeta=None):
+    _f32(y, out, dout, mean, invstd, scale, ws, dy, dres, dgamma, dbeta)
+    check(lib.mauv_bn_bwd(_p(y), _p(out), _p(dout), int(relu), _p(mean), _p(invstd), _p(scale),
+                          G, M, C, _p(ws), _p(dy), _p(dres), _p(dgamma), _p(dbeta), stream()),
+          "bn_bwd")
+
+
+# ----------------------------------------------------------------------- pooling
+def maxpool_fwd(x, N, H, W, C, y, idx):
+    check(lib.mauv_maxpool_fwd(_p(x), N, H, W, C, _p(y), _p(idx), stream()), "maxpool_fwd")
+
+
+def maxpool_bwd(dy, idx, N, H, W, C, dx):
+    check(lib.mauv_maxpool_bwd(_p(dy), _p(idx), N, H, W, C, _p(dx), stream()), "maxpool_bwd")
+
+
+def avgpool_fwd(x, N, HW, C, y):
+    check(lib.mauv_avgpool_fwd(_p(x), N, HW, C, _p(y), stream()), "avgpool_fwd")
+
+
+def avgpool_bwd(dy, N, HW, C, dx):
+    check(lib.mauv_avgpool_bwd(_p(dy), N, HW, C, _p(dx), stream()), "avgpool_bwd")
+
+
+# ----------------------------------------------------------------------- head
+def attn_t(qkv, rows, t):
+    check(lib.mauv_attn_t(_p(qkv), rows, _p(t), stream()), "attn_t")
+
+
+def attn_t_bwd(dt, t, rows, dqkv):
+    check(lib.mauv_attn_t_bwd(_p(dt), _p(t), rows, _p(dqkv), stream()), "attn_t_bwd")
+
+
+def attn_out(qkv, s, rows, comb, ld, off):
+    check(lib.mauv_attn_out(_p(qkv), _p(s), rows, _p(comb), ld, off, stream()), "attn_out")
+
+
+def attn_out_bwd(dcomb, ld, off, qkv, s, rows, dqkv, ds):
+    check(lib.mauv_attn_out_bwd(_p(dcomb), ld, off, _p(qkv), _p(s), rows, _p(dqkv), _p(ds),
+                                stream()), "attn_out_bwd")
+
+
+def colsum(dy, G, rows, N, out, accumulate=False):
+    check(lib.mauv_colsum(_p(dy), G, rows, N, _p(out), int(accumulate), stream()), "colsum")
+
+
+def mc_mean_ce(logits, labels, G, B, C, mean, loss):
+    check(lib.mauv_mc_mean_ce(_p(logits), _p(labels), G, B, C, _p(mean), _p(loss), stream()),
+          "mc_mean_ce")
+
+
+def mc_mean_bwd(dmean, gloss, mean, labels, G, B, C, dlogits):
+    check(lib.mauv_mc_mean_bwd(_p(dmean), _p(gloss), _p(mean), _p(labels), G, B, C,
+                               _p(dlogits), stream()), "mc_mean_bwd")
+
+
+def mc_stats(logits, G, B, C, eps_h, sums, accumulate=False):
+    check(lib.mauv_mc_stats(_p(logits), G, B, C, eps_h, _p(sums), int(accumulate), stream()),
+          "mc_stats")
+
+
+def mc_finalize(sums, N, B, C, eps_pred, mean_prob=None, var_unc=None, alea=None,
+                pred_entropy=None, pred=None):
+    check(lib.mauv_mc_finalize(_p(sums), N, B, C, eps_pred, _p(mean_prob), _p(var_unc),
+                               _p(alea), _p(pred_entropy), _p(pred), stream()), "mc_finalize")
+
+
+def nonfinite_count(t, out):
+    check(lib.mauv_nonfinite_count(_p(t), t.numel(), _p(out), stream()), "nonfinite_count")

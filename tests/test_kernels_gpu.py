@@ -1,0 +1,323 @@
+"""Kernel-level parity on the GPU: every libmauv_hip kernel vs a float64 torch-CPU
+reference of the same op (conv fwd/dgrad/wgrad, BN fwd/bwd, pooling, reparam, KL, head).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def close(a, b, rtol=1e-4, atol=1e-5):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    err = (a - b).abs().max().item()
+    lim = atol + rtol * b.abs().max().item()
+    assert err <= lim, f"max err {err:.3e} > {lim:.3e}"
+
+
+CONV_CASES = [
+    # G, B, H, Cin, Cout, R, stride, pad
+    (2, 2, 8, 64, 64, 1, 1, 0),
+    (2, 2, 8, 64, 64, 3, 1, 1),
+    (2, 3, 9, 128, 128, 3, 2, 1),
+    (1, 2, 8, 256, 512, 1, 2, 0),
+    (2, 2, 4, 512, 2048, 1, 1, 0),
+    (3, 2, 5, 64, 256, 1, 1, 0),
+]
+
+
+def _ref_conv(x, w, stride, pad):
+    # x [G,B,H,W,C] w [G,Cout,R,R,Cin] -> y [G,B,Ho,Wo,Cout] (float64)
+    outs = []
+    for g in range(x.shape[0]):
+        xg = x[g].permute(0, 3, 1, 2).double()
+        wg = w[g].permute(0, 3, 1, 2).double()
+        outs.append(F.conv2d(xg, wg, stride=stride, padding=pad).permute(0, 2, 3, 1))
+    return torch.stack(outs)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case):
+    from mauv import ops
+    G, B, H, Cin, Cout, R, st, pad = case
+    torch.manual_seed(0)
+    x = torch.randn(G, B, H, H, Cin)
+    w = torch.randn(G, Cout, R, R, Cin) / math.sqrt(Cin * R * R)
+    Ho = ops.out_hw(H, R, st, pad)
+    ref = _ref_conv(x, w, st, pad)
+    y = torch.empty(G, B, Ho, Ho, Cout, device=dev)
+    ops.conv2d_fwd(x.to(dev), w.to(dev), y, G, B, H, H, Cin, Cout, R, st, pad)
+    close(y, ref)
+
+    dy = torch.randn(G, B, Ho, Ho, Cout)
+    dx_ref, dw_ref = [], []
+    for g in range(G):
+        xg = x[g].permute(0, 3, 1, 2).double().requires_grad_(True)
+        wg = w[g].permute(0, 3, 1, 2).double().requires_grad_(True)
+        out = F.conv2d(xg, wg, stride=st, padding=pad)
+        out.backward(dy[g].permute(0, 3, 1, 2).double())
+        dx_ref.append(xg.grad.permute(0, 2, 3, 1))
+        dw_ref.append(wg.grad.permute(0, 2, 3, 1))
+    dx = torch.empty(G, B, H, H, Cin, device=dev)
+    addend = torch.randn(G, B, H, H, Cin)
+    ops.conv2d_bwd_data(dy.to(dev), w.to(dev), dx, G, B, H, H, Cin, Cout, R, st, pad,
+                        addend=addend.to(dev))
+    close(dx, torch.stack(dx_ref) + addend.double())
+    splits = ops.wgrad_splits(G, B, H, H, Cin, Cout, R, st, pad)
+    ws = torch.empty(splits, G, Cout, R * R * Cin, device=dev)
+    ops.conv2d_bwd_weight(x.to(dev), dy.to(dev), ws, splits, G, B, H, H, Cin, Cout, R, st, pad)
+    close(ws.sum(0).view(G, Cout, R, R, Cin), torch.stack(dw_ref))
+
+
+@pytest.mark.parametrize("cin", [3, 1])
+def test_stem_nchw_shared_input(cin):
+    """Stem 7x7/2 reading the caller's NCHW images directly, input shared by G groups."""
+    from mauv import ops
+    G, B, H = 3, 2, 20
+    torch.manual_seed(1)
+    x = torch.randn(B, cin, H, H)
+    w = torch.randn(G, 64, 7, 7, cin) * 0.1
+    Ho = ops.out_hw(H, 7, 2, 3)
+    strides = (0, cin * H * H, H, 1, H * H)
+    y = torch.empty(G, B, Ho, Ho, 64, device=dev)
+    xd = x.to(dev)
+    ops.conv2d_fwd(xd, w.to(dev), y, G, B, H, H, cin, 64, 7, 2, 3, x_strides=strides)
+    xs = x.permute(0, 2, 3, 1).unsqueeze(0).expand(G, -1, -1, -1, -1)
+    close(y, _ref_conv(xs, w, 2, 3))
+    dy = torch.randn(G, B, Ho, Ho, 64)
+    splits = ops.wgrad_splits(G, B, H, H, cin, 64, 7, 2, 3)
+    ws = torch.empty(splits, G, 64, 49 * cin, device=dev)
+    ops.conv2d_bwd_weight(xd, dy.to(dev), ws, splits, G, B, H, H, cin, 64, 7, 2, 3,
+                          x_strides=strides)
+    ref = []
+    for g in range(G):
+        wg = w[g].permute(0, 3, 1, 2).double().requires_grad_(True)
+        F.conv2d(x.double(), wg, stride=2, padding=3).backward(dy[g].permute(0, 3, 1, 2).double())
+        ref.append(wg.grad.permute(0, 2, 3, 1))
+    close(ws.sum(0).view(G, 64, 7, 7, cin), torch.stack(ref))
+
+
+@pytest.mark.parametrize("K,N", [(2048, 384), (384, 1284), (1284, 32), (32, 7), (128, 128)])
+def test_linear_as_1x1(K, N):
+    from mauv import ops
+    G, B = 2, 5
+    torch.manual_seed(2)
+    x = torch.randn(G, B, K)
+    w = torch.randn(G, N, K) / math.sqrt(K)
+    b = torch.randn(G, N)
+    y = torch.empty(G, B, N, device=dev)
+    ops.conv2d_fwd(x.to(dev), w.to(dev), y, G, B, 1, 1, K, N, 1, 1, 0, bias=b.to(dev))
+    ref = torch.einsum("gbk,gnk->gbn", x.double(), w.double()) + b.double()[:, None]
+    close(y, ref)
+    dy = torch.randn(G, B, N)
+    dx = torch.empty(G, B, K, device=dev)
+    ops.conv2d_bwd_data(dy.to(dev), w.to(dev), dx, G, B, 1, 1, K, N, 1, 1, 0)
+    close(dx, torch.einsum("gbn,gnk->gbk", dy.double(), w.double()))
+    splits = ops.wgrad_splits(G, B, 1, 1, K, N, 1, 1, 0)
+    ws = torch.empty(splits, G, N, K, device=dev)
+    ops.conv2d_bwd_weight(x.to(dev), dy.to(dev), ws, splits, G, B, 1, 1, K, N, 1, 1, 0)
+    close(ws.sum(0), torch.einsum("gbn,gbk->gnk", dy.double(), x.double()))
+    db = torch.empty(G, N, device=dev)
+    ops.colsum(dy.to(dev), G, B, N, db)
+    close(db, dy.double().sum(1))
+
+
+@pytest.mark.parametrize("C,relu,res", [(64, True, False), (256, True, True), (2048, False, False)])
+def test_bn_fwd_bwd(C, relu, res):
+    from mauv import ops
+    G, B, H = 3, 4, 5
+    M = B * H * H
+    torch.manual_seed(3)
+    y = torch.randn(G, M, C) * 3 + 2
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
+    rm, rv = torch.randn(C), torch.rand(C) + 0.5
+    r = torch.randn(G, M, C) if res else None
+    yd = y.to(dev)
+    rmd, rvd = rm.clone().to(dev), rv.clone().to(dev)
+    wsz = ops.bn_workspace_floats(G, M, C)
+    ws = torch.empty(wsz, device=dev)
+    mean, invstd, scale, shift = (torch.empty(G, C, device=dev) for _ in range(4))
+    out = torch.empty(G, M, C, device=dev)
+    ops.bn_fwd_train(yd, G, M, C, gamma.to(dev), beta.to(dev), rmd, rvd, 0.1, 1e-5, ws, mean,
+                     invstd, scale, shift, None if r is None else r.to(dev), relu, out)
+    # reference: G sequential torch BN calls in train mode
+    bn = torch.nn.BatchNorm2d(C).double()
+    bn.weight.data.copy_(gamma)
+    bn.bias.data.copy_(beta)
+    bn.running_mean.copy_(rm)
+    bn.running_var.copy_(rv)
+    refs, xs = [], []
+    for g in range(G):
+        xg = y[g].double().view(B, H, H, C).permute(0, 3, 1, 2).requires_grad_(True)
+        o = bn(xg)
+        if r is not None:
+            o = o + r[g].double().view(B, H, H, C).permute(0, 3, 1, 2)
+        if relu:
+            o = torch.relu(o)
+        refs.append(o)
+        xs.append(xg)
+    ref = torch.stack([o.permute(0, 2, 3, 1).reshape(M, C) for o in refs])
+    close(out, ref)
+    close(rmd, bn.running_mean)
+    close(rvd, bn.running_var)
+    dout = torch.randn(G, M, C)
+    loss = sum((o.permute(0, 2, 3, 1).reshape(M, C) * dout[g].double()).sum()
+               for g, o in enumerate(refs))
+    loss.backward()
+    dy = torch.empty(G, M, C, device=dev)
+    dres = torch.empty(G, M, C, device=dev) if res else None
+    dg = torch.zeros(C, device=dev)
+    db = torch.zeros(C, device=dev)
+    ops.bn_bwd(yd, out, dout.to(dev), relu, mean, invstd, scale, G, M, C, ws, dy, dres, dg, db)
+    close(dy, torch.stack([x.grad.permute(0, 2, 3, 1).reshape(M, C) for x in xs]))
+    close(dg, bn.weight.grad)
+    close(db, bn.bias.grad)
+
+
+def test_pools():
+    from mauv import ops
+    N, H, C = 3, 9, 64
+    torch.manual_seed(4)
+    x = torch.randn(N, H, H, C)
+    x[0, :3, :3, :] = 0.0  # ties (post-ReLU zeros) exercise the first-max rule
+    Ho = ops.out_hw(H, 3, 2, 1)
+    y = torch.empty(N, Ho, Ho, C, device=dev)
+    idx = torch.empty(N, Ho, Ho, C, dtype=torch.uint8, device=dev)
+    ops.maxpool_fwd(x.to(dev), N, H, H, C, y, idx)
+    xr = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    close(y, yr.permute(0, 2, 3, 1))
+    dy = torch.randn(N, Ho, Ho, C)
+    yr.backward(dy.double().permute(0, 3, 1, 2))
+    dx = torch.empty(N, H, H, C, device=dev)
+    ops.maxpool_bwd(dy.to(dev), idx, N, H, H, C, dx)
+    close(dx, xr.grad.permute(0, 2, 3, 1))
+    a = torch.empty(N, C, device=dev)
+    ops.avgpool_fwd(x.to(dev), N, H * H, C, a)
+    close(a, x.double().mean((1, 2)))
+    da = torch.randn(N, C)
+    dxa = torch.empty(N, H, H, C, device=dev)
+    ops.avgpool_bwd(da.to(dev), N, H * H, C, dxa)
+    close(dxa, (da.double() / (H * H))[:, None, None, :].expand(N, H, H, C))
+
+
+def test_reparam_and_kl():
+    from mauv import ops
+    G, Cout, Cin, R = 3, 16, 8, 3
+    torch.manual_seed(5)
+    mu = torch.randn(Cout, Cin, R, R) * 0.1
+    rho = torch.log(torch.expm1(0.1 * mu.abs()) + 1e-20)
+    eps = torch.randn(G, Cout * Cin * R * R)
+    out = torch.empty(G, Cout, R, R, Cin, device=dev)
+    ops.reparam_sample(mu.to(dev), rho.to(dev), out, G, 0, 0, 0, Cout, Cin, R * R,
+                       eps=eps.to(dev))
+    sig = torch.log1p(torch.exp(rho.double()))
+    ref = (mu.double() + sig * eps.double().view(G, Cout, Cin, R, R)).permute(0, 1, 3, 4, 2)
+    close(out, ref)
+    # backward with explicit eps
+    dws = torch.randn(2, G, Cout, R, R, Cin)
+    dmu = torch.zeros(Cout, Cin, R, R, device=dev)
+    drho = torch.zeros_like(dmu)
+    ops.reparam_bwd(dws.to(dev), 2, mu.to(dev), rho.to(dev), dmu, drho, G, 0, 0, 0, Cout, Cin,
+                    R * R, eps=eps.to(dev))
+    dW = dws.double().sum(0).permute(0, 1, 4, 2, 3)  # [G][Cout][Cin][R][R]
+    close(dmu, dW.sum(0))
+    close(drho, (dW * eps.double().view(G, Cout, Cin, R, R)).sum(0) * torch.sigmoid(rho.double()))
+    # Philox path: G-batched sample == G sequential single-sample draws
+    outb = torch.empty(G, Cout, R, R, Cin, device=dev)
+    ops.reparam_sample(mu.to(dev), rho.to(dev), outb, G, 42, 10, 7, Cout, Cin, R * R)
+    for g in range(G):
+        o1 = torch.empty(1, Cout, R, R, Cin, device=dev)
+        ops.reparam_sample(mu.to(dev), rho.to(dev), o1, 1, 42, 10 + g, 7, Cout, Cin, R * R)
+        assert torch.equal(o1[0], outb[g])
+
+
+def test_philox_matches_oracle_restatement():
+    from mauv import ops
+    from oracle.philox_ref import philox4x32_10, normal4
+    raw, nrm = ops.philox_raw(0x1234_5678_9ABC, 77, 3, 1000)
+    ref_raw = philox4x32_10(np.arange(1000, dtype=np.uint64), 77, 3, 0x1234_5678_9ABC)
+    assert np.array_equal(raw.cpu().numpy().view(np.uint32).reshape(-1, 4), ref_raw)
+    np.testing.assert_allclose(nrm.cpu().numpy().reshape(-1, 4), normal4(ref_raw), atol=1e-4,
+                               rtol=1e-5)
+    z = nrm.cpu().double()
+    assert abs(z.mean()) < 0.05 and abs(z.std() - 1) < 0.05
+
+
+def test_head_kernels():
+    from mauv import ops
+    rows = 6
+    torch.manual_seed(6)
+    qkv = torch.randn(rows, 384)
+    s = torch.randn(rows, 128)
+    t = torch.empty(rows, 128, device=dev)
+    ops.attn_t(qkv.to(dev), rows, t)
+    close(t, torch.tanh(qkv[:, :128].double() + qkv[:, 128:256].double()))
+    comb = torch.zeros(rows, 384, device=dev)
+    ops.attn_out(qkv.to(dev), s.to(dev), rows, comb, 384, 128)
+    sr = s.double().requires_grad_(True)
+    vr = qkv[:, 256:].double().requires_grad_(True)
+    o = vr * torch.softmax(sr, 1)
+    close(comb[:, 128:256], o)
+    do = torch.randn(rows, 128)
+    o.backward(do.double())
+    dcomb = torch.zeros(rows, 384)
+    dcomb[:, 128:256] = do
+    dqkv = torch.zeros(rows, 384, device=dev)
+    ds = torch.empty(rows, 128, device=dev)
+    ops.attn_out_bwd(dcomb.to(dev), 384, 128, qkv.to(dev), s.to(dev), rows, dqkv, ds)
+    close(ds, sr.grad)
+    close(dqkv[:, 256:], vr.grad)
+    dt = torch.randn(rows, 128)
+    ops.attn_t_bwd(dt.to(dev), t, rows, dqkv)
+    tt = torch.tanh(qkv[:, :128].double() + qkv[:, 128:256].double())
+    close(dqkv[:, :128], dt.double() * (1 - tt * tt))
+    close(dqkv[:, 128:256], dt.double() * (1 - tt * tt))
+
+
+def test_mc_head_kernels():
+    from mauv import ops
+    G, B, C = 5, 9, 7
+    torch.manual_seed(7)
+    logits = torch.randn(G, B, C)
+    labels = torch.randint(0, C, (B,))
+    mean = torch.empty(B, C, device=dev)
+    loss = torch.empty(1, device=dev)
+    ops.mc_mean_ce(logits.to(dev), labels.to(dev), G, B, C, mean, loss)
+    lr = logits.double().requires_grad_(True)
+    m = lr.mean(0)
+    ce = F.cross_entropy(m, labels)
+    close(mean, m)
+    close(loss, ce.reshape(1))
+    ce.backward()
+    dl = torch.empty(G, B, C, device=dev)
+    g = torch.tensor([1.0], device=dev)
+    ops.mc_mean_bwd(None, g, mean, labels.to(dev), G, B, C, dl)
+    close(dl, lr.grad)
+    sums = torch.empty(B, 2 * C + 1, dtype=torch.float64, device=dev)
+    ops.mc_stats(logits.to(dev), G, B, C, 1e-7, sums)
+    mp = torch.empty(B, C, device=dev)
+    var = torch.empty(B, device=dev)
+    alea = torch.empty(B, device=dev)
+    pe = torch.empty(B, device=dev)
+    pred = torch.empty(B, dtype=torch.int64, device=dev)
+    ops.mc_finalize(sums, G, B, C, 1e-8, mp, var, alea, pe, pred)
+    P = torch.softmax(logits.double(), -1)
+    close(mp, P.mean(0))
+    close(var, torch.var(P, 0).mean(1))
+    close(alea, torch.mean(-torch.sum(P * torch.log(P + 1e-7), -1), 0))
+    close(pe, -torch.sum(P.mean(0) * torch.log(P.mean(0) + 1e-8), 1))
+    assert torch.equal(pred.cpu(), torch.argmax(P.mean(0), 1))
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    x = torch.randn(10000, device=dev)
+    ops.nonfinite_count(x, cnt)
+    assert cnt.item() == 0
+    x[777] = float("nan")
+    ops.nonfinite_count(x, cnt)
+    assert cnt.item() > 0
