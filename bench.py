@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark: tri-modal Bayesian MC training step (BASELINE.json configs[1]) on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (driver, one rank per GPU, RCCL)
+
+A step = one reference training batch (train/multimodal.py:104-146) of synthetic triplets
+already resident in HBM: num_mc=5 stochastic forwards (one batched launch per layer), KL,
+cross-entropy, backward, RCCL gradient all-reduce (N>1), NaN/Inf guard, Adam step.
+Workload per GPU: B=64 triplets, optical 3x224x224 ~N(0,1), bathy 3x256x256 ~U[0,1) with
+channel 2 = 0, SSS 1x256x256 ~U[0,1), 7 classes, fp32 (weak scaling: 64 per GPU).
+
+Also reported: MC inference (configs[3]: 100 passes over 256 triplets, MC-sharded across
+ranks), the roofline of the dominant kernel family (implicit-GEMM conv fwd/dgrad/wgrad,
+HIP-event timed inside this run), and the reference-semantics CPU path (oracle/, torch-CPU
+fp32, sequential MC loop) timed on a bounded sample on this host.
+"""
+import argparse
+import json
+import os
+import platform
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+import sys  # noqa: E402
+for _p in (REPO, os.path.join(REPO, "multimodal-auv_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "triplets/sec training + MC-samples/sec inference, 7-class BNN, 1/2/4/8 MI355X"
+FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md: f32-in MFMA = vector peak (spec)
+
+
+def synthetic_batch(B, S_opt, S_son, device, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(B, 3, S_opt, S_opt, generator=g)
+    bathy = torch.rand(B, 3, S_son, S_son, generator=g)
+    bathy[:, 2] = 0
+    sss = torch.rand(B, 1, S_son, S_son, generator=g)
+    y = torch.randint(0, 7, (B,), generator=g)
+    return [t.to(device) for t in (x, bathy, sss, y)]
+
+
+def cpu_baseline(args):
+    """Reference-semantics CPU path (oracle = torch-CPU restatement, sequential MC loop,
+    per-pass KL, torch Adam) on a bounded sample: B=2, num_mc=2 at full resolution, scaled
+    to the GPU workload's per-triplet cost (work is linear in num_mc)."""
+    from oracle.model_ref import define_models, DEFAULT_PRIOR
+    from oracle import loops_ref
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    model = define_models(None, 7, DEFAULT_PRIOR)["multimodal_model"]
+    opt = torch.optim.Adam(model.parameters(), lr=5e-5)
+    crit = torch.nn.CrossEntropyLoss()
+    Bc, Nc = 2, 2
+    x, b, s, y = synthetic_batch(Bc, args.optical, args.sonar, "cpu", 1)
+    loops_ref.train_step_multimodal(model, x, b, s, y, crit, opt, 0, 2, Nc, Bc)  # warm-up
+    t0 = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        loops_ref.train_step_multimodal(model, x, b, s, y, crit, opt, 0, 2, Nc, Bc)
+    dt = (time.perf_counter() - t0) / reps
+    per_triplet = dt / Bc * (args.num_mc / Nc)
+    return {"value": round(1.0 / per_triplet, 4), "unit": "triplets/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle train step, B={Bc}, num_mc={Nc} (scaled x{args.num_mc}/{Nc} to "
+                      f"num_mc={args.num_mc}), {args.optical}/{args.sonar} px, torch-CPU fp32, "
+                      f"{reps} timed steps of {dt:.2f} s",
+            "host": platform.processor() or platform.machine()}
+
+
+def roofline_step(step_fn):
+    from mauv import ops
+    ops.PROFILE = []
+    torch.cuda.synchronize()
+    step_fn()
+    torch.cuda.synchronize()
+    rows, ops.PROFILE = ops.PROFILE, None
+    by = {}
+    for kind, fl, e0, e1 in rows:
+        ms = e0.elapsed_time(e1)
+        d = by.setdefault(kind, [0, 0.0, 0.0])
+        d[0] += 1
+        d[1] += fl
+        d[2] += ms
+    tot_fl = sum(v[1] for v in by.values())
+    tot_ms = sum(v[2] for v in by.values())
+    n = sum(v[0] for v in by.values())
+    achieved = tot_fl / (tot_ms * 1e-3) / 1e12
+    return {
+        "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TF,
+        "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TF, 4), "traffic": None,
+        "kernel": "conv_gemm_f32 (implicit-GEMM fwd+dgrad+wgrad, all launches of one step)",
+        "launches": n, "avg_launch_us": round(tot_ms * 1e3 / max(n, 1), 2),
+        "algorithmic_gflop_per_launch": round(tot_fl / max(n, 1) / 1e9, 3),
+        "conv_ms_per_step": round(tot_ms, 2),
+        "breakdown": {k: {"launches": v[0], "gflop": round(v[1] / 1e9, 1),
+                          "ms": round(v[2], 2), "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 1)}
+                      for k, v in by.items()},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=64, help="triplets per GPU")
+    ap.add_argument("--num-mc", type=int, default=5)
+    ap.add_argument("--optical", type=int, default=224)
+    ap.add_argument("--sonar", type=int, default=256)
+    ap.add_argument("--infer-batch", type=int, default=256)
+    ap.add_argument("--infer-mc", type=int, default=100)
+    ap.add_argument("--no-infer", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from mauv.models import define_models, DEFAULT_PRIOR
+    from mauv.train import mc_train_step
+    from mauv.predict import mc_statistics
+
+    torch.manual_seed(0)
+    model = define_models(None, 7, DEFAULT_PRIOR)["multimodal_model"].to(dev)
+    if world > 1:
+        from mauv.ddp import DistributedMC
+        model = DistributedMC(model)
+    opt = torch.optim.Adam(model.parameters(), lr=5e-5)
+    crit = torch.nn.CrossEntropyLoss()
+    x, b, s, y = synthetic_batch(args.batch, args.optical, args.sonar, dev, 1234 + rank)
+    kl_w = 2.0 ** 1 / 2.0 ** 30   # epoch 0 of 30 (main.py:293)
+
+    def step():
+        return mc_train_step(model, (x, b, s), y, crit, opt, args.num_mc, args.batch, kl_w)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step()
+        if rank == 0 and args.steps > 3:
+            print(f"[bench] step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    triplets_s = args.batch * world * args.steps / dt
+    roof = None if args.no_roofline else roofline_step(step)
+
+    infer = None
+    if not args.no_infer:
+        opt.zero_grad(set_to_none=True)
+        xi, bi, si, _ = synthetic_batch(args.infer_batch, args.optical, args.sonar, dev, 99)
+        group = dist.group.WORLD if world > 1 else None
+        with torch.no_grad():
+            mc_statistics(model, xi, bi, si, max(world, 2), group=group)   # warm-up
+            barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            mc_statistics(model, xi, bi, si, args.infer_mc, group=group)
+            torch.cuda.synchronize()
+            barrier()
+            di = time.perf_counter() - t1
+        infer = {"value": round(args.infer_mc * args.infer_batch / di, 2), "unit": "MC-samples/s",
+                 "batch": args.infer_batch, "num_mc": args.infer_mc,
+                 "ms_per_batch": round(di * 1e3, 1), "sharding": "mc" if world > 1 else "none"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(triplets_s, 3), "unit": "triplets/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (random-init weights, MOPED rho; inputs resident in HBM)",
+            "config": {"workload": "configs[1]: tri-modal BNN training step, 7 classes, "
+                                   f"B={args.batch}/GPU fp32, num_mc={args.num_mc}, optical "
+                                   f"{args.optical}px + bathy/SSS {args.sonar}px",
+                       "global_batch": args.batch * world, "num_mc": args.num_mc,
+                       "parallelism": f"dp{world}"},
+            "inference": infer, "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

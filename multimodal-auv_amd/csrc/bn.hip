@@ -97,43 +97,60 @@ __global__ __launch_bounds__(256) void bn_stats_partial(const float* __restrict_
   }
 }
 
-// Stage 2: per channel, merge blocks (double), then the G running-stat updates in order.
-__global__ void bn_stats_final(int G, int nblk, int C, const float* __restrict__ pmean,
-                               const float* __restrict__ pm2, const float* __restrict__ pcnt,
-                               const float* __restrict__ gamma, const float* __restrict__ beta,
-                               float* __restrict__ run_mean, float* __restrict__ run_var,
-                               float momentum, float eps, float* __restrict__ mean_out,
-                               float* __restrict__ invstd_out, float* __restrict__ scale_out,
-                               float* __restrict__ shift_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float rmean = run_mean ? run_mean[c] : 0.f, rvar = run_var ? run_var[c] : 0.f;
-  for (int g = 0; g < G; ++g) {
-    double nn = 0.0, mu = 0.0, mm = 0.0;
-    for (int b = 0; b < nblk; ++b) {
-      const double nb = pcnt[(long long)g * nblk + b];
-      if (nb == 0.0) continue;
+__device__ __forceinline__ void chan_merge(double& nn, double& mu, double& mm, double nb,
+                                           double mb, double m2b) {
+  if (nb == 0.0) return;
+  const double nt = nn + nb, d = mb - mu;
+  mu += d * (nb / nt);
+  mm += m2b + d * d * (nn * nb / nt);
+  nn = nt;
+}
+
+// Stage 2: grid (C/64, G); 64 channels x 4 lanes per block, each lane Chan-merging a strided
+// quarter of the block partials in double, then a 4-way merge in LDS.
+__global__ __launch_bounds__(256) void bn_stats_final(
+    int G, int nblk, int C, const float* __restrict__ pmean, const float* __restrict__ pm2,
+    const float* __restrict__ pcnt, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float* __restrict__ mean_out,
+    float* __restrict__ invstd_out, float* __restrict__ scale_out,
+    float* __restrict__ shift_out, float* __restrict__ uvar_out) {
+  const int g = blockIdx.y, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  double nn = 0.0, mu = 0.0, mm = 0.0;
+  if (c < C) {
+    for (int b = ty; b < nblk; b += 4) {
       const long long o = ((long long)g * nblk + b) * C + c;
-      const double mb = pmean[o], m2b = pm2[o];
-      const double nt = nn + nb, d = mb - mu;
-      mu += d * (nb / nt);
-      mm += m2b + d * d * (nn * nb / nt);
-      nn = nt;
-    }
-    const double var = mm / nn;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float sc = gamma[c] * invstd;
-    mean_out[g * C + c] = (float)mu;
-    invstd_out[g * C + c] = invstd;
-    scale_out[g * C + c] = sc;
-    shift_out[g * C + c] = beta[c] - (float)mu * sc;
-    if (run_mean) {
-      const double uvar = nn > 1.0 ? mm / (nn - 1.0) : var;
-      rmean = (1.f - momentum) * rmean + momentum * (float)mu;
-      rvar = (1.f - momentum) * rvar + momentum * (float)uvar;
+      chan_merge(nn, mu, mm, pcnt[(long long)g * nblk + b], pmean[o], pm2[o]);
     }
   }
-  if (run_mean) { run_mean[c] = rmean; run_var[c] = rvar; }
+  __shared__ double sn[4][64], smu[4][64], smm[4][64];
+  sn[ty][tx] = nn; smu[ty][tx] = mu; smm[ty][tx] = mm;
+  __syncthreads();
+  if (ty != 0 || c >= C) return;
+  for (int k = 1; k < 4; ++k) chan_merge(nn, mu, mm, sn[k][tx], smu[k][tx], smm[k][tx]);
+  const double var = mm / nn;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * invstd;
+  mean_out[g * C + c] = (float)mu;
+  invstd_out[g * C + c] = invstd;
+  scale_out[g * C + c] = sc;
+  shift_out[g * C + c] = beta[c] - (float)mu * sc;
+  uvar_out[g * C + c] = (float)(nn > 1.0 ? mm / (nn - 1.0) : var);
+}
+
+// Stage 3: the G running-stat updates, in MC-sample order (= G sequential forward calls).
+__global__ void bn_running_kernel(int G, int C, const float* __restrict__ mean,
+                                  const float* __restrict__ uvar, float* __restrict__ run_mean,
+                                  float* __restrict__ run_var, float momentum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float rm = run_mean[c], rv = run_var[c];
+  for (int g = 0; g < G; ++g) {
+    rm = (1.f - momentum) * rm + momentum * mean[g * C + c];
+    rv = (1.f - momentum) * rv + momentum * uvar[g * C + c];
+  }
+  run_mean[c] = rm;
+  run_var[c] = rv;
 }
 
 // out = [relu]( y * scale[g][c] + shift[g][c] (+ res) )
@@ -230,28 +247,43 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ 
   }
 }
 
-// Backward stage 2: k1 = sum dz / M, k2 = sum dz*xhat / M per (g,c); dgamma/dbeta += over g.
-__global__ void bn_bwd_final(int G, int nblk, int C, long long M, const float* __restrict__ p1,
-                             const float* __restrict__ p2, float* __restrict__ k1,
-                             float* __restrict__ k2, float* __restrict__ dgamma,
-                             float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double tg = 0.0, tb = 0.0;
-  for (int g = 0; g < G; ++g) {
-    double a = 0.0, b = 0.0;
-    for (int k = 0; k < nblk; ++k) {
+// Backward stage 2: grid (C/64, G), 64 channels x 4 lanes: k1 = sum dz / M, k2 = sum
+// dz*xhat / M per (g,c) (double sums, fixed order).
+__global__ __launch_bounds__(256) void bn_bwd_final(int G, int nblk, int C, long long M,
+                                                    const float* __restrict__ p1,
+                                                    const float* __restrict__ p2,
+                                                    float* __restrict__ k1,
+                                                    float* __restrict__ k2) {
+  const int g = blockIdx.y, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int k = ty; k < nblk; k += 4) {
       const long long o = ((long long)g * nblk + k) * C + c;
       a += p1[o];
       b += p2[o];
     }
-    k1[g * C + c] = (float)(a / (double)M);
-    k2[g * C + c] = (float)(b / (double)M);
-    tb += a;
-    tg += b;
   }
-  if (dgamma) dgamma[c] += (float)tg;
-  if (dbeta) dbeta[c] += (float)tb;
+  __shared__ double sa[4][64], sb[4][64];
+  sa[ty][tx] = a; sb[ty][tx] = b;
+  __syncthreads();
+  if (ty != 0 || c >= C) return;
+  a = sa[0][tx] + sa[1][tx] + sa[2][tx] + sa[3][tx];
+  b = sb[0][tx] + sb[1][tx] + sb[2][tx] + sb[3][tx];
+  k1[g * C + c] = (float)(a / (double)M);
+  k2[g * C + c] = (float)(b / (double)M);
+}
+
+// Backward stage 3: dgamma += M * sum_g k2, dbeta += M * sum_g k1 (sample order).
+__global__ void bn_bwd_param_kernel(int G, int C, long long M, const float* __restrict__ k1,
+                                    const float* __restrict__ k2, float* __restrict__ dgamma,
+                                    float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double tg = 0.0, tb = 0.0;
+  for (int g = 0; g < G; ++g) { tb += k1[g * C + c]; tg += k2[g * C + c]; }
+  if (dgamma) dgamma[c] += (float)(tg * (double)M);
+  if (dbeta) dbeta[c] += (float)(tb * (double)M);
 }
 
 // dy = gamma*invstd * (dz - k1 - xhat*k2); dres = dz (optional)
@@ -306,13 +338,35 @@ static int ew_grid(long long n4) {
   return (int)(b < 1 ? 1 : b);
 }
 
+// eval-mode BN (running statistics): per-group copies of scale/shift
+__global__ void bn_eval_params_kernel(int G, int C, const float* __restrict__ gamma,
+                                      const float* __restrict__ beta,
+                                      const float* __restrict__ rm, const float* __restrict__ rv,
+                                      float eps, float* __restrict__ scale,
+                                      float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float sc = gamma[c] / sqrtf(rv[c] + eps);
+  const float sh = beta[c] - rm[c] * sc;
+  for (int g = 0; g < G; ++g) { scale[g * C + c] = sc; shift[g * C + c] = sh; }
+}
+
 }  // namespace mauv
+
+// Eval-mode BN parameters (module.eval()): scale = gamma/sqrt(rv+eps), shift = beta - rm*scale.
+MAUV_API int mauv_bn_eval_params(int G, int C, const float* gamma, const float* beta,
+                                 const float* run_mean, const float* run_var, float eps,
+                                 float* scale, float* shift, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_eval_params_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
+                     gamma, beta, run_mean, run_var, eps, scale, shift);
+  return check_launch("bn_eval_params");
+}
 
 // Workspace floats needed by mauv_bn_fwd_train / mauv_bn_bwd for (G, M, C).
 MAUV_API long long mauv_bn_workspace_floats(int G, long long M, int C) {
   int nblk, rpb;
   reduce_geometry(M, C, nblk, rpb);
-  return (long long)G * nblk * (2LL * C + 1) + 2LL * G * C;
+  return (long long)G * nblk * (2LL * C + 1) + 3LL * G * C;
 }
 
 // Training-mode BN forward for G groups: statistics (mean/invstd/scale/shift out, [G][C]),
@@ -331,9 +385,12 @@ MAUV_API int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const 
   float* pcnt = pm2 + (long long)G * nblk * C;
   hipLaunchKernelGGL(bn_stats_partial, dim3(nblk, G), dim3(256), 0, stream, y, M, C, rpb, rm,
                      pmean, pm2, pcnt);
-  hipLaunchKernelGGL(bn_stats_final, dim3((C + 255) / 256), dim3(256), 0, stream, G, nblk, C,
-                     pmean, pm2, pcnt, gamma, beta, run_mean, run_var, momentum, eps, mean,
-                     invstd, scale, shift);
+  float* uvar = pcnt + (long long)G * nblk;
+  hipLaunchKernelGGL(bn_stats_final, dim3((C + 63) / 64, G), dim3(256), 0, stream, G, nblk, C,
+                     pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift, uvar);
+  if (run_mean && run_var)
+    hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
+                       mean, uvar, run_mean, run_var, momentum);
   if (out) {
     hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C / 4 / 1), G), dim3(256), 0, stream,
                        y, scale, shift, res, relu, out, M, C);
@@ -367,8 +424,11 @@ MAUV_API int mauv_bn_bwd(const float* y, const float* out, const float* dout, in
   float* k2 = k1 + (long long)G * C;
   hipLaunchKernelGGL(bn_bwd_partial, dim3(nblk, G), dim3(256), 0, stream, y, out, dout, relu,
                      mean, invstd, M, C, rpb, rm, p1, p2);
-  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 255) / 256), dim3(256), 0, stream, G, nblk, C, M,
-                     p1, p2, k1, k2, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(256), 0, stream, G, nblk, C, M,
+                     p1, p2, k1, k2);
+  if (dgamma || dbeta)
+    hipLaunchKernelGGL(bn_bwd_param_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C, M,
+                       k1, k2, dgamma, dbeta);
   hipLaunchKernelGGL(bn_bwd_apply, dim3(ew_grid(M * C / 4), G), dim3(256), 0, stream, y, out,
                      dout, relu, mean, invstd, scale, k1, k2, dy, dres, M, C);
   return check_launch("bn_bwd");

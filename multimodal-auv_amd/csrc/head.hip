@@ -108,18 +108,21 @@ __global__ __launch_bounds__(256) void mc_mean_ce_kernel(const float* __restrict
                                                          const long long* __restrict__ labels,
                                                          int G, int B, int C,
                                                          float* __restrict__ mean,
-                                                         float* __restrict__ loss) {
+                                                         float* __restrict__ loss,
+                                                         long long* __restrict__ pred) {
   __shared__ float red[256];
   float acc = 0.f;
   for (int b = threadIdx.x; b < B; b += 256) {
     float m = -INFINITY;
+    int arg = 0;
     for (int c = 0; c < C; ++c) {
       float s = 0.f;
       for (int g = 0; g < G; ++g) s += logits[((long long)g * B + b) * C + c];
       s = s / (float)G;
       mean[(long long)b * C + c] = s;
-      m = fmaxf(m, s);
+      if (s > m) { m = s; arg = c; }
     }
+    if (pred) pred[b] = arg;
     if (labels) {
       float se = 0.f;
       for (int c = 0; c < C; ++c) se += expf(mean[(long long)b * C + c] - m);
@@ -264,10 +267,12 @@ MAUV_API int mauv_colsum(const float* dy, int G, int rows, int N, float* out, in
   hipLaunchKernelGGL(colsum_kernel, dim3(grid1((long long)G * N)), dim3(256), 0, stream, dy, G, rows, N, out, accumulate);
   return check_launch("colsum");
 }
+// mean over MC samples of logits (train/multimodal.py:121), cross-entropy against int64
+// labels (:127, nullable) and argmax of the mean (torch.max(output, 1), :151; nullable).
 MAUV_API int mauv_mc_mean_ce(const float* logits, const long long* labels, int G, int B, int C,
-                             float* mean, float* loss, hipStream_t stream) {
+                             float* mean, float* loss, long long* pred, hipStream_t stream) {
   if (C > 32) { set_error("mc_mean_ce: C > 32"); return kErrArg; }
-  hipLaunchKernelGGL(mc_mean_ce_kernel, dim3(1), dim3(256), 0, stream, logits, labels, G, B, C, mean, loss);
+  hipLaunchKernelGGL(mc_mean_ce_kernel, dim3(1), dim3(256), 0, stream, logits, labels, G, B, C, mean, loss, pred);
   return check_launch("mc_mean_ce");
 }
 MAUV_API int mauv_mc_mean_bwd(const float* dmean, const float* gloss, const float* mean,

@@ -32,7 +32,7 @@ namespace mauv {
 __global__ __launch_bounds__(256) void reparam_sample_kernel(
     const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
     uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS,
-    float* __restrict__ out) {
+    float* __restrict__ out, long long out_gs) {
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
   for (long long q = blockIdx.x * 256LL + threadIdx.x; q < nq; q += (long long)gridDim.x * 256) {
@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void reparam_sample_kernel(
       } else {
         ep = normal4(seed, sample0 + g, layer, (uint32_t)q);
       }
-      float* og = out + (long long)g * numel;
+      float* og = out + (long long)g * out_gs;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         if (dst[e] >= 0) og[dst[e]] = m[e] + s[e] * ep[e];
@@ -69,10 +69,11 @@ __global__ __launch_bounds__(256) void reparam_sample_kernel(
 }
 
 __global__ __launch_bounds__(256) void reparam_bwd_kernel(
-    const float* __restrict__ dw, int splits, const float* __restrict__ mu,
+    const float* __restrict__ dw, int splits, long long dw_gs, long long dw_ss,
+    const float* __restrict__ mu,
     const float* __restrict__ rho, const float* __restrict__ eps, uint64_t seed,
     uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS,
-    float* __restrict__ dmu, float* __restrict__ drho) {
+    float* __restrict__ dmu, float* __restrict__ drho, long long fixed) {
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
   for (long long q = blockIdx.x * 256LL + threadIdx.x; q < nq; q += (long long)gridDim.x * 256) {
@@ -91,19 +92,30 @@ __global__ __launch_bounds__(256) void reparam_bwd_kernel(
         sg[e] = 0.f; src[e] = -1;
       }
     }
-    for (int g = 0; g < G; ++g) {
-      floatx4 ep;
+    floatx4 efix = {0.f, 0.f, 0.f, 0.f};
+    if (fixed >= 0) {  // reference mode: one epsilon (the last drawn sample) for every g
       if (eps) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ep[e] = src[e] >= 0 ? eps[(long long)g * numel + 4 * q + e] : 0.f;
+        for (int e = 0; e < 4; ++e) efix[e] = src[e] >= 0 ? eps[fixed * numel + 4 * q + e] : 0.f;
       } else {
-        ep = normal4(seed, sample0 + g, layer, (uint32_t)q);
+        efix = normal4(seed, sample0 + fixed, layer, (uint32_t)q);
+      }
+    }
+    for (int g = 0; g < G; ++g) {
+      floatx4 ep = efix;
+      if (fixed < 0) {
+        if (eps) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ep[e] = src[e] >= 0 ? eps[(long long)g * numel + 4 * q + e] : 0.f;
+        } else {
+          ep = normal4(seed, sample0 + g, layer, (uint32_t)q);
+        }
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         if (src[e] < 0) continue;
         float d = 0.f;
-        for (int s = 0; s < splits; ++s) d += dw[((long long)s * G + g) * numel + src[e]];
+        for (int s = 0; s < splits; ++s) d += dw[s * dw_ss + g * dw_gs + src[e]];
         gm[e] += d;
         gr[e] += d * ep[e];
       }
@@ -187,24 +199,40 @@ static int grid_for(long long nq) {
 
 // Sample G weight sets: out[g] (KRSC) = mu + softplus(rho) * eps_g.  mu/rho in OIHW
 // [Cout][Cin][R*S] (linear: [out][in], R*S = 1; bias: Cout = n, Cin = RS = 1).
+// out_gstride: element stride between groups (0 = numel; lets several layers share one
+// concatenated weight buffer, e.g. the attention q|k|v projection).
 MAUV_API int mauv_reparam_sample(const float* mu, const float* rho, const float* eps,
                                  unsigned long long seed, unsigned long long sample0,
                                  unsigned int layer, int G, int Cout, int Cin, int RS,
-                                 float* out, hipStream_t stream) {
-  const long long nq = ((long long)Cout * Cin * RS + 3) / 4;
+                                 float* out, long long out_gstride, hipStream_t stream) {
+  const long long numel = (long long)Cout * Cin * RS;
+  const long long nq = (numel + 3) / 4;
   hipLaunchKernelGGL(reparam_sample_kernel, dim3(grid_for(nq)), dim3(256), 0, stream, mu, rho,
-                     eps, seed, sample0, layer, G, Cout, Cin, RS, out);
+                     eps, seed, sample0, layer, G, Cout, Cin, RS, out,
+                     out_gstride ? out_gstride : numel);
   return check_launch("reparam_sample");
 }
 
-// dmu += sum_g sum_s dw[s][g];  drho += sum_g (sum_s dw[s][g]) * eps_g * sigmoid(rho).
-MAUV_API int mauv_reparam_bwd(const float* dw, int splits, const float* mu, const float* rho,
+// dmu += sum_g sum_s dw[s][g];  drho += sum_g (sum_s dw[s][g]) * eps_g' * sigmoid(rho), where
+// g' = g (exact reparameterisation gradient, fixed_sample < 0) or g' = fixed_sample - sample0
+// for every g (fixed_sample >= 0: bayesian-torch 0.5.0 semantics — its forward does
+// `eps = self.eps_kernel.data.normal_()`, so when several MC forwards precede one backward
+// autograd's saved eps aliases the buffer and every pass's rho-gradient sees the LAST draw).
+// dw element (s, g, i) at dw[s*dw_sstride + g*dw_gstride + i] (strides 0 = dense
+// [splits][G][numel]); i in the KRSC weight layout.
+MAUV_API int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride,
+                              long long dw_sstride, const float* mu, const float* rho,
                               const float* eps, unsigned long long seed,
                               unsigned long long sample0, unsigned int layer, int G, int Cout,
-                              int Cin, int RS, float* dmu, float* drho, hipStream_t stream) {
-  const long long nq = ((long long)Cout * Cin * RS + 3) / 4;
+                              int Cin, int RS, float* dmu, float* drho,
+                              long long fixed_sample, hipStream_t stream) {
+  const long long numel = (long long)Cout * Cin * RS;
+  const long long nq = (numel + 3) / 4;
+  const long long gs = dw_gstride ? dw_gstride : numel;
+  const long long ss = dw_sstride ? dw_sstride : gs * G;
   hipLaunchKernelGGL(reparam_bwd_kernel, dim3(grid_for(nq)), dim3(256), 0, stream, dw, splits,
-                     mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS, dmu, drho);
+                     gs, ss, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS, dmu, drho,
+                     fixed_sample >= 0 ? (long long)(fixed_sample - (long long)sample0) : -1LL);
   return check_launch("reparam_bwd");
 }
 

@@ -30,8 +30,8 @@ SIGNATURES = {
     "mauv_conv2d_wgrad_splits": [I, I, I, I, I, I, I, I, I, I],
     "mauv_conv2d_bwd_weight_f32": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
     # reparam.hip
-    "mauv_reparam_sample": [P, P, P, U64, U64, U32, I, I, I, I, P, P],
-    "mauv_reparam_bwd": [P, I, P, P, P, U64, U64, U32, I, I, I, I, P, P, P],
+    "mauv_reparam_sample": [P, P, P, U64, U64, U32, I, I, I, I, P, LL, P],
+    "mauv_reparam_bwd": [P, I, LL, LL, P, P, P, U64, U64, U32, I, I, I, I, P, P, LL, P],
     "mauv_kl_workspace_bytes": [I],
     "mauv_kl_fwd": [P, I, P, F, P, P],
     "mauv_kl_bwd": [P, I, P, F, P],
@@ -40,6 +40,7 @@ SIGNATURES = {
     "mauv_bn_workspace_floats": [I, LL, I],
     "mauv_bn_fwd_train": [P, I, LL, I, P, P, P, P, F, F, P, P, P, P, P, P, I, P, P],
     "mauv_bn_apply": [P, P, P, P, I, P, I, LL, I, P],
+    "mauv_bn_eval_params": [I, I, P, P, P, P, F, P, P, P],
     "mauv_bn_bwd": [P, P, P, I, P, P, P, I, LL, I, P, P, P, P, P, P],
     # pool.hip
     "mauv_maxpool_fwd": [P, I, I, I, I, P, P, P],
@@ -52,7 +53,7 @@ SIGNATURES = {
     "mauv_attn_out": [P, P, I, P, I, I, P],
     "mauv_attn_out_bwd": [P, I, I, P, P, I, P, P, P],
     "mauv_colsum": [P, I, I, I, P, I, P],
-    "mauv_mc_mean_ce": [P, P, I, I, I, P, P, P],
+    "mauv_mc_mean_ce": [P, P, I, I, I, P, P, P, P],
     "mauv_mc_mean_bwd": [P, P, P, P, I, I, I, P, P],
     "mauv_mc_stats": [P, I, I, I, F, P, I, P],
     "mauv_mc_finalize": [P, I, I, I, F, P, P, P, P, P, P],

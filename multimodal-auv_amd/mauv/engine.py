@@ -1,0 +1,500 @@
+"""MC-batched execution engine: compiles the tri-modal Bayesian model into HIP launches.
+
+What the reference does (train/multimodal.py:107-118, inference/predictors.py:54-65):
+``for _ in range(num_mc): model(inputs, bathy, sss)`` — N sequential stochastic forwards, each
+re-sampling every Bayesian weight (bayesian-torch ``eps.normal_()``) and each running
+BatchNorm in training mode on its own batch statistics, then one ``loss.backward()`` through
+the N graphs.
+
+What this engine does: one pass over the network in which every layer is ONE launch for all
+N samples (G = N groups on blockIdx.z of the implicit-GEMM kernels), with per-group weights
+``W_g = mu + softplus(rho) * eps_g`` (eps_g regenerated from Philox in the backward instead of
+stored), per-group BN statistics and sequential running-stat updates, and a hand-scheduled
+backward that writes dmu/drho/dgamma/dbeta straight into a flat gradient arena (one buffer
+per model, so the data-parallel all-reduce is a single bucketed RCCL call).
+
+Activations are NHWC ``[G][B][H][W][C]`` fp32.  The stems read the caller's NCHW images in
+place (strided loads, group stride 0 = image shared by all MC samples).
+"""
+import torch
+
+from . import ops
+from .layers import is_bayesian, LinearReparameterization
+
+
+# ----------------------------------------------------------------------------- root state
+class GradArena:
+    """Flat fp32 gradient buffer; every ``p.grad`` is a view into it."""
+
+    def __init__(self, params, device):
+        self.params = [p for p in params if p.requires_grad]
+        self.numel = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(self.numel, device=device)
+        self.views, off = [], 0
+        for p in self.params:
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+
+    def ensure(self):
+        ptrs_none = [p.grad is None for p in self.params]
+        if all(ptrs_none):
+            self.flat.zero_()
+            for p, v in zip(self.params, self.views):
+                p.grad = v
+            return
+        for p, v, none in zip(self.params, self.views, ptrs_none):
+            if none:
+                v.zero_()
+                p.grad = v
+            elif p.grad.data_ptr() != v.data_ptr():
+                v.copy_(p.grad)
+                p.grad = v
+
+
+class RootState:
+    """Per-model engine state: Philox layer ids, the MC sample counter, the grad arena."""
+
+    def __init__(self, root):
+        self.ids = {}
+        for m in root.modules():
+            if is_bayesian(m):
+                self.ids[id(m)] = len(self.ids)
+        self.params = list(root.parameters())
+        self.seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self.offset = 0
+        self.arena = None
+        self.eps_provider = None  # tests: fn(module, name, G) -> [G, numel] tensor or None
+        self.anchor = torch.zeros((), requires_grad=True)
+        # "reference": bayesian-torch 0.5.0 rho-gradient (every MC pass sees the epsilon of
+        # the LAST forward before backward — its eps buffer is overwritten in place while
+        # autograd still references it); "exact": per-sample reparameterisation gradient.
+        self.rho_grad = "reference"
+
+    def layer_id(self, m, bias=False):
+        return 2 * self.ids[id(m)] + int(bias)
+
+    def next_samples(self, G):
+        s = self.offset
+        self.offset += G
+        return s
+
+    def grads(self, device):
+        if self.arena is None or self.arena.flat.device != device:
+            self.arena = GradArena(self.params, device)
+        self.arena.ensure()
+        return self.arena
+
+
+def root_state(root):
+    st = root.__dict__.get("_mauv_state")
+    if st is None:
+        st = RootState(root)
+        root.__dict__["_mauv_state"] = st
+    return st
+
+
+def invalidate(root):
+    root.__dict__.pop("_mauv_state", None)
+
+
+def set_rho_grad_mode(root, mode):
+    """"reference" (default; bayesian-torch 0.5.0 behaviour) or "exact"."""
+    assert mode in ("reference", "exact")
+    root_state(root).rho_grad = mode
+
+
+def needs_grad(params):
+    return torch.is_grad_enabled() and any(p.requires_grad for p in params)
+
+
+class _Engine(torch.autograd.Function):
+    """Autograd node around a runner: forward = the HIP schedule; backward = the reverse
+    HIP schedule, which writes parameter gradients into the arena directly."""
+
+    @staticmethod
+    def forward(ctx, runner, anchor, *inputs):
+        ctx.runner = runner
+        return runner.run_forward(*inputs)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, *grads):
+        runner, ctx.runner = ctx.runner, None
+        gins = runner.run_backward(*grads)
+        return (None, None) + tuple(gins)
+
+
+# ----------------------------------------------------------------------------- base runner
+class _Runner:
+    def __init__(self, state, G, sample0, save):
+        self.st, self.G, self.s0, self.save = state, G, sample0, save
+
+    def _eps(self, m, name):
+        fn = self.st.eps_provider
+        return None if fn is None else fn(m, name, self.G)
+
+    # ---- Bayesian parameter sampling (mauv_reparam_sample) ----
+    def _sample(self, m, mu, rho, name, out, Cout, Cin, RS, bias=False, out_gstride=0):
+        ops.reparam_sample(mu, rho, out, self.G, self.st.seed, self.s0,
+                           self.st.layer_id(m, bias), Cout, Cin, RS, eps=self._eps(m, name),
+                           out_gstride=out_gstride)
+
+    def _reparam_bwd(self, m, mu, rho, dw, splits, Cout, Cin, RS, name, bias=False,
+                     dw_gstride=0, dw_sstride=0):
+        if not mu.requires_grad:
+            return
+        fixed = self.st.offset - 1 if self.st.rho_grad == "reference" else -1
+        ops.reparam_bwd(dw, splits, mu, rho, mu.grad, rho.grad, self.G, self.st.seed, self.s0,
+                        self.st.layer_id(m, bias), Cout, Cin, RS, eps=self._eps(m, name),
+                        dw_gstride=dw_gstride, dw_sstride=dw_sstride, fixed_sample=fixed)
+
+    # ---- linear = 1x1 conv on [G][rows][K] ----
+    def _linear(self, lin, x, rows):
+        G, N, K = self.G, lin.out_features, lin.in_features
+        w = torch.empty(G, N, K, device=x.device)
+        self._sample(lin, lin.mu_weight, lin.rho_weight, "weight", w, N, K, 1)
+        b = None
+        if lin.mu_bias is not None:
+            b = torch.empty(G, N, device=x.device)
+            self._sample(lin, lin.mu_bias, lin.rho_bias, "bias", b, N, 1, 1, bias=True)
+        y = torch.empty(G, rows, N, device=x.device)
+        ops.conv2d_fwd(x, w, y, G, rows, 1, 1, K, N, 1, 1, 0, bias=b)
+        return y, (lin, x, w, rows)
+
+    def _linear_bwd(self, rec, dy, need_dx=True):
+        lin, x, w, rows = rec
+        G, N, K = self.G, lin.out_features, lin.in_features
+        if lin.mu_weight.requires_grad:
+            splits = ops.wgrad_splits(G, rows, 1, 1, K, N, 1, 1, 0)
+            ws = torch.empty(splits, G, N, K, device=dy.device)
+            ops.conv2d_bwd_weight(x, dy, ws, splits, G, rows, 1, 1, K, N, 1, 1, 0)
+            self._reparam_bwd(lin, lin.mu_weight, lin.rho_weight, ws, splits, N, K, 1, "weight")
+        if lin.mu_bias is not None and lin.mu_bias.requires_grad:
+            db = torch.empty(G, N, device=dy.device)
+            ops.colsum(dy, G, rows, N, db)
+            self._reparam_bwd(lin, lin.mu_bias, lin.rho_bias, db, 1, N, 1, 1, "bias", bias=True)
+        if not need_dx:
+            return None
+        dx = torch.empty(G, rows, K, device=dy.device)
+        ops.conv2d_bwd_data(dy, w, dx, G, rows, 1, 1, K, N, 1, 1, 0)
+        return dx
+
+
+# ----------------------------------------------------------------------------- trunk
+class TrunkRunner(_Runner):
+    """torchvision ResNet-50 trunk (Bayesian convs, train-mode BN) for G MC samples."""
+
+    def __init__(self, trunk, state, G, sample0, save):
+        super().__init__(state, G, sample0, save)
+        self.trunk = trunk
+
+    # ---- conv / bn units ----
+    def _conv(self, conv, x, B, H, W, x_strides=None):
+        G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
+        st, pd = conv.stride[0], conv.padding[0]
+        w = torch.empty(G, Cout, k, k, Cin, device=x.device)
+        self._sample(conv, conv.mu_kernel, conv.rho_kernel, "kernel", w, Cout, Cin, k * k)
+        Ho, Wo = ops.out_hw(H, k, st, pd), ops.out_hw(W, k, st, pd)
+        y = torch.empty(G, B, Ho, Wo, Cout, device=x.device)
+        ops.conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, k, st, pd, x_strides=x_strides)
+        rec = (conv, x, x_strides, w, B, H, W) if self.save else None
+        return y, rec
+
+    def _conv_bwd(self, rec, dy, need_dx=True, addend=None, dx=None, accumulate=False):
+        conv, x, xs, w, B, H, W = rec
+        G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
+        st, pd = conv.stride[0], conv.padding[0]
+        if conv.mu_kernel.requires_grad:
+            splits = ops.wgrad_splits(G, B, H, W, Cin, Cout, k, st, pd)
+            ws = torch.empty(splits, G, Cout, k * k * Cin, device=dy.device)
+            ops.conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, k, st, pd,
+                                  x_strides=xs)
+            self._reparam_bwd(conv, conv.mu_kernel, conv.rho_kernel, ws, splits, Cout, Cin,
+                              k * k, "kernel")
+            del ws
+        if not need_dx:
+            return None
+        if dx is None:
+            dx = torch.empty(G, B, H, W, Cin, device=dy.device)
+        ops.conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, k, st, pd, addend=addend,
+                            accumulate=accumulate)
+        return dx
+
+    def _bn(self, bn, y, relu, res=None):
+        G, C = self.G, y.shape[-1]
+        M = y.numel() // (G * C)
+        out = torch.empty_like(y)
+        stats = torch.empty(4, G, C, device=y.device)
+        mean, invstd, scale, shift = stats[0], stats[1], stats[2], stats[3]
+        if bn.training or not bn.track_running_stats:
+            if bn.momentum is None:
+                raise NotImplementedError("mauv: cumulative-average BN (momentum=None)")
+            ws = torch.empty(ops.bn_workspace_floats(G, M, C), device=y.device)
+            track = bn.training and bn.track_running_stats
+            ops.bn_fwd_train(y, G, M, C, bn.weight, bn.bias,
+                             bn.running_mean if track else None,
+                             bn.running_var if track else None, bn.momentum, bn.eps, ws, mean,
+                             invstd, scale, shift, res, relu, out)
+            if track:
+                bn.num_batches_tracked.add_(G)
+            batch_stats = True
+        else:
+            ops.bn_eval_params(G, C, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                               bn.eps, scale, shift)
+            ops.bn_apply(y, scale, shift, res, relu, out, G, M, C)
+            batch_stats = False
+        rec = (bn, y, out, stats, relu, M, C, batch_stats) if self.save else None
+        return out, rec
+
+    def _bn_bwd(self, rec, dout, want_dres=False):
+        bn, y, out, stats, relu, M, C, batch_stats = rec
+        if not batch_stats:
+            raise NotImplementedError("mauv: backward through eval-mode BN is not on the path "
+                                      "(the reference trains and predicts in .train())")
+        G = self.G
+        dy = torch.empty_like(y)
+        dres = torch.empty_like(y) if want_dres else None
+        ws = torch.empty(ops.bn_workspace_floats(G, M, C), device=y.device)
+        dg = bn.weight.grad if bn.weight.requires_grad else None
+        db = bn.bias.grad if bn.bias.requires_grad else None
+        ops.bn_bwd(y, out, dout, relu, stats[0], stats[1], stats[2], G, M, C, ws, dy, dres, dg,
+                   db)
+        return dy, dres
+
+    # ---- schedule ----
+    def run_forward(self, x):
+        t, G = self.trunk, self.G
+        x = x.contiguous()
+        if x.dtype != torch.float32:
+            x = x.float()
+        B, Cin, H, W = x.shape
+        if Cin != t.conv1.in_channels:
+            raise ValueError(f"trunk expects {t.conv1.in_channels} input channels, got {Cin}")
+        self.B = B
+        recs = self.recs = []
+        y, rc = self._conv(t.conv1, x, B, H, W, x_strides=(0, Cin * H * W, W, 1, H * W))
+        a, rb = self._bn(t.bn1, y, relu=True)
+        del y
+        H, W = a.shape[2], a.shape[3]
+        Hp, Wp = ops.out_hw(H, 3, 2, 1), ops.out_hw(W, 3, 2, 1)
+        p = torch.empty(G, B, Hp, Wp, 64, device=x.device)
+        idx = torch.empty(G, B, Hp, Wp, 64, dtype=torch.uint8, device=x.device)
+        ops.maxpool_fwd(a, G * B, H, W, 64, p, idx)
+        self.stem = (rc, rb, idx, (H, W)) if self.save else None
+        if not self.save:
+            del a, idx
+        cur, H, W = p, Hp, Wp
+        for blk in t.blocks():
+            y1, r1 = self._conv(blk.conv1, cur, B, H, W)
+            a1, s1 = self._bn(blk.bn1, y1, relu=True)
+            del y1
+            y2, r2 = self._conv(blk.conv2, a1, B, H, W)
+            H2, W2 = y2.shape[2], y2.shape[3]
+            a2, s2 = self._bn(blk.bn2, y2, relu=True)
+            del y2
+            y3, r3 = self._conv(blk.conv3, a2, B, H2, W2)
+            rd = sd = None
+            if blk.downsample is not None:
+                yd, rd = self._conv(blk.downsample[0], cur, B, H, W)
+                res, sd = self._bn(blk.downsample[1], yd, relu=False)
+                del yd
+            else:
+                res = cur
+            a3, s3 = self._bn(blk.bn3, y3, relu=True, res=res)
+            del y3, res
+            if self.save:
+                recs.append((r1, s1, r2, s2, r3, s3, rd, sd))
+            cur, H, W = a3, H2, W2
+        self.final_hw = (H, W)
+        feat = torch.empty(G, B, 2048, device=x.device)
+        ops.avgpool_fwd(cur, G * B, H * W, 2048, feat)
+        del cur
+        if t.has_classifier():
+            out, self.fc_rec = self._linear(t.fc, feat, B)
+            if not self.save:
+                self.fc_rec = None
+            return out
+        return feat
+
+    def run_backward(self, dout):
+        t, G, B = self.trunk, self.G, self.B
+        self.st.grads(dout.device)
+        dout = dout.contiguous()
+        if t.has_classifier():
+            dfeat = self._linear_bwd(self.fc_rec, dout)
+            self.fc_rec = None
+        else:
+            dfeat = dout
+        H, W = self.final_hw
+        da = torch.empty(G, B, H, W, 2048, device=dout.device)
+        ops.avgpool_bwd(dfeat, G * B, H * W, 2048, da)
+        del dfeat
+        while self.recs:
+            r1, s1, r2, s2, r3, s3, rd, sd = self.recs.pop()
+            dy3, dres = self._bn_bwd(s3, da, want_dres=True)
+            del da, s3
+            da2 = self._conv_bwd(r3, dy3)
+            del dy3, r3
+            dy2, _ = self._bn_bwd(s2, da2)
+            del da2, s2
+            da1 = self._conv_bwd(r2, dy2)
+            del dy2, r2
+            dy1, _ = self._bn_bwd(s1, da1)
+            del da1, s1
+            if rd is not None:
+                dyd, _ = self._bn_bwd(sd, dres)
+                del dres, sd
+                dx = self._conv_bwd(r1, dy1)
+                self._conv_bwd(rd, dyd, dx=dx, accumulate=True)
+                del dyd, rd
+            else:
+                dx = self._conv_bwd(r1, dy1, addend=dres)
+                del dres
+            del dy1, r1
+            da = dx
+        rc, rb, idx, (H, W) = self.stem
+        self.stem = None
+        da0 = torch.empty(G, B, H, W, 64, device=da.device)
+        ops.maxpool_bwd(da, idx, G * B, H, W, 64, da0)
+        del da, idx
+        dy0, _ = self._bn_bwd(rb, da0)
+        del da0
+        self._conv_bwd(rc, dy0, need_dx=False)
+        return (None,)
+
+
+# ----------------------------------------------------------------------------- head
+class HeadRunner(_Runner):
+    """AdditiveAttention x3 + concat + fc -> fc1 -> fc2 (models/base_models.py:74-90)."""
+
+    def __init__(self, model, state, G, sample0, save):
+        super().__init__(state, G, sample0, save)
+        self.m = model
+
+    def _qkv(self, att, f, rows):
+        G, dev = self.G, f.device
+        w = torch.empty(G, 384, 2048, device=dev)
+        b = torch.empty(G, 384, device=dev)
+        for j, lin in enumerate((att.query_projection, att.key_projection,
+                                 att.value_projection)):
+            self._sample(lin, lin.mu_weight, lin.rho_weight, "weight",
+                         w.view(G, -1)[:, j * 128 * 2048:], 128, 2048, 1,
+                         out_gstride=384 * 2048)
+            self._sample(lin, lin.mu_bias, lin.rho_bias, "bias", b[:, j * 128:], 128, 1, 1,
+                         bias=True, out_gstride=384)
+        qkv = torch.empty(G, rows, 384, device=dev)
+        ops.conv2d_fwd(f, w, qkv, G, rows, 1, 1, 2048, 384, 1, 1, 0, bias=b)
+        return qkv, w
+
+    def _qkv_bwd(self, att, f, w, dqkv, rows):
+        G, dev = self.G, dqkv.device
+        lins = (att.query_projection, att.key_projection, att.value_projection)
+        if any(l.mu_weight.requires_grad for l in lins):
+            splits = ops.wgrad_splits(G, rows, 1, 1, 2048, 384, 1, 1, 0)
+            ws = torch.empty(splits, G, 384, 2048, device=dev)
+            ops.conv2d_bwd_weight(f, dqkv, ws, splits, G, rows, 1, 1, 2048, 384, 1, 1, 0)
+            db = torch.empty(G, 384, device=dev)
+            ops.colsum(dqkv, G, rows, 384, db)
+            for j, lin in enumerate(lins):
+                self._reparam_bwd(lin, lin.mu_weight, lin.rho_weight,
+                                  ws.view(splits, G, -1)[:, :, j * 128 * 2048:], splits, 128,
+                                  2048, 1, "weight", dw_gstride=384 * 2048,
+                                  dw_sstride=G * 384 * 2048)
+                self._reparam_bwd(lin, lin.mu_bias, lin.rho_bias, db[:, j * 128:], 1, 128, 1, 1,
+                                  "bias", bias=True, dw_gstride=384)
+        df = torch.empty(G, rows, 2048, device=dev)
+        ops.conv2d_bwd_data(dqkv, w, df, G, rows, 1, 1, 2048, 384, 1, 1, 0)
+        return df
+
+    def run_forward(self, f_img, f_bathy, f_sss):
+        m, G = self.m, self.G
+        rows = f_img.shape[1]
+        self.rows = rows
+        comb = torch.empty(G, rows, 384, device=f_img.device)
+        self.att_recs = []
+        for j, (att, f) in enumerate(((m.attention_image, f_img), (m.attention_bathy, f_bathy),
+                                      (m.attention_sss, f_sss))):
+            f = f.contiguous()
+            qkv, wqkv = self._qkv(att, f, rows)
+            t = torch.empty(G, rows, 128, device=f.device)
+            ops.attn_t(qkv, G * rows, t)
+            s, rm_ = self._linear(att.attention_mechanism, t, rows)
+            ops.attn_out(qkv, s, G * rows, comb, 384, 128 * j)
+            if self.save:
+                self.att_recs.append((att, f, wqkv, qkv, t, s, rm_))
+        h1, self.r_fc = self._linear(m.fc, comb, rows)
+        h2, self.r_fc1 = self._linear(m.fc1, h1, rows)
+        out, self.r_fc2 = self._linear(m.fc2, h2, rows)
+        if not self.save:
+            self.r_fc = self.r_fc1 = self.r_fc2 = None
+        return out
+
+    def run_backward(self, dlogits):
+        rows = self.rows
+        self.st.grads(dlogits.device)
+        dh2 = self._linear_bwd(self.r_fc2, dlogits.contiguous())
+        dh1 = self._linear_bwd(self.r_fc1, dh2)
+        dcomb = self._linear_bwd(self.r_fc, dh1)
+        self.r_fc = self.r_fc1 = self.r_fc2 = None
+        dfs = []
+        for j, (att, f, wqkv, qkv, t, s, rm_) in enumerate(self.att_recs):
+            dqkv = torch.empty_like(qkv)
+            ds = torch.empty_like(s)
+            ops.attn_out_bwd(dcomb, 384, 128 * j, qkv, s, self.G * rows, dqkv, ds)
+            dt = self._linear_bwd(rm_, ds)
+            ops.attn_t_bwd(dt, t, self.G * rows, dqkv)
+            dfs.append(self._qkv_bwd(att, f, wqkv, dqkv, rows))
+        self.att_recs = []
+        return tuple(dfs)
+
+
+# ----------------------------------------------------------------------------- entry points
+def _check_trunk(trunk):
+    from .resnet import ResNet
+    if not isinstance(trunk, ResNet):
+        raise TypeError(f"mauv engine needs a mauv.resnet.ResNet trunk, got {type(trunk)}")
+    for m in (trunk.conv1,) + tuple(b.conv1 for b in trunk.blocks()):
+        if not is_bayesian(m):
+            raise TypeError("trunk is not Bayesian: convert it with dnn_to_bnn first "
+                            "(models/model_utils.py:26-28,35)")
+
+
+def _run(runner, params, inputs, save):
+    if save:
+        return _Engine.apply(runner, runner.st.anchor, *inputs)
+    with torch.no_grad():
+        return runner.run_forward(*inputs)
+
+
+def _to_device(x, dev):
+    return x if x.device == dev else x.to(dev, non_blocking=True)
+
+
+def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None):
+    """[num_mc, B, 2048|C] for one ResNet trunk (root = the trunk unless ``state`` given)."""
+    _check_trunk(trunk)
+    st = state or root_state(trunk)
+    dev = trunk.conv1.mu_kernel.device
+    if dev.type != "cuda":
+        raise RuntimeError("mauv: the model must be on a ROCm device (model.to('cuda'))")
+    s0 = st.next_samples(num_mc) if sample0 is None else sample0
+    params = list(trunk.parameters())
+    save = needs_grad(params)
+    runner = TrunkRunner(trunk, st, num_mc, s0, save)
+    return _run(runner, params, (_to_device(x, dev),), save)
+
+
+def run_multimodal_mc(model, inputs, bathy, sss, num_mc):
+    """[num_mc, B, C] logits of MultiModalModel for num_mc MC samples in one batched pass."""
+    st = root_state(model)
+    for trunk in (model.image_model_feat, model.bathy_model_feat, model.sss_model_feat):
+        _check_trunk(trunk)
+    dev = model.fc.mu_weight.device
+    s0 = st.next_samples(num_mc)
+    f_img = run_trunk_mc(model.image_model_feat, inputs, num_mc, st, s0)
+    f_bathy = run_trunk_mc(model.bathy_model_feat, bathy, num_mc, st, s0)
+    f_sss = run_trunk_mc(model.sss_model_feat, sss, num_mc, st, s0)
+    head_params = [p for n, p in model.named_parameters() if not n.split(".")[0].endswith("_feat")]
+    save = needs_grad(head_params) or any(f.requires_grad for f in (f_img, f_bathy, f_sss))
+    runner = HeadRunner(model, st, num_mc, s0, save)
+    return _run(runner, head_params, (f_img, f_bathy, f_sss), save)

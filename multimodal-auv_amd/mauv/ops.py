@@ -32,22 +32,50 @@ def out_hw(H, R, stride, pad):
     return (H + 2 * pad - R) // stride + 1
 
 
+# ----------------------------------------------------------------------- profiling hook
+# bench.py sets PROFILE to a list to time every implicit-GEMM launch with HIP events on the
+# stream the kernel runs on (torch's current stream); entries: (kind, flops, ev0, ev1).
+PROFILE = None
+
+
+class _Prof:
+    __slots__ = ("kind", "flops", "e0")
+
+    def __init__(self, kind, flops):
+        self.kind, self.flops = kind, flops
+
+    def __enter__(self):
+        if PROFILE is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+
+    def __exit__(self, *a):
+        if PROFILE is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            PROFILE.append((self.kind, self.flops, self.e0, e1))
+
+
 # ----------------------------------------------------------------------- convolutions
 def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_strides=None):
     """y[G][B*Ho*Wo][Cout] = conv(x[g], w[g]) (+ bias[g]); w: [G][Cout][R][R][Cin]."""
     _f32(w, y, bias)
     assert x.is_cuda and x.dtype == torch.float32
     xs = None if x_strides is None else _LL5(*x_strides)
-    check(lib.mauv_conv2d_fwd_f32(_p(x), xs, _p(w), _p(bias), _p(y), G, B, H, W, Cin, Cout,
-                                  R, R, stride, pad, stream()), "conv2d_fwd")
+    Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
+    with _Prof("fwd", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin):
+        check(lib.mauv_conv2d_fwd_f32(_p(x), xs, _p(w), _p(bias), _p(y), G, B, H, W, Cin, Cout,
+                                      R, R, stride, pad, stream()), "conv2d_fwd")
 
 
 def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=None,
                     accumulate=False):
     _f32(dy, w, dx, addend)
-    check(lib.mauv_conv2d_bwd_data_f32(_p(dy), _p(w), _p(dx), _p(addend), int(accumulate), G,
-                                       B, H, W, Cin, Cout, R, R, stride, pad, stream()),
-          "conv2d_bwd_data")
+    Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
+    with _Prof("dgrad", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin):
+        check(lib.mauv_conv2d_bwd_data_f32(_p(dy), _p(w), _p(dx), _p(addend), int(accumulate),
+                                           G, B, H, W, Cin, Cout, R, R, stride, pad, stream()),
+              "conv2d_bwd_data")
 
 
 def wgrad_splits(G, B, H, W, Cin, Cout, R, stride, pad):
@@ -59,23 +87,30 @@ def conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, R, stride, pad,
     """ws[splits][G][Cout][R*R*Cin] partial slabs."""
     _f32(dy, ws)
     xs = None if x_strides is None else _LL5(*x_strides)
-    check(lib.mauv_conv2d_bwd_weight_f32(_p(x), xs, _p(dy), _p(ws), splits, G, B, H, W, Cin,
-                                         Cout, R, R, stride, pad, stream()),
-          "conv2d_bwd_weight")
+    Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
+    with _Prof("wgrad", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin):
+        check(lib.mauv_conv2d_bwd_weight_f32(_p(x), xs, _p(dy), _p(ws), splits, G, B, H, W,
+                                             Cin, Cout, R, R, stride, pad, stream()),
+              "conv2d_bwd_weight")
 
 
 # ----------------------------------------------------------------------- reparam / KL
-def reparam_sample(mu, rho, out, G, seed, sample0, layer, Cout, Cin, RS, eps=None):
-    _f32(mu, rho, out, eps)
+def reparam_sample(mu, rho, out, G, seed, sample0, layer, Cout, Cin, RS, eps=None,
+                   out_gstride=0):
+    """out[g] (KRSC, group stride out_gstride or numel) = mu + softplus(rho) * eps_g."""
+    _f32(mu, rho, eps)
     check(lib.mauv_reparam_sample(_p(mu), _p(rho), _p(eps), seed, sample0, layer, G, Cout, Cin,
-                                  RS, _p(out), stream()), "reparam_sample")
+                                  RS, _p(out), out_gstride, stream()), "reparam_sample")
 
 
 def reparam_bwd(dw, splits, mu, rho, dmu, drho, G, seed, sample0, layer, Cout, Cin, RS,
-                eps=None):
-    _f32(dw, mu, rho, dmu, drho, eps)
-    check(lib.mauv_reparam_bwd(_p(dw), splits, _p(mu), _p(rho), _p(eps), seed, sample0, layer,
-                               G, Cout, Cin, RS, _p(dmu), _p(drho), stream()), "reparam_bwd")
+                eps=None, dw_gstride=0, dw_sstride=0, fixed_sample=-1):
+    """fixed_sample >= 0: bayesian-torch semantics (rho-gradient uses that sample's eps for
+    every MC group); -1: exact per-sample reparameterisation gradient."""
+    _f32(mu, rho, dmu, drho, eps)
+    check(lib.mauv_reparam_bwd(_p(dw), splits, dw_gstride, dw_sstride, _p(mu), _p(rho), _p(eps),
+                               seed, sample0, layer, G, Cout, Cin, RS, _p(dmu), _p(drho),
+                               fixed_sample, stream()), "reparam_bwd")
 
 
 def kl_fwd(table, n, workspace, out, scale=1.0):
@@ -111,6 +146,11 @@ def bn_fwd_train(y, G, M, C, gamma, beta, run_mean, run_var, momentum, eps, ws, 
 def bn_apply(y, scale, shift, res, relu, out, G, M, C):
     check(lib.mauv_bn_apply(_p(y), _p(scale), _p(shift), _p(res), int(relu), _p(out), G, M, C,
                             stream()), "bn_apply")
+
+
+def bn_eval_params(G, C, gamma, beta, run_mean, run_var, eps, scale, shift):
+    check(lib.mauv_bn_eval_params(G, C, _p(gamma), _p(beta), _p(run_mean), _p(run_var), eps,
+                                  _p(scale), _p(shift), stream()), "bn_eval_params")
 
 
 def bn_bwd(y, out, dout, relu, mean, invstd, scale, G, M, C, ws, dy, dres=None, dgamma=None,
@@ -160,9 +200,9 @@ def colsum(dy, G, rows, N, out, accumulate=False):
     check(lib.mauv_colsum(_p(dy), G, rows, N, _p(out), int(accumulate), stream()), "colsum")
 
 
-def mc_mean_ce(logits, labels, G, B, C, mean, loss):
-    check(lib.mauv_mc_mean_ce(_p(logits), _p(labels), G, B, C, _p(mean), _p(loss), stream()),
-          "mc_mean_ce")
+def mc_mean_ce(logits, labels, G, B, C, mean, loss, pred=None):
+    check(lib.mauv_mc_mean_ce(_p(logits), _p(labels), G, B, C, _p(mean), _p(loss), _p(pred),
+                              stream()), "mc_mean_ce")
 
 
 def mc_mean_bwd(dmean, gloss, mean, labels, G, B, C, dlogits):

@@ -1,0 +1,332 @@
+"""MC training / evaluation loops with the reference's call surface.
+
+Signatures, return values, CSV rows, KL weighting and skip rules follow
+``train/multimodal.py`` and ``train/unimodal.py``; the difference is inside the batch:
+
+* the ``num_mc`` stochastic forwards run as ONE batched pass (``model.mc_forward``) instead of
+  a Python loop of single forwards (multimodal.py:107-118, unimodal.py:127-130);
+* the KL term is computed once per batch (it does not depend on the MC sample — the reference
+  recomputes the identical value ``num_mc`` times and averages);
+* mean-over-MC + cross-entropy is one fused kernel; the NaN/Inf gradient guard
+  (multimodal.py:141) is one fused scan over the flat gradient arena + one host sync instead
+  of ~700 per-tensor syncs.
+
+Models without ``mc_forward`` (e.g. the reference tests' dummy modules) run the reference's
+sequential loop unchanged.
+"""
+import csv
+import logging
+import os
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .kl import get_kl_loss, unwrap
+from . import mchead
+
+
+def kl_weight_for(epoch, total_num_epochs):
+    return (2 ** (epoch + 1)) / (2 ** total_num_epochs)  # multimodal.py:80, unimodal.py:71
+
+
+def _is_plain_ce(criterion):
+    return (type(criterion) is nn.CrossEntropyLoss and criterion.weight is None
+            and criterion.reduction == "mean" and criterion.ignore_index == -100
+            and float(getattr(criterion, "label_smoothing", 0.0)) == 0.0)
+
+
+def mc_logits(model, num_mc, *inputs):
+    """[num_mc, B, C]: batched on mauv models, the reference's sequential loop otherwise."""
+    core = unwrap(model)
+    if hasattr(core, "mc_forward"):
+        return model.mc_forward(*inputs, num_mc) if hasattr(model, "mc_forward") \
+            else core.mc_forward(*inputs, num_mc)
+    if isinstance(model, torch.nn.parallel.DistributedDataParallel):
+        model = model.module
+    return torch.stack([model(*inputs) for _ in range(num_mc)])
+
+
+def _grads_finite(model):
+    st = unwrap(model).__dict__.get("_mauv_state")
+    if st is not None and st.arena is not None and all(
+            p.grad is None or p.grad.data_ptr() == v.data_ptr()
+            for p, v in zip(st.arena.params, st.arena.views)):
+        return mchead.all_finite(st.arena.flat)
+    grads = [p.grad for p in model.parameters() if p.grad is not None]
+    return True if not grads else mchead.all_finite(grads)
+
+
+def mc_loss(model, inputs_tuple, labels, criterion, num_mc, batch_size, kl_w):
+    """Forward part of one training batch -> (loss, output_mean, predicted, ce, scaled_kl)."""
+    logits = mc_logits(model, num_mc, *inputs_tuple)
+    kl = get_kl_loss(model)
+    if _is_plain_ce(criterion) and logits.is_cuda:
+        ce, output, predicted = mchead.mc_mean_ce(logits, labels)
+    else:
+        output = mchead.mc_mean(logits) if logits.is_cuda else logits.mean(0)
+        ce = criterion(output, labels)
+        predicted = torch.max(output.detach(), 1)[1]
+    scaled_kl = kl / batch_size * kl_w if kl is not None else torch.zeros((), device=ce.device)
+    return ce + scaled_kl, output, predicted, ce, scaled_kl
+
+
+def mc_train_step(model, inputs_tuple, labels, criterion, optimizer, num_mc, batch_size, kl_w):
+    """One reference training batch (multimodal.py:104-146): MC forward, KL, CE, NaN/Inf loss
+    skip, backward, NaN/Inf gradient guard, optimizer step + zero_grad."""
+    loss, output, predicted, ce, scaled_kl = mc_loss(model, inputs_tuple, labels, criterion,
+                                                     num_mc, batch_size, kl_w)
+    if not torch.isfinite(loss).item():
+        logging.warning(f"Skipping batch due to NaN/Inf loss: {loss}")
+        return None
+    loss.backward()
+    if hasattr(model, "allreduce_grads"):  # mauv.ddp.DistributedMC: one RCCL all-reduce
+        model.allreduce_grads()
+    stepped = _grads_finite(model)
+    if stepped:
+        optimizer.step()
+        optimizer.zero_grad()
+    else:
+        logging.warning("Skipping optimizer step due to NaN/Inf gradients")
+    return dict(loss=loss.detach(), output=output, predicted=predicted, ce=ce.detach(),
+                scaled_kl=scaled_kl.detach(), stepped=stepped)
+
+
+def _batch_to(batch, device, bathy_patch_type, sss_patch_type):
+    inputs = batch["main_image"].to(device, non_blocking=True)
+    labels = batch["label"].long().to(device, non_blocking=True)
+    bathy = batch["bathy_image"].to(device, non_blocking=True)
+    sss = batch["sss_image"].to(device, non_blocking=True)
+    # only the selected patch tensors move to the device (the reference copies all of them)
+    pb, ps = batch.get("patch_bathy", {}), batch.get("patch_sss", {})
+    if bathy_patch_type in pb:
+        bathy = pb[bathy_patch_type].to(device, non_blocking=True)
+    if sss_patch_type in ps:
+        sss = ps[sss_patch_type].to(device, non_blocking=True)
+    return inputs, labels, bathy, sss
+
+
+def _patch_tag(t, kind):
+    return t.replace("patch_", "").replace(f"_{kind}", "") if t else "none"
+
+
+def train_multimodal_model(multimodal_model, dataloader, criterion, optimizer, epoch, device,
+                           model_type, total_num_epochs, num_mc, sum_writer,
+                           bathy_patch_type=None, sss_patch_type=None, csv_path=""):
+    """train/multimodal.py:25-202 -> (train_loss, train_accuracy)."""
+    from .checkpointing import save_model
+    multimodal_model.train()
+    csv_path = str(Path(csv_path))
+    sss_tag, bathy_tag = _patch_tag(sss_patch_type, "sss"), _patch_tag(bathy_patch_type, "bathy")
+    new_file = not os.path.isfile(csv_path)
+    try:
+        with open(csv_path, mode="a", newline="") as fh:
+            w = csv.writer(fh)
+            if new_file:
+                w.writerow(["Epoch", "Model type", "Loss", "Accuracy", "lr", "kl loss",
+                            "cross entropy loss", "SSS Patch Type", "Channel Patch Type"])
+            kl_w = kl_weight_for(epoch, total_num_epochs)
+            total_loss, correct, total = 0.0, 0, 0
+            last = None
+            for i, batch in enumerate(dataloader):
+                inputs, labels, bathy, sss = _batch_to(batch, device, bathy_patch_type,
+                                                       sss_patch_type)
+                r = mc_train_step(multimodal_model, (inputs, bathy, sss), labels, criterion,
+                                  optimizer, num_mc, dataloader.batch_size, kl_w)
+                if r is None:
+                    continue
+                last = r
+                lv = r["loss"].item()
+                total_loss += lv
+                correct += int((r["predicted"] == labels).sum().item())
+                total += labels.size(0)
+                sum_writer.add_scalar("Loss/train", lv, i)
+                logging.info(f"[Epoch {epoch} | Batch {i}] Loss: {lv:.4f}, "
+                             f"Accuracy: {correct / max(total, 1):.4f}")
+            train_accuracy = correct / total
+            train_loss = total_loss / total
+            lr = optimizer.param_groups[0]["lr"]
+            logging.info(f"Epoch {epoch + 1} complete. Loss: {train_loss:.4f}, "
+                         f"Accuracy: {train_accuracy:.4f}, LR: {lr:.6f}")
+            w.writerow([epoch, model_type, train_loss, train_accuracy, lr,
+                        last["scaled_kl"].item(), last["ce"].item(), sss_tag, bathy_tag])
+        if epoch % 5 == 0:
+            save_model(multimodal_model, csv_path,
+                       f"{model_type}_bathy_patch{bathy_tag}_sss_patch{sss_tag}")
+    except Exception:
+        save_model(multimodal_model, csv_path,
+                   f"{model_type}_bathy_patch{bathy_tag}_sss_patch{sss_tag}")
+        logging.error(f"Error at epoch {epoch}", exc_info=True)
+        train_loss, train_accuracy = 0.0, 0.0
+    return train_loss, train_accuracy
+
+
+def _confusion_png(labels, predicted, csv_path, model_type, epoch):
+    fig = None
+    try:
+        import matplotlib
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+        from sklearn.metrics import confusion_matrix, ConfusionMatrixDisplay
+        cm = confusion_matrix(labels, predicted)
+        fig, ax = plt.subplots(figsize=(8, 8))
+        ConfusionMatrixDisplay(confusion_matrix=cm).plot(cmap="Blues", ax=ax)
+        plt.title(f"Confusion Matrix for Epoch {epoch}")
+        folder = os.path.join(os.path.dirname(csv_path), "confusion_matrices")
+        os.makedirs(folder, exist_ok=True)
+        plt.savefig(os.path.join(folder, f"conf_matrix_model_{model_type}_{epoch}.png"))
+    except Exception as e:
+        logging.warning(f"Confusion matrix not saved due to plotting error: {e}")
+    finally:
+        if fig is not None:
+            import matplotlib.pyplot as plt
+            plt.close(fig)
+
+
+def evaluate_multimodal_model(multimodal_model, dataloader, device, epoch, total_num_epochs,
+                              num_mc, model_type, bathy_patch_type=None, sss_patch_type=None,
+                              csv_path=""):
+    """train/multimodal.py:204-369 -> test accuracy (BN stays in train mode, :232)."""
+    multimodal_model.train()
+    csv_path = str(Path(csv_path))
+    new_file = not os.path.isfile(csv_path)
+    try:
+        with open(csv_path, mode="a", newline="") as fh:
+            w = csv.writer(fh)
+            if new_file:
+                w.writerow(["Epoch", "Model Type", "Test Loss", "Test Accuracy",
+                            "Predictive Uncertainty", "Model Uncertainty", "Scaled KL",
+                            "Cross Entropy Loss", "bathy Patch Type", "SSS Patch Type"])
+            kl_w = kl_weight_for(epoch, total_num_epochs)
+            total_loss, correct, total = 0.0, 0, 0
+            all_pred, all_lab, all_pu, all_mu = [], [], [], []
+            with torch.no_grad():
+                for batch in dataloader:
+                    inputs, labels, bathy, sss = _batch_to(batch, device, bathy_patch_type,
+                                                           sss_patch_type)
+                    logits = mc_logits(multimodal_model, num_mc, inputs, bathy, sss)
+                    kl = get_kl_loss(multimodal_model)
+                    kl_scaled = kl / len(dataloader) * kl_w
+                    ce, _, predicted = mchead.mc_mean_ce(logits, labels)
+                    total_loss += (ce + kl_scaled).item()
+                    correct += int((predicted == labels).sum().item())
+                    total += labels.size(0)
+                    st = mchead.mc_finalize(mchead.mc_stats(logits, 1e-8), num_mc,
+                                            logits.shape[2], 1e-8)
+                    pu = st["predictive_entropy"]
+                    all_pu.extend(pu.cpu().numpy())
+                    all_mu.extend((pu - st["aleatoric"]).cpu().numpy())
+                    all_pred.extend(predicted.cpu().numpy())
+                    all_lab.extend(labels.cpu().numpy())
+            test_accuracy = correct / total
+            test_loss = total_loss / len(dataloader)
+            _confusion_png(all_lab, all_pred, csv_path, model_type, epoch)
+            w.writerow([epoch + 1, model_type, test_loss, test_accuracy, np.mean(all_pu),
+                        np.mean(all_mu), kl_scaled.item(), ce.item(),
+                        bathy_patch_type or "patch_30_bathy", sss_patch_type or "patch_30_sss"])
+            logging.info(f"Epoch {epoch + 1}: Test Loss: {test_loss:.4f}, "
+                         f"Accuracy: {test_accuracy:.4f}")
+    except Exception as e:
+        logging.error(f"Critical error at epoch {epoch}: {e}", exc_info=True)
+        test_accuracy = 0.0
+    return test_accuracy
+
+
+_UNI_SOURCES = {"image": "main_image", "sss": "sss_image", "bathy": "bathy_image"}
+
+
+def train_unimodal_model(model, dataloader, criterion, optimizer, epoch, total_num_epochs,
+                         num_mc, sum_writer, device, model_type="image", csv_path="",
+                         patch_type=None):
+    """train/unimodal.py:21-175 -> (train_accuracy, train_loss) (note the reference's order)."""
+    from .checkpointing import save_model
+    model.train()
+    model.to(device)
+    kl_w = kl_weight_for(epoch, total_num_epochs)
+    new_file = not os.path.isfile(csv_path)
+    try:
+        with open(csv_path, mode="a", newline="") as fh:
+            w = csv.writer(fh)
+            if new_file:
+                w.writerow(["Epoch", "Model type", "Loss", "Accuracy", "lr"])
+            total_loss, correct, total = 0.0, 0, 0
+            for i, batch in enumerate(dataloader):
+                if model_type not in _UNI_SOURCES:
+                    logging.error(f"Unknown model_type: {model_type}")
+                    raise ValueError(f"Unknown model_type: {model_type}")
+                x = batch[_UNI_SOURCES[model_type]].to(device, non_blocking=True)
+                labels = batch["label"].long().to(device, non_blocking=True)
+                optimizer.zero_grad()
+                logits = mc_logits(model, num_mc, x)
+                kl = get_kl_loss(model)
+                if _is_plain_ce(criterion) and logits.is_cuda:
+                    ce, output, predicted = mchead.mc_mean_ce(logits, labels)
+                else:
+                    output = mchead.mc_mean(logits) if logits.is_cuda else logits.mean(0)
+                    ce = criterion(output, labels)
+                    predicted = output.detach().float().max(1)[1]
+                loss = ce + kl_w * (kl / dataloader.batch_size)
+                loss.backward()
+                optimizer.step()
+                lv = loss.item()
+                total_loss += lv
+                correct += int((predicted == labels).sum().item())
+                total += labels.size(0)
+                sum_writer.add_scalar("Loss/train", lv, i)
+            train_accuracy = correct / total
+            train_loss = total_loss / total
+            lr = optimizer.param_groups[0]["lr"]
+            w.writerow([epoch + 1, model_type, train_loss, train_accuracy, lr])
+        if epoch % 5 == 0:
+            save_model(model, csv_path, model_type)
+    except Exception:
+        save_model(model, csv_path, model_type)
+        logging.error(f"Error at epoch {epoch}", exc_info=True)
+        train_accuracy, train_loss = 0.0, 0.0
+    return train_accuracy, train_loss
+
+
+def evaluate_unimodal_model(model, dataloader, device, epoch, csv_path, total_num_epochs, num_mc,
+                            model_type="image", patch_type=None):
+    """train/unimodal.py:178-365 -> accuracy (epistemic = var over MC, eps 1e-7 entropy)."""
+    model.train()
+    kl_w = kl_weight_for(epoch, total_num_epochs)
+    new_file = not os.path.isfile(csv_path)
+    try:
+        with open(csv_path, mode="a", newline="") as fh:
+            w = csv.writer(fh)
+            if new_file:
+                w.writerow(["Epoch", "Model Type", "Test Loss", "Test Accuracy",
+                            "predictive_uncertainty", "model_uncertainty"])
+            correct, total, total_loss = 0, 0, 0.0
+            all_ep, all_al, all_pred, all_lab = [], [], [], []
+            with torch.no_grad():
+                for batch in dataloader:
+                    if model_type not in _UNI_SOURCES:
+                        raise ValueError(f"Unknown model_type: {model_type}")
+                    x = batch[_UNI_SOURCES[model_type]].to(device, non_blocking=True)
+                    labels = batch["label"].long().to(device, non_blocking=True)
+                    logits = mc_logits(model, num_mc, x)
+                    kl = get_kl_loss(model)
+                    ce, _, predicted = mchead.mc_mean_ce(logits, labels)
+                    total_loss += (ce + kl_w * (kl / dataloader.batch_size)).item()
+                    correct += int((predicted == labels).sum().item())
+                    total += labels.size(0)
+                    st = mchead.mc_finalize(mchead.mc_stats(logits, 1e-7), num_mc,
+                                            logits.shape[2], 1e-7)
+                    all_ep.extend(st["var"].cpu().numpy())
+                    all_al.extend(st["aleatoric"].cpu().numpy())
+                    all_pred.extend(predicted.cpu().numpy())
+                    all_lab.extend(labels.cpu().numpy())
+            accuracy = correct / total
+            avg_loss = total_loss / total
+            _confusion_png(all_lab, all_pred, csv_path, model_type, epoch)
+            w.writerow([epoch + 1, model_type, avg_loss, accuracy,
+                        np.mean(all_ep) if all_ep else 0.0, np.mean(all_al) if all_al else 0.0])
+    except Exception:
+        from .checkpointing import save_model
+        save_model(model, csv_path, model_type)
+        logging.error(f"Error at epoch {epoch}", exc_info=True)
+        accuracy = 0.0
+    return accuracy

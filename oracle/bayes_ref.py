@@ -35,12 +35,19 @@ def set_eps_source(fn):
     _EPS_SOURCE = fn
 
 
+ALIAS_EPS = True   # bayesian-torch behaviour; False = fresh tensor per draw (exact gradient)
+
+
 def _draw_eps(layer, name, buf):
+    # bayesian-torch 0.5.0 does `eps = self.eps_kernel.data.normal_()`: the tensor autograd
+    # saves for d(sigma*eps)/d(sigma) aliases the buffer, so when several MC forwards run
+    # before one backward every pass's rho-gradient sees the LAST draw.  Reproduced here.
     if _EPS_SOURCE is None:
-        return buf.data.normal_()
+        e = buf.data.normal_()
+        return e if ALIAS_EPS else e.clone()
     e = _EPS_SOURCE(layer, name, tuple(buf.shape))
     buf.data.copy_(e)
-    return buf.data
+    return buf.data if ALIAS_EPS else e
 
 
 def kl_div(mu_q, sigma_q, mu_p, sigma_p):

@@ -1,0 +1,90 @@
+"""Shared helpers for the parity tests: build matching oracle / mauv models and feed both the
+same epsilons (the oracle's draws are recorded and replayed into the HIP sampler)."""
+import torch
+
+from oracle import bayes_ref
+from oracle.model_ref import define_models as oracle_define, DEFAULT_PRIOR
+from tests.golden.common import RecordingEpsSource
+
+
+def build_pair(seed=0, num_classes=7, key="multimodal_model"):
+    from mauv.models import define_models
+    torch.manual_seed(seed)
+    o = oracle_define(None, num_classes, DEFAULT_PRIOR)[key]
+    torch.manual_seed(seed)
+    m = define_models(None, num_classes, DEFAULT_PRIOR)[key]
+    m.load_state_dict(o.state_dict())
+    return o, m.cuda()
+
+
+class EpsBridge:
+    """Record the oracle's per-layer epsilons over N sequential passes and serve them to the
+    mauv engine as [G, numel] tensors keyed by the same qualified module name."""
+
+    def __init__(self, oracle_model, mauv_model, seed):
+        self.src = RecordingEpsSource(seed)
+        self.o_names = {id(mod): n for n, mod in oracle_model.named_modules()}
+        self.m_names = {id(mod): n for n, mod in mauv_model.named_modules()}
+        self.store = {}
+
+    def __enter__(self):
+        bayes_ref.set_eps_source(self.src)
+        return self
+
+    def __exit__(self, *a):
+        bayes_ref.set_eps_source(None)
+
+    def collect(self):
+        self.store = {}
+        for layer, name, e in self.src.log:
+            self.store.setdefault((self.o_names[id(layer)], name), []).append(e.reshape(-1))
+        self.src.log.clear()
+
+    def provider(self, module, name, G):
+        lst = self.store[(self.m_names[id(module)], name)]
+        assert len(lst) >= G, (self.m_names[id(module)], name, len(lst), G)
+        return torch.stack(lst[:G]).cuda().contiguous()
+
+
+def oracle64(o, store, fn):
+    """Run ``fn(o64)`` on a float64 copy of the oracle, replaying the recorded epsilons
+    (``store`` from EpsBridge.collect) in the same per-layer order -> the 'truth' used to
+    judge the fp32 HIP path against the fp32 CPU path (both are fp32 chains through an
+    ill-conditioned BN backward at small spatial sizes)."""
+    import copy
+    o64 = copy.deepcopy(o).double()
+    for p in o64.parameters():
+        p.grad = None
+    names = {id(mod): n for n, mod in o64.named_modules()}
+    cnt = {}
+
+    def src(layer, name, shape):
+        k = (names[id(layer)], name)
+        i = cnt.get(k, 0)
+        cnt[k] = i + 1
+        return store[k][i].double().reshape(shape)
+    bayes_ref.set_eps_source(src)
+    try:
+        out = fn(o64)
+    finally:
+        bayes_ref.set_eps_source(None)
+    return o64, out
+
+
+def grad_error_profile(hip_params, cpu_params, truth_params):
+    """Per-tensor max-relative errors of HIP and CPU-fp32 grads vs the fp64 truth."""
+    hip, cpu = [], []
+    for ph, pc, pt in zip(hip_params, cpu_params, truth_params):
+        if pt.grad is None:
+            continue
+        hip.append(max_rel(ph.grad, pt.grad))
+        cpu.append(max_rel(pc.grad, pt.grad))
+    import numpy as np
+    q = lambda v: np.quantile(np.array(v), [0.5, 0.9, 1.0])
+    return q(hip), q(cpu)
+
+
+def max_rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()

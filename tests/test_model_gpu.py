@@ -1,0 +1,192 @@
+"""Model-level parity on the GPU: the mauv HIP path vs the oracle (the reference's algorithm on
+torch-CPU fp32, pinned to the reference's own code by tests/golden) on identical weights and
+identical injected epsilons.
+
+Tolerances (stated per SURVEY.md §8c):
+  logits / loss / KL   |d| <= 2e-4 * max(1, |ref|)  (observed ~1e-6 relative)
+  uncertainties        entropies 1e-5 abs, variances 1e-6 abs
+  gradients            judged against a float64 run of the oracle ('truth'): at these test
+                       shapes the BN backward is ill-conditioned and the reference's own fp32
+                       CPU gradients deviate from fp64 by up to ~30 % on some layer-4 tensors.
+                       Requirement: the HIP path is as accurate as the fp32 CPU path — its
+                       median / 90th-percentile / max per-tensor error vs fp64 are within
+                       1.5x / 2x / 2x (+1e-4) of the CPU fp32 path's.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import bayes_ref, loops_ref
+from tests.golden.common import make_batches, SEED_DATA
+from tests.helpers import build_pair, EpsBridge, max_rel, oracle64, grad_error_profile
+
+pytestmark = pytest.mark.gpu
+
+
+def _cuda(*ts):
+    return [t.cuda() for t in ts]
+
+
+def _assert_close(a, ref, tol=2e-4):
+    d = (a.detach().double().cpu() - ref.detach().double().cpu()).abs().max().item()
+    assert d <= tol * max(1.0, ref.detach().abs().max().item()), d
+
+
+def _assert_grads_as_accurate(hip, cpu, truth):
+    h, c = grad_error_profile(hip, cpu, truth)
+    assert h[0] <= 1.5 * c[0] + 1e-4, (h, c)
+    assert h[1] <= 2.0 * c[1] + 1e-4, (h, c)
+    assert h[2] <= 2.0 * c[2] + 1e-4, (h, c)
+
+
+@pytest.mark.parametrize("S,B,N", [(64, 2, 3), (96, 3, 2)])
+def test_multimodal_train_step_parity(S, B, N):
+    from mauv.engine import root_state
+    from mauv.kl import get_kl_loss
+    from mauv import mchead
+    o, m = build_pair()
+    batch = make_batches(SEED_DATA, 1, B=B, S_opt=S, S_son=S)[0]
+    x, b, s, y = batch["main_image"], batch["bathy_image"], batch["sss_image"], batch["label"]
+
+    def oracle_loss(model, dt=torch.float32):
+        lg = torch.stack([model(x.to(dt), b.to(dt), s.to(dt)) for _ in range(N)])
+        loss = F.cross_entropy(lg.mean(0), y) + bayes_ref.get_kl_loss(model) / B * 0.5
+        loss.backward()
+        return lg, loss
+
+    bridge = EpsBridge(o, m, 99)
+    with bridge:
+        o_logits, loss_o = oracle_loss(o)
+    bridge.collect()
+    o64, (l64, loss64) = oracle64(o, bridge.store, lambda mm: oracle_loss(mm, torch.float64))
+
+    root_state(m).eps_provider = bridge.provider
+    logits = m.mc_forward(*_cuda(x, b, s), N)
+    _assert_close(logits, o_logits)
+    _assert_close(logits, l64)
+    kl = get_kl_loss(m)
+    assert abs(kl.item() - bayes_ref.get_kl_loss(o).item()) <= 1e-5 * abs(kl.item())
+    ce, out, pred = mchead.mc_mean_ce(logits, y.cuda())
+    loss = ce + kl / B * 0.5
+    assert abs(loss.item() - loss_o.item()) <= 1e-4 * abs(loss_o.item())
+    loss.backward()
+    _assert_grads_as_accurate(list(m.parameters()), list(o.parameters()), list(o64.parameters()))
+    # running statistics after N sequential train-mode passes
+    obuf = dict(o.named_buffers())  # (the oracle also holds non-persistent eps/prior buffers)
+    for n, bm in m.named_buffers():
+        if "running_mean" in n:
+            assert (bm.cpu() - obuf[n]).abs().max().item() <= 1e-5 + 1e-4 * obuf[n].abs().max(), n
+        if "running_var" in n:
+            assert max_rel(bm, obuf[n]) <= 1e-4, n
+        if "num_batches" in n:
+            assert int(bm) == int(obuf[n]) == N
+
+
+def test_exact_rho_gradient_mode():
+    """rho_grad="exact" (per-sample eps) vs the oracle with non-aliased epsilons."""
+    from mauv.engine import root_state, set_rho_grad_mode
+    from mauv import mchead
+    o, m = build_pair()
+    batch = make_batches(SEED_DATA, 1, B=2, S_opt=64, S_son=64)[0]
+    x, b, s, y = batch["main_image"], batch["bathy_image"], batch["sss_image"], batch["label"]
+
+    def oracle_loss(model, dt=torch.float32):
+        lg = torch.stack([model(x.to(dt), b.to(dt), s.to(dt)) for _ in range(3)])
+        F.cross_entropy(lg.mean(0), y).backward()
+
+    bridge = EpsBridge(o, m, 11)
+    bayes_ref.ALIAS_EPS = False
+    try:
+        with bridge:
+            oracle_loss(o)
+        bridge.collect()
+        o64, _ = oracle64(o, bridge.store, lambda mm: oracle_loss(mm, torch.float64))
+    finally:
+        bayes_ref.ALIAS_EPS = True
+    set_rho_grad_mode(m, "exact")
+    root_state(m).eps_provider = bridge.provider
+    logits = m.mc_forward(*_cuda(x, b, s), 3)
+    mchead.mc_mean_ce(logits, y.cuda())[0].backward()
+    _assert_grads_as_accurate(list(m.parameters()), list(o.parameters()), list(o64.parameters()))
+
+
+def test_mc_batched_equals_sequential():
+    """G samples in one launch == G sequential single-sample forwards (same Philox stream)."""
+    from mauv.engine import root_state
+    _, m = build_pair()
+    batch = make_batches(SEED_DATA, 1, B=2, S_opt=64, S_son=64)[0]
+    x, b, s = _cuda(batch["main_image"], batch["bathy_image"], batch["sss_image"])
+    st = root_state(m)
+    with torch.no_grad():
+        st.offset = 0
+        batched = m.mc_forward(x, b, s, 4)
+        st.offset = 0
+        seq = torch.stack([m(x, b, s) for _ in range(4)])
+    assert torch.equal(batched, seq)
+    assert not torch.equal(batched[0], batched[1])  # samples differ
+
+
+def test_unimodal_resnet50custom_parity():
+    from mauv.engine import root_state
+    from mauv.kl import get_kl_loss
+    from mauv import mchead
+    o, m = build_pair(key="image_model")
+    batch = make_batches(SEED_DATA, 1, B=2, S_opt=64, S_son=64)[0]
+    x, y = batch["main_image"], batch["label"]
+
+    def oracle_loss(model, dt=torch.float32):
+        lg = torch.stack([model(x.to(dt)) for _ in range(2)])
+        loss = F.cross_entropy(lg.mean(0), y) + 0.25 * bayes_ref.get_kl_loss(model) / 2
+        loss.backward()
+        return lg, loss
+
+    bridge = EpsBridge(o, m, 7)
+    with bridge:
+        o_logits, loss_o = oracle_loss(o)
+    bridge.collect()
+    o64, _ = oracle64(o, bridge.store, lambda mm: oracle_loss(mm, torch.float64))
+    root_state(m).eps_provider = bridge.provider
+    logits = m.mc_forward(x.cuda(), 2)
+    _assert_close(logits, o_logits)
+    ce, _, _ = mchead.mc_mean_ce(logits, y.cuda())
+    loss = ce + 0.25 * get_kl_loss(m) / 2
+    assert abs(loss.item() - loss_o.item()) <= 1e-4 * abs(loss_o.item())
+    loss.backward()
+    _assert_grads_as_accurate(list(m.parameters()), list(o.parameters()), list(o64.parameters()))
+
+
+def test_predict_uncertainty_parity():
+    """Fused MC statistics (HIP) vs predictors.py maths on the oracle (fp32, no autocast)."""
+    from mauv.engine import root_state
+    from mauv.predict import mc_statistics
+    o, m = build_pair()
+    batch = make_batches(SEED_DATA, 1, B=3, S_opt=64, S_son=64)[0]
+    x, b, s = batch["main_image"], batch["bathy_image"], batch["sss_image"]
+    N = 5
+    bridge = EpsBridge(o, m, 5)
+    with bridge:
+        pred_o, var_o, alea_o, P = loops_ref.predict_batch(o, x, b, s, N)
+    bridge.collect()
+    root_state(m).eps_provider = bridge.provider
+    with torch.no_grad():
+        st = mc_statistics(m, *_cuda(x, b, s), N, chunk=N)
+    assert torch.equal(st["pred"].cpu(), pred_o)
+    np.testing.assert_allclose(st["var"].cpu().numpy(), var_o.numpy(), atol=1e-6, rtol=1e-3)
+    np.testing.assert_allclose(st["aleatoric"].cpu().numpy(), alea_o.numpy(), atol=1e-5)
+
+
+def test_full_resolution_forward():
+    """224 optical + 256 sonar tiles (BASELINE shapes), B=2, N=2: logits parity."""
+    from mauv.engine import root_state
+    o, m = build_pair()
+    batch = make_batches(SEED_DATA, 1, B=2, S_opt=224, S_son=256)[0]
+    x, b, s = batch["main_image"], batch["bathy_image"], batch["sss_image"]
+    bridge = EpsBridge(o, m, 3)
+    with bridge, torch.no_grad():
+        o_logits = torch.stack([o(x, b, s) for _ in range(2)])
+    bridge.collect()
+    root_state(m).eps_provider = bridge.provider
+    with torch.no_grad():
+        logits = m.mc_forward(*_cuda(x, b, s), 2)
+    _assert_close(logits, o_logits)
