@@ -1,0 +1,163 @@
+/* libmauv_hip — C-ABI of the MI355X (gfx950) hot path of sams-tom/Multimodal-AUV.
+ *
+ * The reference is pure Python: its hot path calls into third-party framework kernels
+ * (bayesian-torch 0.5.0 reparameterisation layers -> F.conv2d / F.linear / normal_ /
+ * log1p(exp) on cuDNN/cuBLAS/curand).  Each entry point below replaces one of those call
+ * sites (file:line in /root/reference/src/Multimodal_AUV unless noted) and is bound from
+ * Python with ctypes by multimodal-auv_amd/mauv/_lib.py.
+ *
+ * Conventions:
+ *  - every pointer is a DEVICE pointer owned by the caller (PyTorch caching allocator);
+ *    the library never allocates device memory — workspace sizes come from *_workspace_*;
+ *  - every call takes the hipStream_t to launch on (torch.cuda.current_stream()) and is
+ *    asynchronous (no host synchronisation);
+ *  - return 0 on success, < 0 on error (-1 bad argument, -2 launch failure);
+ *    mauv_last_error() returns a thread-local message;
+ *  - stateless and re-entrant; one process per GPU.
+ *  - MC groups: G = number of Monte-Carlo samples processed by ONE launch (the reference's
+ *    `for _ in range(num_mc): model(...)` loop, train/multimodal.py:107-112,
+ *    inference/predictors.py:54-61, collapsed onto blockIdx.z).
+ *  - layouts: activations NHWC [G][B][H][W][C] fp32; sampled weights KRSC [G][Cout][R][S][Cin];
+ *    parameters/gradients in the reference's OIHW layout (bayesian-torch state_dict shapes).
+ */
+#ifndef MAUV_H
+#define MAUV_H
+
+#include <hip/hip_runtime.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- housekeeping ---------------------------------------------------------------------- */
+const char* mauv_last_error(void);
+int mauv_abi_version(void);
+
+/* ---- implicit-GEMM convolution on MFMA (conv_gemm.hip) ---------------------------------
+ * Replaces F.conv2d inside bayesian-torch Conv2dReparameterization.forward for every conv of
+ * the three torchvision ResNet-50 trunks (models/base_models.py:15-18,
+ * models/model_utils.py:57-61) and F.linear in LinearReparameterization.forward (attention
+ * q/k/v/score, fc, fc1, fc2: models/base_models.py:38-41,60-65) as the 1x1, H=W=1 case.
+ * x_strides (host pointer, nullable): element strides {group, batch, h, w, c} of x; NULL =
+ * dense NHWC.  Group stride 0 = one input shared by all G samples (the stems read the
+ * caller's NCHW images this way). */
+int mauv_conv2d_fwd_f32(const float* x, const long long* x_strides, const float* w,
+                        const float* bias, float* y, int G, int B, int H, int W, int Cin,
+                        int Cout, int R, int S, int stride, int pad, hipStream_t stream);
+/* cuDNN dgrad in loss.backward() (train/multimodal.py:138): dx = conv^T(dy, W_g)
+ * (+ addend) (+ dx if accumulate). */
+int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx, const float* addend,
+                             int accumulate, int G, int B, int H, int W, int Cin, int Cout,
+                             int R, int S, int stride, int pad, hipStream_t stream);
+/* cuDNN wgrad (train/multimodal.py:138): split-K partial slabs ws[splits][G][Cout][R*S*Cin],
+ * reduced deterministically by mauv_reparam_bwd.  mauv_conv2d_wgrad_splits sizes them. */
+int mauv_conv2d_wgrad_splits(int G, int B, int H, int W, int Cin, int Cout, int R, int S,
+                             int stride, int pad);
+int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strides, const float* dy,
+                               float* ws, int splits, int G, int B, int H, int W, int Cin,
+                               int Cout, int R, int S, int stride, int pad, hipStream_t stream);
+
+/* ---- variational sampling / KL (reparam.hip) --------------------------------------------
+ * bayesian-torch Conv2dReparameterization/LinearReparameterization.forward:
+ *   sigma = log1p(exp(rho)); eps.normal_(); w = mu + sigma*eps      (per MC sample g)
+ * eps from Philox4x32-10(seed, sample0+g, layer, quad) — or the explicit eps [G][numel]
+ * (parameter order) when non-NULL (parity tests).  out_gstride 0 = numel. */
+int mauv_reparam_sample(const float* mu, const float* rho, const float* eps,
+                        unsigned long long seed, unsigned long long sample0, unsigned int layer,
+                        int G, int Cout, int Cin, int RS, float* out, long long out_gstride,
+                        hipStream_t stream);
+/* Backward of the above: dmu += sum_g dW_g; drho += sum_g dW_g * eps_g' * sigmoid(rho),
+ * g' = g (fixed_sample < 0) or the sample `fixed_sample` for every g (bayesian-torch 0.5.0
+ * semantics: its eps buffer is overwritten in place by later MC forwards while autograd
+ * still references it).  dw element (s, g, i) at dw[s*dw_sstride + g*dw_gstride + i]. */
+int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride, long long dw_sstride,
+                     const float* mu, const float* rho, const float* eps,
+                     unsigned long long seed, unsigned long long sample0, unsigned int layer,
+                     int G, int Cout, int Cin, int RS, float* dmu, float* drho,
+                     long long fixed_sample, hipStream_t stream);
+
+/* get_kl_loss (bayesian-torch 0.5.0; called at train/multimodal.py:114,284 and
+ * train/unimodal.py:130,262): sum over entries of mean(log s_p - log s + (s^2 + (mu-m_p)^2)
+ * / (2 s_p^2) - 1/2), s = softplus(rho).  `table` is a device array of MauvKlEntry. */
+typedef struct MauvKlEntry {
+  const float* mu;
+  const float* rho;
+  float* dmu;
+  float* drho;
+  long long numel;
+  float prior_mu;
+  float prior_sigma;
+} MauvKlEntry;
+int mauv_kl_workspace_bytes(int n_entries);
+int mauv_kl_fwd(const MauvKlEntry* table, int n, double* workspace, float scale, float* out,
+                hipStream_t stream);
+/* dmu/drho += (coef_dev ? *coef_dev : 1) * scale * dKL/d(mu, rho) (coef_dev: device scalar,
+ * the upstream gradient — no host sync). */
+int mauv_kl_bwd(const MauvKlEntry* table, int n, const float* coef_dev, float scale,
+                hipStream_t stream);
+/* test hook: raw Philox words [nq][4] and the derived normals [nq][4] */
+int mauv_philox_raw(unsigned long long seed, unsigned long long sample, unsigned int layer,
+                    int nq, unsigned int* out_u32x4, float* out_normal4, hipStream_t stream);
+
+/* ---- BatchNorm2d (training mode, per MC group) + residual + ReLU (bn.hip) ---------------
+ * torchvision Bottleneck bn1..3 / downsample.1 / stem bn1 in .train() for every MC pass
+ * (train/multimodal.py:60,232; inference/predictors.py:27).  y/out [G][M][C], M = B*H*W. */
+long long mauv_bn_workspace_floats(int G, long long M, int C);
+int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const float* gamma,
+                      const float* beta, float* run_mean, float* run_var, float momentum,
+                      float eps, float* workspace, float* mean, float* invstd, float* scale,
+                      float* shift, const float* res, int relu, float* out,
+                      hipStream_t stream);
+int mauv_bn_apply(const float* y, const float* scale, const float* shift, const float* res,
+                  int relu, float* out, int G, long long M, int C, hipStream_t stream);
+int mauv_bn_eval_params(int G, int C, const float* gamma, const float* beta,
+                        const float* run_mean, const float* run_var, float eps, float* scale,
+                        float* shift, hipStream_t stream);
+int mauv_bn_bwd(const float* y, const float* out, const float* dout, int relu,
+                const float* mean, const float* invstd, const float* scale, int G, long long M,
+                int C, float* workspace, float* dy, float* dres, float* dgamma, float* dbeta,
+                hipStream_t stream);
+
+/* ---- pooling (pool.hip): torchvision stem maxpool 3x3/2 pad 1 and adaptive avgpool ------ */
+int mauv_maxpool_fwd(const float* x, int N, int H, int W, int C, float* y, unsigned char* idx,
+                     hipStream_t stream);
+int mauv_maxpool_bwd(const float* dy, const unsigned char* idx, int N, int H, int W, int C,
+                     float* dx, hipStream_t stream);
+int mauv_avgpool_fwd(const float* x, int N, int HW, int C, float* y, hipStream_t stream);
+int mauv_avgpool_bwd(const float* dy, int N, int HW, int C, float* dx, hipStream_t stream);
+
+/* ---- fusion head + MC head (head.hip) ----------------------------------------------------
+ * AdditiveAttention.forward (models/base_models.py:43-52) epilogues around the q|k|v and
+ * score GEMMs: t = tanh(q + k); o = v * softmax(s, dim=1) into the concat slot (:86). */
+int mauv_attn_t(const float* qkv, int rows, float* t, hipStream_t stream);
+int mauv_attn_t_bwd(const float* dt, const float* t, int rows, float* dqkv, hipStream_t stream);
+int mauv_attn_out(const float* qkv, const float* s, int rows, float* comb, int comb_ld,
+                  int comb_off, hipStream_t stream);
+int mauv_attn_out_bwd(const float* dcomb, int comb_ld, int comb_off, const float* qkv,
+                      const float* s, int rows, float* dqkv, float* ds, hipStream_t stream);
+/* bias gradients of the linear layers */
+int mauv_colsum(const float* dy, int G, int rows, int N, float* out, int accumulate,
+                hipStream_t stream);
+/* train/multimodal.py:121 (mean over MC), :127 (CrossEntropyLoss), :151 (argmax) */
+int mauv_mc_mean_ce(const float* logits, const long long* labels, int G, int B, int C,
+                    float* mean, float* loss, long long* pred, hipStream_t stream);
+int mauv_mc_mean_bwd(const float* dmean, const float* gloss, const float* mean,
+                     const long long* labels, int G, int B, int C, float* dlogits,
+                     hipStream_t stream);
+/* inference/predictors.py:65-84, train/multimodal.py:305-310, train/unimodal.py:298-308:
+ * sufficient statistics sums[b] = {sum_g p (C), sum_g p^2 (C), sum_g H[p_g]} (float64,
+ * all-reducible across MC-sharded ranks), then mean prob, unbiased variance (mean over
+ * classes), aleatoric entropy, predictive entropy, argmax. */
+int mauv_mc_stats(const float* logits, int G, int B, int C, float eps_h, double* sums,
+                  int accumulate, hipStream_t stream);
+int mauv_mc_finalize(const double* sums, int N, int B, int C, float eps_pred, float* mean_prob,
+                     float* var_unc, float* alea, float* pred_entropy, long long* pred,
+                     hipStream_t stream);
+/* train/multimodal.py:133,141 NaN/Inf guards as one fused scan (*out += blocks with a
+ * non-finite value) */
+int mauv_nonfinite_count(const float* p, long long n, int* out, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAUV_H */

@@ -4,6 +4,8 @@
 #include <stdint.h>
 #include <string>
 
+#include "mauv.h"  // the C-ABI (include/mauv.h): definitions below must match it
+
 #define MAUV_API extern "C" __attribute__((visibility("default")))
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));

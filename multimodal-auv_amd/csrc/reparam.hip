@@ -17,16 +17,6 @@
 
 using namespace mauv;
 
-struct MauvKlEntry {
-  const float* mu;
-  const float* rho;
-  float* dmu;
-  float* drho;
-  long long numel;
-  float prior_mu;
-  float prior_sigma;
-};
-
 namespace mauv {
 
 __global__ __launch_bounds__(256) void reparam_sample_kernel(

@@ -32,6 +32,11 @@ def mc_chunk(model, batch_size, num_mc, budget_bytes=None):
     return max(1, min(num_mc, int(budget_bytes // max(per_sample, 1))))
 
 
+def local_mc_count(num_mc, rank, world):
+    """MC samples this rank draws when ``num_mc`` are sharded over ``world`` ranks."""
+    return num_mc // world + (1 if rank < num_mc % world else 0)
+
+
 def mc_statistics(model, inputs, bathy, sss, num_mc, eps_h=1e-7, eps_pred=1e-8, chunk=None,
                   group=None):
     """Fused MC statistics for one batch; with ``group`` (torch.distributed), the MC samples
@@ -40,13 +45,14 @@ def mc_statistics(model, inputs, bathy, sss, num_mc, eps_h=1e-7, eps_pred=1e-8, 
     B = inputs.shape[0]
     rank, world = (dist.get_rank(group), dist.get_world_size(group)) if group is not None \
         else (0, 1)
-    local = num_mc // world + (1 if rank < num_mc % world else 0)
+    local = local_mc_count(num_mc, rank, world)
     chunk = chunk or mc_chunk(model, B, max(local, 1))
+    core = model if hasattr(model, "mc_forward") else unwrap(model)
     sums = None
     done = 0
     while done < local:
         g = min(chunk, local - done)
-        logits = model.mc_forward(inputs, bathy, sss, g)
+        logits = core.mc_forward(inputs, bathy, sss, g)
         sums = mchead.mc_stats(logits, eps_h, sums)
         done += g
         del logits

@@ -1,0 +1,127 @@
+"""CPU checks: the C-ABI library loads and exports every symbol include/mauv.h declares; host
+logic (state_dict compatibility, MOPED init, known answers, checkpoint key rewrites, Philox
+known-answer vectors, KL table packing).  No compute calls — there is no GPU here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "mauv.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_ ]+\**\s+\**(mauv_\w+)\(", txt, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from mauv._lib import LIB_PATH, SIGNATURES
+    lib = ctypes.CDLL(LIB_PATH)
+    names = header_functions()
+    assert len(names) >= 30, names
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in include/mauv.h but not exported"
+    assert set(SIGNATURES) == set(names), set(SIGNATURES) ^ set(names)
+
+
+def test_library_reports_gfx950_only():
+    from mauv._lib import LIB_PATH
+    out = os.popen(f"/opt/rocm/lib/llvm/bin/llvm-readelf -n {LIB_PATH} 2>/dev/null | head -0; "
+                   f"strings -a {LIB_PATH} | grep -o 'amdgcn-amd-amdhsa--gfx[0-9a-z]*' | sort -u"
+                   ).read().split()
+    assert out and all(t.endswith("gfx950") for t in out), out
+
+
+def test_abi_version_and_error_string():
+    from mauv._lib import lib
+    assert lib.mauv_abi_version() == 1
+    assert isinstance(lib.mauv_last_error(), bytes)
+
+
+def test_state_dict_compatible_with_reference_layout():
+    from mauv.models import define_models, DEFAULT_PRIOR
+    from oracle.model_ref import define_models as oracle_define
+    torch.manual_seed(0)
+    m = define_models(None, 7, DEFAULT_PRIOR)
+    torch.manual_seed(0)
+    o = oracle_define(None, 7, DEFAULT_PRIOR)
+    for k in m:
+        a, b = m[k].state_dict(), o[k].state_dict()
+        assert list(a) == list(b), k
+        for n in a:
+            assert a[n].shape == b[n].shape and torch.equal(a[n], b[n]), (k, n)
+    mm = m["multimodal_model"]
+    assert sum(p.numel() for p in mm.parameters()) == 146_767_638
+    assert sum(p.numel() for n, p in mm.named_parameters() if "mu_" in n) == 73_304_139
+    assert sum(p.numel() for n, p in m["image_model"].named_parameters() if "mu_" in n) \
+        == 23_469_255
+
+
+def test_moped_rho_and_prior():
+    from mauv.layers import dnn_to_bnn, Conv2dReparameterization, LinearReparameterization
+    net = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 3, bias=False), torch.nn.Linear(4, 2))
+    w = net[0].weight.detach().clone()
+    dnn_to_bnn(net, {"prior_mu": 0.0, "prior_sigma": 1.0, "posterior_mu_init": 0.0,
+                     "posterior_rho_init": -3.0, "moped_enable": True, "moped_delta": 0.1})
+    assert isinstance(net[0], Conv2dReparameterization) and isinstance(net[1], LinearReparameterization)
+    assert torch.equal(net[0].mu_kernel.detach(), w)
+    assert torch.allclose(net[0].rho_kernel.detach(), torch.log(torch.expm1(0.1 * w.abs()) + 1e-20))
+    assert net[0].dnn_to_bnn_flag and net[1].prior_variance == 1.0
+    dnn_to_bnn(net, {"prior_mu": 0.0, "prior_sigma": 1.0, "posterior_mu_init": 0.0,
+                     "posterior_rho_init": -3.0, "moped_enable": True, "moped_delta": 0.1})
+    assert isinstance(net[0], Conv2dReparameterization)  # idempotent
+
+
+def test_checkpoint_key_rewrites():
+    from mauv.checkpointing import remap_keys
+    keys = {"image_model_feat.conv1.mu_kernel": (64, 3, 7, 7), "fc2.mu_weight": (7, 32)}
+    sd = {"module.image_model_feat.model.conv1.mu_kernel": torch.zeros(64, 3, 7, 7),
+          "fc2.mu_weight": torch.zeros(5, 32), "junk": torch.zeros(1)}
+    out, skipped = remap_keys(sd, keys)
+    assert list(out) == ["image_model_feat.conv1.mu_kernel"]
+    assert len(skipped) == 2 and any("shape mismatch" in s for s in skipped)
+
+
+def test_philox_known_answers():
+    """Random123 Philox4x32-10 known-answer vectors (the generator behind every epsilon)."""
+    from oracle.philox_ref import philox4x32_10
+    r = philox4x32_10(np.array([0], dtype=np.uint64), 0, 0, 0)[0]
+    assert [hex(v) for v in r] == ["0x6627e8d5", "0xe169c58d", "0xbc57ac4c", "0x9b00dbd8"]
+    # counter (0xffffffff x4), key (0xffffffff x2)
+    r = philox4x32_10(np.array([0xFFFFFFFF], dtype=np.uint64), 0xFFFFFFFFFFFFFFFF, 0xFFFFFFFF,
+                      0xFFFFFFFFFFFFFFFF)[0]
+    assert [hex(v) for v in r] == ["0x408f276d", "0x41c83b0e", "0xa20bc7c6", "0x6d5451fd"]
+
+
+def test_kl_table_packing():
+    from mauv.kl import KLTable
+    from mauv.layers import LinearReparameterization
+    lin = LinearReparameterization(4, 3, prior_mean=0.25, prior_variance=2.0)
+    tab = KLTable([lin])
+    rows = tab._build(False, "cpu").numpy()
+    assert rows.shape == (2, 6) and rows[0, 4] == 12 and rows[1, 4] == 3
+    pm, ps = rows[0, 5:6].view(np.float32)
+    assert (pm, ps) == (0.25, 2.0)
+    assert rows[0, 0] == lin.mu_weight.data_ptr() and rows[1, 1] == lin.rho_bias.data_ptr()
+
+
+def test_engine_layer_ids_and_sample_counter():
+    from mauv.models import define_models, DEFAULT_PRIOR
+    from mauv.engine import root_state
+    m = define_models(None, 7, DEFAULT_PRIOR)["multimodal_model"]
+    st = root_state(m)
+    assert len(st.ids) == 174  # 159 convs + 15 linears
+    assert len(set(st.ids.values())) == 174
+    assert st.next_samples(5) == 0 and st.next_samples(1) == 5 and st.offset == 6
+
+
+def test_mc_shard_counts():
+    from mauv.predict import local_mc_count
+    for n in (1, 5, 100, 101):
+        for w in (1, 2, 3, 8):
+            counts = [local_mc_count(n, r, w) for r in range(w)]
+            assert sum(counts) == n and max(counts) - min(counts) <= 1
