@@ -1,0 +1,107 @@
+"""Per-shape timing of the implicit-GEMM conv kernels at the bench workload (G=5 MC groups,
+B=64, 224 optical / 256 sonar trunks).  Prints TF/s per (trunk, layer, pass) and totals.
+
+    python tools/conv_bench.py [--G 5] [--B 64] [--only fwd,dgrad,wgrad] [--top 20]
+"""
+import argparse
+import os
+import sys
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-auv_amd")]
+import torch  # noqa: E402
+from mauv import ops  # noqa: E402
+
+
+def trunk_convs(cin, S):
+    """(name, Cin, Cout, R, stride, pad, H) for every conv of a ResNet-50 trunk."""
+    out = [("stem", cin, 64, 7, 2, 3, S)]
+    H = (S + 6 - 7) // 2 + 1
+    H = (H + 2 - 3) // 2 + 1
+    inp = 64
+    for li, (planes, blocks, st) in enumerate(((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))):
+        for bi in range(blocks):
+            s = st if bi == 0 else 1
+            out.append((f"l{li+1}.{bi}.c1", inp, planes, 1, 1, 0, H))
+            out.append((f"l{li+1}.{bi}.c2", planes, planes, 3, s, 1, H))
+            H2 = (H + 2 - 3) // s + 1
+            out.append((f"l{li+1}.{bi}.c3", planes, planes * 4, 1, 1, 0, H2))
+            if bi == 0:
+                out.append((f"l{li+1}.{bi}.ds", inp, planes * 4, 1, s, 0, H))
+            inp = planes * 4
+            H = H2
+    return out
+
+
+def timeit(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--G", type=int, default=5)
+    ap.add_argument("--B", type=int, default=64)
+    ap.add_argument("--only", default="fwd,dgrad,wgrad")
+    ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--trunks", default="opt,bathy,sss")
+    a = ap.parse_args()
+    G, B, dev = a.G, a.B, "cuda"
+    kinds = a.only.split(",")
+    rows = []
+    cache = {}
+    for trunk, cin, S in (("opt", 3, 224), ("bathy", 3, 256), ("sss", 1, 256)):
+        if trunk not in a.trunks:
+            continue
+        for name, Cin, Cout, R, st, pd, H in trunk_convs(cin, S):
+            key = (Cin, Cout, R, st, pd, H)
+            Ho = ops.out_hw(H, R, st, pd)
+            fl = 2.0 * G * B * Ho * Ho * Cout * R * R * Cin
+            if key in cache:
+                for kind, ms in cache[key]:
+                    rows.append((trunk, name, kind, key, ms, fl))
+                continue
+            res = []
+            x = torch.randn(G, B, H, H, Cin, device=dev)
+            w = torch.randn(G, Cout, R, R, Cin, device=dev) * 0.05
+            y = torch.empty(G, B, Ho, Ho, Cout, device=dev)
+            if "fwd" in kinds:
+                res.append(("fwd", timeit(lambda: ops.conv2d_fwd(x, w, y, G, B, H, H, Cin, Cout, R, st, pd))))
+            if "dgrad" in kinds and name != "stem":
+                dx = torch.empty_like(x)
+                res.append(("dgrad", timeit(lambda: ops.conv2d_bwd_data(y, w, dx, G, B, H, H, Cin, Cout, R, st, pd))))
+                del dx
+            if "wgrad" in kinds:
+                sp = ops.wgrad_splits(G, B, H, H, Cin, Cout, R, st, pd)
+                ws = torch.empty(sp, G, Cout, R * R * Cin, device=dev)
+                res.append(("wgrad", timeit(lambda: ops.conv2d_bwd_weight(x, y, ws, sp, G, B, H, H, Cin, Cout, R, st, pd))))
+                del ws
+            del x, w, y
+            torch.cuda.empty_cache()
+            cache[key] = res
+            for kind, ms in res:
+                rows.append((trunk, name, kind, key, ms, fl))
+    tot = defaultdict(lambda: [0.0, 0.0])
+    for r in rows:
+        tot[r[2]][0] += r[4]
+        tot[r[2]][1] += r[5]
+    print(f"{'trunk':6s} {'layer':10s} {'pass':6s} {'Cin,Cout,R,s,p,H':28s} {'ms':>8s} {'TF/s':>7s}")
+    for r in sorted(rows, key=lambda r: -r[4])[:a.top]:
+        print(f"{r[0]:6s} {r[1]:10s} {r[2]:6s} {str(r[3]):28s} {r[4]:8.3f} {r[5] / r[4] / 1e9:7.1f}")
+    for k, (ms, fl) in tot.items():
+        print(f"TOTAL {k:6s}: {ms:8.2f} ms  {fl / 1e12:8.2f} TFLOP  {fl / ms / 1e9:6.1f} TF/s")
+    allms = sum(v[0] for v in tot.values())
+    allfl = sum(v[1] for v in tot.values())
+    print(f"TOTAL all   : {allms:8.2f} ms  {allfl / allms / 1e9:6.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()
