@@ -20,6 +20,8 @@
 // Tiles: 256 threads = 4 waves (2x2), block tile BM x BN x 16, double-buffered LDS stored
 // k-major ([k][row], rows contiguous) so each MFMA operand is one conflict-free ds_read_b32;
 // MFMA v_mfma_f32_32x32x2_f32 (exact fp32, fmaf-chain numerics).
+#include <stdlib.h>
+
 #include "mauv_common.h"
 
 namespace mauv {
@@ -41,25 +43,41 @@ struct ConvArgs {
   int accumulate;
   int G, splits, kchunk;
   int M, N, K;  // GEMM dims (per group)
+  // DGRAD output-parity class (sub-pixel decomposition): this launch computes dx for the
+  // input pixels (stride*i + ph, stride*j + pw) only, whose contributing taps are
+  // r = r0 + stride*tr (tr < nr), s = s0 + stride*ts (ts < ns) — no structurally-zero MACs.
+  int ph, pw, Hc, Wc, r0, s0, nr, ns;
 };
 
-constexpr int BK = 16;
+constexpr int BK = 16;  // host-side alignment granule (both tile depths are multiples)
 constexpr int PAD = 4;
 
-template <int MODE, int BM, int BN, bool VA, bool VB>
+template <int MODE, int BM, int BN, int BKT, bool VA, bool VB>
 __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
+  constexpr int KQ = BKT / 4;  // float4 per k-row of a k-contiguous tile row
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 32, NI = WN / 32;
-  constexpr int NVA = BM * BK / 4 / 256, NVB = BN * BK / 4 / 256;
-  __shared__ float As[2][BK][BM + PAD];
-  __shared__ float Bs[2][BK][BN + PAD];
+  constexpr int NVA = BM * BKT / 4 / 256, NVB = BN * BKT / 4 / 256;
+  __shared__ float As[2][BKT][BM + PAD];
+  __shared__ float Bs[2][BKT][BN + PAD];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // XCD-aware tile order (1-D grid over tiles): blocks are dealt round-robin to the 8 XCDs,
+  // so consecutive logical tiles are remapped onto one XCD (bijective for any grid size);
+  // logical tiles run n-fastest, so the N/BN blocks that share an A (activation) tile sit on
+  // the same XCD at the same time and hit its L2.
+  int m0, n0;
+  {
+    const int nN = (a.N + BN - 1) / BN;
+    const int b = blockIdx.x, nwg = gridDim.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    m0 = (L / nN) * BM;
+    n0 = (L - (L / nN) * nN) * BN;
+  }
   int g, sp = 0;
-  if constexpr (MODE == WGRAD) { g = blockIdx.z / a.splits; sp = blockIdx.z % a.splits; }
-  else g = blockIdx.z;
+  if constexpr (MODE == WGRAD) { g = blockIdx.y / a.splits; sp = blockIdx.y % a.splits; }
+  else g = blockIdx.y;
   int kbeg = 0, kend = a.K;
   if constexpr (MODE == WGRAD) { kbeg = sp * a.kchunk; kend = min(a.K, kbeg + a.kchunk); }
 
@@ -79,20 +97,20 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
   for (int j = 0; j < NVA; ++j) {
     const int idx = tid + 256 * j;
     if constexpr (MODE == FWD || MODE == DGRAD) {
-      const int m = m0 + (idx >> 2);
+      const int m = m0 + idx / KQ;
       a_ok[j] = m < a.M;
       const int mm = a_ok[j] ? m : 0;
-      const int HW = (MODE == FWD) ? a.Ho * a.Wo : a.H * a.W;
-      const int WW = (MODE == FWD) ? a.Wo : a.W;
+      const int HW = (MODE == FWD) ? a.Ho * a.Wo : a.Hc * a.Wc;
+      const int WW = (MODE == FWD) ? a.Wo : a.Wc;
       const int b = mm / HW, rem = mm - b * HW, oh = rem / WW, ow = rem - oh * WW;
       if constexpr (MODE == FWD) {
         a_off[j] = (long long)b * a.xs_b;
         a_p0[j] = oh * a.stride - a.pad;
         a_p1[j] = ow * a.stride - a.pad;
-      } else {
+      } else {  // (oh, ow) = class-local (i, j); ih = stride*i + ph
         a_off[j] = (long long)b * a.Ho * a.Wo * a.Cout;
-        a_p0[j] = oh + a.pad;  // ih + pad
-        a_p1[j] = ow + a.pad;
+        a_p0[j] = oh * a.stride + a.ph + a.pad;  // ih + pad
+        a_p1[j] = ow * a.stride + a.pw + a.pad;
       }
     } else {  // WGRAD: row4 fixed
       const int row = m0 + 4 * (idx % (BM / 4));
@@ -106,7 +124,7 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
   for (int j = 0; j < NVB; ++j) {
     const int idx = tid + 256 * j;
     if constexpr (MODE == FWD) {
-      const int n = n0 + (idx >> 2);
+      const int n = n0 + idx / KQ;
       b_ok[j] = n < a.N;
       b_r[j] = n;
     } else if constexpr (MODE == DGRAD) {
@@ -132,7 +150,7 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
       const int idx = tid + 256 * j;
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if constexpr (MODE == FWD) {
-        const int kq = idx & 3;
+        const int kq = idx % KQ;
         if constexpr (VA) {
           const int SC = a.S * a.Cin;
           const int r = k0 / SC, rem = k0 - r * SC, s = rem / a.Cin;
@@ -154,14 +172,16 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
           }
         }
       } else if constexpr (MODE == DGRAD) {
-        const int kq = idx & 3;
+        const int kq = idx % KQ;
+        // k = (tap t = (tr, ts), n); tap (tr, ts) -> (r0 + stride*tr, s0 + stride*ts), so
+        // ih + pad - r is a multiple of the stride by construction
         if constexpr (VA) {
-          const int SC = a.S * a.Cout;
-          const int r = k0 / SC, rem = k0 - r * SC, s = rem / a.Cout;
-          const int n = rem - s * a.Cout + 4 * kq;
-          const int ohn = a_p0[j] - r, own = a_p1[j] - s;
-          if (a_ok[j] && ohn >= 0 && own >= 0 && ohn % a.stride == 0 && own % a.stride == 0) {
-            const int oh = ohn / a.stride, ow = own / a.stride;
+          const int t = k0 / a.Cout, n = k0 - t * a.Cout + 4 * kq;
+          const int tr = t / a.ns, ts = t - tr * a.ns;
+          const int ohn = a_p0[j] - a.r0 - a.stride * tr, own = a_p1[j] - a.s0 - a.stride * ts;
+          if (a_ok[j] && ohn >= 0 && own >= 0) {
+            const int oh = a.stride == 1 ? ohn : ohn / a.stride;
+            const int ow = a.stride == 1 ? own : own / a.stride;
             if (oh < a.Ho && ow < a.Wo)
               v = *(const floatx4*)(dyg + a_off[j] + ((long long)oh * a.Wo + ow) * a.Cout + n);
           }
@@ -170,9 +190,10 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
           for (int e = 0; e < 4; ++e) {
             const int k = k0 + 4 * kq + e;
             if (a_ok[j] && k < kend) {
-              const int rs = k / a.Cout, n = k - rs * a.Cout, r = rs / a.S, s = rs - r * a.S;
-              const int ohn = a_p0[j] - r, own = a_p1[j] - s;
-              if (ohn >= 0 && own >= 0 && ohn % a.stride == 0 && own % a.stride == 0) {
+              const int t = k / a.Cout, n = k - t * a.Cout, tr = t / a.ns, ts = t - tr * a.ns;
+              const int ohn = a_p0[j] - a.r0 - a.stride * tr;
+              const int own = a_p1[j] - a.s0 - a.stride * ts;
+              if (ohn >= 0 && own >= 0) {
                 const int oh = ohn / a.stride, ow = own / a.stride;
                 if (oh < a.Ho && ow < a.Wo)
                   v[e] = dyg[a_off[j] + ((long long)oh * a.Wo + ow) * a.Cout + n];
@@ -203,7 +224,7 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
       const int idx = tid + 256 * j;
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if constexpr (MODE == FWD) {
-        const int kq = idx & 3;
+        const int kq = idx % KQ;
         const int k = k0 + 4 * kq;
         const float* src = wg + (long long)b_r[j] * a.K;
         if constexpr (VB) {
@@ -217,7 +238,8 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
         const int k = k0 + b_r[j];
         const int c = b_c[j];
         if (k < kend) {
-          const int rs = k / a.Cout, n = k - rs * a.Cout, r = rs / a.S, s = rs - r * a.S;
+          const int t = k / a.Cout, n = k - t * a.Cout, tr = t / a.ns, ts = t - tr * a.ns;
+          const int r = a.r0 + a.stride * tr, s = a.s0 + a.stride * ts;
           const float* src = wg + (((long long)n * a.R + r) * a.S + s) * a.Cin;
           if constexpr (VB) {
             if (c < a.N) v = *(const floatx4*)(src + c);
@@ -265,7 +287,7 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
         const int kr = idx / (BM / 4), r4 = idx % (BM / 4);
         *(floatx4*)&As[buf][kr][4 * r4] = ra[j];
       } else {
-        const int row = idx >> 2, kq = idx & 3;
+        const int row = idx / KQ, kq = idx % KQ;
 #pragma unroll
         for (int e = 0; e < 4; ++e) As[buf][4 * kq + e][row] = ra[j][e];
       }
@@ -274,7 +296,7 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
     for (int j = 0; j < NVB; ++j) {
       const int idx = tid + 256 * j;
       if constexpr (MODE == FWD) {
-        const int row = idx >> 2, kq = idx & 3;
+        const int row = idx / KQ, kq = idx % KQ;
 #pragma unroll
         for (int e = 0; e < 4; ++e) Bs[buf][4 * kq + e][row] = rb[j][e];
       } else {
@@ -292,7 +314,7 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
-  const int ntiles = (kend - kbeg + BK - 1) / BK;
+  const int ntiles = (kend - kbeg + BKT - 1) / BKT;
   if (ntiles > 0) {
     load_a(kbeg);
     load_b(kbeg);
@@ -303,11 +325,11 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
   for (int t = 0; t < ntiles; ++t) {
     const bool more = t + 1 < ntiles;
     if (more) {
-      load_a(kbeg + (t + 1) * BK);
-      load_b(kbeg + (t + 1) * BK);
+      load_a(kbeg + (t + 1) * BKT);
+      load_b(kbeg + (t + 1) * BKT);
     }
 #pragma unroll
-    for (int kk = 0; kk < BK / 2; ++kk) {
+    for (int kk = 0; kk < BKT / 2; ++kk) {
       float av[MI], bv[NI];
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) av[mi] = As[cur][2 * kk + lh][wm * WM + mi * 32 + li];
@@ -343,7 +365,15 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (row >= a.M) continue;
-        const long long o = (long long)row * a.N + col;
+        long long orow = row;
+        if constexpr (MODE == DGRAD) {  // class-local row -> input pixel
+          if (a.stride != 1) {
+            const int HW = a.Hc * a.Wc, b = row / HW, rem = row - b * HW;
+            const int i = rem / a.Wc, jj = rem - i * a.Wc;
+            orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
+          }
+        }
+        const long long o = orow * a.N + col;
         float v = acc[mi][ni][r] + bias;
         if constexpr (MODE == DGRAD) {
           if (a.addend) v += a.addend[(long long)g * a.out_sg + o];
@@ -354,10 +384,19 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
     }
 }
 
+static int g_bk = 0;  // tile depth: 16 or 32 (MAUV_CONV_BK; default 16)
+
 template <int MODE, int BM, int BN, bool VA, bool VB>
 static void launch(const ConvArgs& a, hipStream_t st) {
-  dim3 grid(ceil_div(a.M, BM), ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
-  hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, VA, VB>), grid, dim3(256), 0, st, a);
+  if (!g_bk) {
+    const char* e = getenv("MAUV_CONV_BK");
+    g_bk = (e && atoi(e) == 32) ? 32 : 16;  // measured: 16 wins (3 vs 2 blocks/CU)
+  }
+  dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
+  if (g_bk == 16)
+    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 32, VA, VB>), grid, dim3(256), 0, st, a);
 }
 
 template <int MODE, bool VA, bool VB>
@@ -405,7 +444,7 @@ MAUV_API int mauv_conv2d_fwd_f32(const float* x, const long long* x_strides, con
   a.x = x; a.w = w; a.out = y; a.bias = bias; a.bias_sg = Cout;
   a.M = B * a.Ho * a.Wo; a.N = Cout; a.K = R * S * Cin;
   a.out_sg = (long long)a.M * a.N;
-  const bool va = (Cin % BK == 0) && a.xs_c == 1 && (a.xs_w % 4 == 0) && (a.xs_h % 4 == 0) &&
+  const bool va = (Cin % 32 == 0) && a.xs_c == 1 && (a.xs_w % 4 == 0) && (a.xs_h % 4 == 0) &&
                   (a.xs_b % 4 == 0) && (a.xs_g % 4 == 0);
   const bool vb = (a.K % 4 == 0);
   if (va && vb) launch_tiles<FWD, true, true>(a, stream);
@@ -421,12 +460,26 @@ MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx
                                       int pad, hipStream_t stream) {
   ConvArgs a = make_args(G, B, H, W, Cin, Cout, R, S, stride, pad, nullptr);
   a.dy = dy; a.w = w; a.out = dx; a.addend = addend; a.accumulate = accumulate;
-  a.M = B * H * W; a.N = Cin; a.K = R * S * Cout;
-  a.out_sg = (long long)a.M * a.N;
-  const bool va = (Cout % BK == 0), vb = (Cin % 4 == 0);
-  if (va && vb) launch_tiles<DGRAD, true, true>(a, stream);
-  else if (vb) launch_tiles<DGRAD, false, true>(a, stream);
-  else launch_tiles<DGRAD, false, false>(a, stream);
+  a.N = Cin;
+  a.out_sg = (long long)B * H * W * Cin;
+  const bool va = (Cout % 32 == 0), vb = (Cin % 4 == 0);
+  // one launch per output-parity class (stride^2 of them; 1 for stride 1)
+  for (int ph = 0; ph < stride; ++ph)
+    for (int pw = 0; pw < stride; ++pw) {
+      a.ph = ph; a.pw = pw;
+      a.Hc = (H - ph + stride - 1) / stride;
+      a.Wc = (W - pw + stride - 1) / stride;
+      a.r0 = (ph + pad) % stride;
+      a.s0 = (pw + pad) % stride;
+      a.nr = a.r0 < R ? (R - a.r0 + stride - 1) / stride : 0;
+      a.ns = a.s0 < S ? (S - a.s0 + stride - 1) / stride : 0;
+      a.M = B * a.Hc * a.Wc;
+      a.K = a.nr * a.ns * Cout;  // 0 -> the class only receives the addend / zeros
+      if (a.M <= 0) continue;
+      if (va && vb) launch_tiles<DGRAD, true, true>(a, stream);
+      else if (vb) launch_tiles<DGRAD, false, true>(a, stream);
+      else launch_tiles<DGRAD, false, false>(a, stream);
+    }
   return check_launch("conv2d_bwd_data");
 }
 
@@ -457,7 +510,7 @@ MAUV_API int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strid
   a.x = x; a.dy = dy; a.out = ws;
   a.M = Cout; a.N = R * S * Cin; a.K = B * a.Ho * a.Wo;
   a.splits = splits;
-  a.kchunk = ((a.K + splits - 1) / splits + BK - 1) / BK * BK;
+  a.kchunk = ((a.K + splits - 1) / splits + 31) / 32 * 32;  // multiple of both tile depths
   const bool va = (Cout % 4 == 0);
   const bool vb = (Cin % 4 == 0) && a.xs_c == 1 && (a.xs_w % 4 == 0) && (a.xs_h % 4 == 0) &&
                   (a.xs_b % 4 == 0) && (a.xs_g % 4 == 0);
