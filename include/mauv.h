@@ -41,21 +41,40 @@ int mauv_abi_version(void);
  * x_strides (host pointer, nullable): element strides {group, batch, h, w, c} of x; NULL =
  * dense NHWC.  Group stride 0 = one input shared by all G samples (the stems read the
  * caller's NCHW images this way). */
-int mauv_conv2d_fwd_f32(const float* x, const long long* x_strides, const float* w,
-                        const float* bias, float* y, int G, int B, int H, int W, int Cin,
-                        int Cout, int R, int S, int stride, int pad, hipStream_t stream);
+/* x_scale/x_shift (nullable, [G][Cin]) + x_relu: the producing layer's BatchNorm(+ReLU)
+ * applied while loading x (its normalised activation is never stored).
+ * st_mean/st_m2/st_cnt (nullable): per-m-tile BatchNorm statistics of y written by the
+ * epilogue ([G][nblk][Cout], [G][nblk][Cout], [G][nblk]; nblk from
+ * mauv_conv2d_fwd_stat_blocks) for mauv_bn_stats_finalize. */
+int mauv_conv2d_fwd_f32(const float* x, const long long* x_strides, const float* x_scale,
+                        const float* x_shift, int x_relu, const float* w, const float* bias,
+                        float* y, int G, int B, int H, int W, int Cin, int Cout, int R, int S,
+                        int stride, int pad, float* st_mean, float* st_m2, float* st_cnt,
+                        hipStream_t stream);
+int mauv_conv2d_fwd_stat_blocks(int G, int B, int H, int W, int Cin, int Cout, int R, int S,
+                                int stride, int pad);
 /* cuDNN dgrad in loss.backward() (train/multimodal.py:138): dx = conv^T(dy, W_g)
- * (+ addend) (+ dx if accumulate). */
+ * (+ addend) (+ dx if accumulate); one launch per output-parity class (stride^2).
+ * bn_* (nullable): dx is the output gradient of a BatchNorm(+ReLU) whose backward partial
+ * sums (sum dz, sum dz*xhat per channel; [G][nblk][Cin], nblk from
+ * mauv_conv2d_bwd_data_stat_blocks) the epilogue writes for mauv_bn_bwd's pre_p1/pre_p2;
+ * the ReLU mask comes from bn_out, else from bn_y*bn_scale+bn_shift. */
 int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx, const float* addend,
                              int accumulate, int G, int B, int H, int W, int Cin, int Cout,
-                             int R, int S, int stride, int pad, hipStream_t stream);
+                             int R, int S, int stride, int pad, const float* bn_y,
+                             const float* bn_out, const float* bn_scale, const float* bn_shift,
+                             const float* bn_mean, const float* bn_invstd, int bn_relu,
+                             float* bn_p1, float* bn_p2, hipStream_t stream);
+int mauv_conv2d_bwd_data_stat_blocks(int G, int B, int H, int W, int Cin, int Cout, int R,
+                                     int S, int stride, int pad);
 /* cuDNN wgrad (train/multimodal.py:138): split-K partial slabs ws[splits][G][Cout][R*S*Cin],
  * reduced deterministically by mauv_reparam_bwd.  mauv_conv2d_wgrad_splits sizes them. */
 int mauv_conv2d_wgrad_splits(int G, int B, int H, int W, int Cin, int Cout, int R, int S,
                              int stride, int pad);
-int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strides, const float* dy,
-                               float* ws, int splits, int G, int B, int H, int W, int Cin,
-                               int Cout, int R, int S, int stride, int pad, hipStream_t stream);
+int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strides, const float* x_scale,
+                               const float* x_shift, int x_relu, const float* dy, float* ws,
+                               int splits, int G, int B, int H, int W, int Cin, int Cout, int R,
+                               int S, int stride, int pad, hipStream_t stream);
 
 /* ---- variational sampling / KL (reparam.hip) --------------------------------------------
  * bayesian-torch Conv2dReparameterization/LinearReparameterization.forward:
@@ -108,15 +127,27 @@ int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const float* ga
                       float eps, float* workspace, float* mean, float* invstd, float* scale,
                       float* shift, const float* res, int relu, float* out,
                       hipStream_t stream);
+/* statistics from per-m-tile partials written by mauv_conv2d_fwd_f32's epilogue: Chan merge,
+ * mean/invstd/scale/shift [G][C], sequential running-stat update (run_* nullable);
+ * workspace: G*C floats */
+int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, const float* pm2,
+                           const float* pcnt, const float* gamma, const float* beta,
+                           float* run_mean, float* run_var, float momentum, float eps,
+                           float* workspace, float* mean, float* invstd, float* scale,
+                           float* shift, hipStream_t stream);
 int mauv_bn_apply(const float* y, const float* scale, const float* shift, const float* res,
                   int relu, float* out, int G, long long M, int C, hipStream_t stream);
 int mauv_bn_eval_params(int G, int C, const float* gamma, const float* beta,
                         const float* run_mean, const float* run_var, float eps, float* scale,
                         float* shift, hipStream_t stream);
+/* out NULL + relu: the mask is recomputed as y*scale + shift > 0 (lazily-applied BN).
+ * pre_p1/pre_p2 (nullable): partial sums already produced by a dgrad epilogue
+ * ([G][pre_nblk][C]) — the partial pass over dout is skipped. */
 int mauv_bn_bwd(const float* y, const float* out, const float* dout, int relu,
-                const float* mean, const float* invstd, const float* scale, int G, long long M,
-                int C, float* workspace, float* dy, float* dres, float* dgamma, float* dbeta,
-                hipStream_t stream);
+                const float* mean, const float* invstd, const float* scale, const float* shift,
+                int G, long long M, int C, float* workspace, float* dy, float* dres,
+                float* dgamma, float* dbeta, const float* pre_p1, const float* pre_p2,
+                int pre_nblk, hipStream_t stream);
 
 /* ---- pooling (pool.hip): torchvision stem maxpool 3x3/2 pad 1 and adaptive avgpool ------ */
 int mauv_maxpool_fwd(const float* x, int N, int H, int W, int C, float* y, unsigned char* idx,

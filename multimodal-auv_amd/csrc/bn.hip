@@ -181,6 +181,19 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
   }
 }
 
+// ReLU mask of the BN output: from the stored output when there is one (residual blocks),
+// else recomputed from y (lazily-applied BN: out = relu(y*scale + shift) was never stored).
+__device__ __forceinline__ floatx4 relu_mask(floatx4 dz, const float* out, long long o,
+                                             floatx4 yv, const float* scale,
+                                             const float* shift, int gc) {
+  floatx4 pre;
+  if (out) pre = *(const floatx4*)(out + o);
+  else pre = yv * *(const floatx4*)(scale + gc) + *(const floatx4*)(shift + gc);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) dz[e] = pre[e] > 0.f ? dz[e] : 0.f;
+  return dz;
+}
+
 // Backward stage 1: per (g, block) partial sums of dz and dz*xhat per channel,
 // dz = dout * (relu ? out > 0 : 1), xhat = (y - mean) * invstd.
 __global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ y,
@@ -188,6 +201,8 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ 
                                                       const float* __restrict__ dout, int relu,
                                                       const float* __restrict__ mean,
                                                       const float* __restrict__ invstd,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift,
                                                       long long M, int C, int rpb, RowMap rm,
                                                       float* __restrict__ p1,
                                                       float* __restrict__ p2) {
@@ -214,11 +229,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ 
       const long long o = go + r * C + 4 * (t_c + j * rm.tpr);
       const floatx4 yv = *(const floatx4*)(y + o);
       floatx4 dz = *(const floatx4*)(dout + o);
-      if (relu) {
-        const floatx4 ov = *(const floatx4*)(out + o);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dz[e] = ov[e] > 0.f ? dz[e] : 0.f;
-      }
+      if (relu) dz = relu_mask(dz, out, o, yv, scale, shift, g * C + 4 * (t_c + j * rm.tpr));
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         s1[j][e] += dz[e];
@@ -293,6 +304,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ y,
                                                     const float* __restrict__ mean,
                                                     const float* __restrict__ invstd,
                                                     const float* __restrict__ scale,
+                                                    const float* __restrict__ shift,
                                                     const float* __restrict__ k1,
                                                     const float* __restrict__ k2,
                                                     float* __restrict__ dy,
@@ -305,12 +317,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ y,
     const int c = 4 * (int)(i % c4n);
     const long long o = go + 4 * i;
     floatx4 dz = *(const floatx4*)(dout + o);
-    if (relu) {
-      const floatx4 ov = *(const floatx4*)(out + o);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) dz[e] = ov[e] > 0.f ? dz[e] : 0.f;
-    }
     const floatx4 yv = *(const floatx4*)(y + o);
+    if (relu) dz = relu_mask(dz, out, o, yv, scale, shift, g * C + c);
     const floatx4 mu = *(const floatx4*)(mean + g * C + c);
     const floatx4 is = *(const floatx4*)(invstd + g * C + c);
     const floatx4 sc = *(const floatx4*)(scale + g * C + c);
@@ -398,6 +406,21 @@ MAUV_API int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const 
   return check_launch("bn_fwd_train");
 }
 
+// Statistics from per-m-tile partials of the fused conv epilogue (conv_gemm.hip).
+MAUV_API int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, const float* pm2,
+                                    const float* pcnt, const float* gamma, const float* beta,
+                                    float* run_mean, float* run_var, float momentum, float eps,
+                                    float* workspace, float* mean, float* invstd, float* scale,
+                                    float* shift, hipStream_t stream) {
+  if (G <= 0 || nblk <= 0 || C <= 0) { set_error("bn_stats_finalize: bad shape"); return kErrArg; }
+  hipLaunchKernelGGL(bn_stats_final, dim3((C + 63) / 64, G), dim3(256), 0, stream, G, nblk, C,
+                     pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift, workspace);
+  if (run_mean && run_var)
+    hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
+                       mean, workspace, run_mean, run_var, momentum);
+  return check_launch("bn_stats_finalize");
+}
+
 // out = [relu](y * scale + shift (+ res)) with precomputed per-group scale/shift.
 MAUV_API int mauv_bn_apply(const float* y, const float* scale, const float* shift,
                            const float* res, int relu, float* out, int G, long long M, int C,
@@ -411,10 +434,13 @@ MAUV_API int mauv_bn_apply(const float* y, const float* scale, const float* shif
 //   dy = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)),  dres = dz (nullable),
 //   dgamma += sum dz*xhat, dbeta += sum dz (over all groups; nullable).
 MAUV_API int mauv_bn_bwd(const float* y, const float* out, const float* dout, int relu,
-                         const float* mean, const float* invstd, const float* scale, int G,
-                         long long M, int C, float* workspace, float* dy, float* dres,
-                         float* dgamma, float* dbeta, hipStream_t stream) {
+                         const float* mean, const float* invstd, const float* scale,
+                         const float* shift, int G, long long M, int C, float* workspace,
+                         float* dy, float* dres, float* dgamma, float* dbeta,
+                         const float* pre_p1, const float* pre_p2, int pre_nblk,
+                         hipStream_t stream) {
   if (C % 4 != 0 || C > 2048) { set_error("bn_bwd: unsupported C"); return kErrArg; }
+  if (relu && !out && !shift) { set_error("bn_bwd: relu mask needs out or scale/shift"); return kErrArg; }
   int nblk, rpb;
   reduce_geometry(M, C, nblk, rpb);
   const RowMap rm = row_map(C);
@@ -422,14 +448,19 @@ MAUV_API int mauv_bn_bwd(const float* y, const float* out, const float* dout, in
   float* p2 = p1 + (long long)G * nblk * C;
   float* k1 = p2 + (long long)G * nblk * C;
   float* k2 = k1 + (long long)G * C;
-  hipLaunchKernelGGL(bn_bwd_partial, dim3(nblk, G), dim3(256), 0, stream, y, out, dout, relu,
-                     mean, invstd, M, C, rpb, rm, p1, p2);
-  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(256), 0, stream, G, nblk, C, M,
-                     p1, p2, k1, k2);
+  if (pre_p1) {  // partial sums already produced by the dgrad epilogue (conv_gemm.hip)
+    hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(256), 0, stream, G, pre_nblk,
+                       C, M, pre_p1, pre_p2, k1, k2);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_partial, dim3(nblk, G), dim3(256), 0, stream, y, out, dout, relu,
+                       mean, invstd, scale, shift, M, C, rpb, rm, p1, p2);
+    hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(256), 0, stream, G, nblk, C,
+                       M, p1, p2, k1, k2);
+  }
   if (dgamma || dbeta)
     hipLaunchKernelGGL(bn_bwd_param_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C, M,
                        k1, k2, dgamma, dbeta);
   hipLaunchKernelGGL(bn_bwd_apply, dim3(ew_grid(M * C / 4), G), dim3(256), 0, stream, y, out,
-                     dout, relu, mean, invstd, scale, k1, k2, dy, dres, M, C);
+                     dout, relu, mean, invstd, scale, shift, k1, k2, dy, dres, M, C);
   return check_launch("bn_bwd");
 }

@@ -47,7 +47,30 @@ struct ConvArgs {
   // input pixels (stride*i + ph, stride*j + pw) only, whose contributing taps are
   // r = r0 + stride*tr (tr < nr), s = s0 + stride*ts (ts < ns) — no structurally-zero MACs.
   int ph, pw, Hc, Wc, r0, s0, nr, ns;
+  // optional per-(group, channel) transform of x on load: x' = [relu](x*xsc + xsh) — the
+  // pending BatchNorm(+ReLU) of the producing layer, applied lazily so that layer's
+  // normalised activation is never written to HBM (FWD A-loader, WGRAD B-loader)
+  const float* xsc;
+  const float* xsh;
+  int xrelu;
+  // FWD epilogue BN statistics partials [G][st_nblk][N] (+ counts [G][st_nblk])
+  float *st_mean, *st_m2, *st_cnt;
+  int st_nblk, st_base;
+  // DGRAD epilogue BN-backward partials [G][bp_nblk][N]: sum dz, sum dz*xhat
+  const float *bp_y, *bp_out, *bp_sc, *bp_sh, *bp_mean, *bp_invstd;
+  int bp_relu;
+  float *bp_p1, *bp_p2;
+  int bp_nblk, bp_base;
 };
+
+__device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int relu) {
+  v = v * sc + sh;
+  if (relu) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+  }
+  return v;
+}
 
 constexpr int BK = 16;  // host-side alignment granule (both tile depths are multiples)
 constexpr int PAD = 4;
@@ -143,6 +166,16 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
   }
 
   floatx4 ra[NVA], rb[NVB];
+  floatx4 bsc[NVB], bsh[NVB];  // WGRAD: per-thread channel transform (fixed columns)
+  if constexpr (MODE == WGRAD && VB) {
+#pragma unroll
+    for (int j = 0; j < NVB; ++j) {
+      if (a.xsc && b_ok[j]) {
+        bsc[j] = *(const floatx4*)(a.xsc + g * a.Cin + b_c[j]);
+        bsh[j] = *(const floatx4*)(a.xsh + g * a.Cin + b_c[j]);
+      }
+    }
+  }
 
   auto load_a = [&](int k0) {
 #pragma unroll
@@ -156,8 +189,12 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
           const int r = k0 / SC, rem = k0 - r * SC, s = rem / a.Cin;
           const int c = rem - s * a.Cin + 4 * kq;
           const int ih = a_p0[j] + r, iw = a_p1[j] + s;
-          if (a_ok[j] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+          if (a_ok[j] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
             v = *(const floatx4*)(xg + a_off[j] + (long long)ih * a.xs_h + (long long)iw * a.xs_w + c);
+            if (a.xsc)
+              v = bn_act(v, *(const floatx4*)(a.xsc + g * a.Cin + c),
+                         *(const floatx4*)(a.xsh + g * a.Cin + c), a.xrelu);
+          }
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -256,9 +293,11 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
           const int b = p / HW, rem = p - b * HW, oh = rem / a.Wo, ow = rem - oh * a.Wo;
           if constexpr (VB) {
             const int ih = oh * a.stride - a.pad + b_r[j], iw = ow * a.stride - a.pad + b_s[j];
-            if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+            if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
               v = *(const floatx4*)(xg + (long long)b * a.xs_b + (long long)ih * a.xs_h +
                                     (long long)iw * a.xs_w + b_c[j]);
+              if (a.xsc) v = bn_act(v, bsc[j], bsh[j], a.xrelu);
+            }
           } else {
             const int col0 = n0 + 4 * (idx % (BN / 4));
 #pragma unroll
@@ -352,6 +391,18 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
     outg = a.out + ((long long)sp * a.G + g) * ((long long)a.M * a.N);
   else
     outg = a.out + (long long)g * a.out_sg;
+  // Fused BatchNorm reductions (per block tile, per column = channel), written as per-m-tile
+  // partials that bn.hip's finalize kernels merge — the standalone statistics passes over y
+  // (forward) and over dx (backward) disappear:
+  //   FWD   + st_mean: tile-local (count, mean, M2) of y (two register passes, Welford-exact)
+  //   DGRAD + bp_p1  : sum dz and sum dz*xhat of the BN whose output gradient this dx is
+  //                    (dz = dx * relu-mask; mask/xhat from that BN's y and statistics)
+  const bool fst = (MODE == FWD) && a.st_mean;
+  const bool bst = (MODE == DGRAD) && a.bp_p1;
+  float s1[NI], s2[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) { s1[ni] = 0.f; s2[ni] = 0.f; }
+  const int nvalid = min(BM, a.M - m0);
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -361,6 +412,14 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
       float bias = 0.f;
       if constexpr (MODE == FWD)
         if (a.bias) bias = a.bias[(long long)g * a.bias_sg + col];
+      float bmu = 0.f, bis = 0.f, bsc = 0.f, bsh = 0.f;
+      if constexpr (MODE == DGRAD) {
+        if (bst) {
+          bmu = a.bp_mean[g * a.N + col];
+          bis = a.bp_invstd[g * a.N + col];
+          if (!a.bp_out) { bsc = a.bp_sc[g * a.N + col]; bsh = a.bp_sh[g * a.N + col]; }
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -378,10 +437,76 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
         if constexpr (MODE == DGRAD) {
           if (a.addend) v += a.addend[(long long)g * a.out_sg + o];
           if (a.accumulate) v += outg[o];
+          if (bst) {
+            const long long go = (long long)g * a.out_sg + o;
+            const float yv = a.bp_y[go];
+            const float pre = a.bp_out ? a.bp_out[go] : yv * bsc + bsh;
+            const float dz = (!a.bp_relu || pre > 0.f) ? v : 0.f;
+            s1[ni] += dz;
+            s2[ni] += dz * (yv - bmu) * bis;
+          }
         }
+        if constexpr (MODE == FWD) s1[ni] += v;
         outg[o] = v;
       }
     }
+  if (fst || bst) {
+    float* red = &As[0][0][0];  // LDS is free: the main loop ended with a barrier
+    const int tcol = wn * WN + li;  // + ni*32
+    // column totals of s1 over the block tile: lane halves, then the two wm waves
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) s1[ni] += __shfl_xor(s1[ni], 32, 64);
+    if (lh == 0) {
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) red[wm * BN + tcol + ni * 32] = s1[ni];
+    }
+    __syncthreads();
+    if (fst) {
+      // pass 2: M2 around the tile mean
+      float mean[NI];
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+        mean[ni] = (red[tcol + ni * 32] + red[BN + tcol + ni * 32]) / (float)nvalid;
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) s2[ni] = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          const int col = n0 + wn * WN + ni * 32 + li;
+          const float bias = (a.bias && col < a.N) ? a.bias[(long long)g * a.bias_sg + col] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (row < a.M) {
+              const float d = acc[mi][ni][r] + bias - mean[ni];
+              s2[ni] += d * d;
+            }
+          }
+        }
+    }
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) s2[ni] += __shfl_xor(s2[ni], 32, 64);
+    if (lh == 0) {
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) red[2 * BN + wm * BN + tcol + ni * 32] = s2[ni];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N) {
+      const float t1 = red[tid] + red[BN + tid], t2 = red[2 * BN + tid] + red[3 * BN + tid];
+      const int mt = m0 / BM;
+      if (fst) {
+        const long long so = ((long long)g * a.st_nblk + a.st_base + mt) * a.N + n0 + tid;
+        a.st_mean[so] = t1 / (float)nvalid;
+        a.st_m2[so] = t2;
+        if (n0 + tid == 0) a.st_cnt[(long long)g * a.st_nblk + a.st_base + mt] = (float)nvalid;
+      } else {
+        const long long so = ((long long)g * a.bp_nblk + a.bp_base + mt) * a.N + n0 + tid;
+        a.bp_p1[so] = t1;
+        a.bp_p2[so] = t2;
+      }
+    }
+  }
 }
 
 static int g_bk = 0;  // tile depth: 16 or 32 (MAUV_CONV_BK; default 16)
@@ -414,6 +539,18 @@ static void launch_tiles(const ConvArgs& a, hipStream_t st) {
 
 using namespace mauv;
 
+// m-tiles of a launch (launch_tiles picks BM = 64 for M <= 64, else 128)
+static int stat_blocks(int M) { return ceil_div(M, M <= 64 ? 64 : 128); }
+static int dgrad_stat_blocks(int B, int H, int W, int stride) {
+  int n = 0;
+  for (int ph = 0; ph < stride; ++ph)
+    for (int pw = 0; pw < stride; ++pw) {
+      const int M = B * ((H - ph + stride - 1) / stride) * ((W - pw + stride - 1) / stride);
+      if (M > 0) n += stat_blocks(M);
+    }
+  return n;
+}
+
 static ConvArgs make_args(int G, int B, int H, int W, int Cin, int Cout, int R, int S,
                           int stride, int pad, const long long* xs) {
   ConvArgs a{};
@@ -435,18 +572,24 @@ static ConvArgs make_args(int G, int B, int H, int W, int Cin, int Cout, int R, 
 // x_strides (nullable): element strides {group, batch, h, w, c} of x; NULL = dense NHWC.
 // Replaces F.conv2d in bayesian-torch Conv2dReparameterization.forward / F.linear in
 // LinearReparameterization.forward (a linear is the 1x1 case with H=W=1).
-MAUV_API int mauv_conv2d_fwd_f32(const float* x, const long long* x_strides, const float* w,
-                                 const float* bias, float* y, int G, int B, int H, int W,
-                                 int Cin, int Cout, int R, int S, int stride, int pad,
+MAUV_API int mauv_conv2d_fwd_f32(const float* x, const long long* x_strides,
+                                 const float* x_scale, const float* x_shift, int x_relu,
+                                 const float* w, const float* bias, float* y, int G, int B,
+                                 int H, int W, int Cin, int Cout, int R, int S, int stride,
+                                 int pad, float* st_mean, float* st_m2, float* st_cnt,
                                  hipStream_t stream) {
   if (G <= 0 || B <= 0 || Cin <= 0 || Cout <= 0) { set_error("conv2d_fwd: bad shape"); return kErrArg; }
   ConvArgs a = make_args(G, B, H, W, Cin, Cout, R, S, stride, pad, x_strides);
   a.x = x; a.w = w; a.out = y; a.bias = bias; a.bias_sg = Cout;
+  a.xsc = x_scale; a.xsh = x_shift; a.xrelu = x_relu;
   a.M = B * a.Ho * a.Wo; a.N = Cout; a.K = R * S * Cin;
   a.out_sg = (long long)a.M * a.N;
+  a.st_mean = st_mean; a.st_m2 = st_m2; a.st_cnt = st_cnt;
+  a.st_nblk = stat_blocks(a.M); a.st_base = 0;
   const bool va = (Cin % 32 == 0) && a.xs_c == 1 && (a.xs_w % 4 == 0) && (a.xs_h % 4 == 0) &&
                   (a.xs_b % 4 == 0) && (a.xs_g % 4 == 0);
   const bool vb = (a.K % 4 == 0);
+  if (x_scale && !(va && vb)) { set_error("conv2d_fwd: x transform needs the vector path"); return kErrArg; }
   if (va && vb) launch_tiles<FWD, true, true>(a, stream);
   else if (vb) launch_tiles<FWD, false, true>(a, stream);
   else launch_tiles<FWD, false, false>(a, stream);
@@ -457,11 +600,20 @@ MAUV_API int mauv_conv2d_fwd_f32(const float* x, const long long* x_strides, con
 MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx,
                                       const float* addend, int accumulate, int G, int B, int H,
                                       int W, int Cin, int Cout, int R, int S, int stride,
-                                      int pad, hipStream_t stream) {
+                                      int pad, const float* bn_y, const float* bn_out,
+                                      const float* bn_scale, const float* bn_shift,
+                                      const float* bn_mean, const float* bn_invstd, int bn_relu,
+                                      float* bn_p1, float* bn_p2, hipStream_t stream) {
   ConvArgs a = make_args(G, B, H, W, Cin, Cout, R, S, stride, pad, nullptr);
   a.dy = dy; a.w = w; a.out = dx; a.addend = addend; a.accumulate = accumulate;
   a.N = Cin;
   a.out_sg = (long long)B * H * W * Cin;
+  a.bp_y = bn_y; a.bp_out = bn_out; a.bp_sc = bn_scale; a.bp_sh = bn_shift;
+  a.bp_mean = bn_mean; a.bp_invstd = bn_invstd; a.bp_relu = bn_relu;
+  a.bp_p1 = bn_p1; a.bp_p2 = bn_p2;
+  a.bp_nblk = dgrad_stat_blocks(B, H, W, stride);
+  a.bp_base = 0;
+  if (bn_p1 && bn_relu && !bn_out && !bn_shift) { set_error("conv2d_bwd_data: mask source"); return kErrArg; }
   const bool va = (Cout % 32 == 0), vb = (Cin % 4 == 0);
   // one launch per output-parity class (stride^2 of them; 1 for stride 1)
   for (int ph = 0; ph < stride; ++ph)
@@ -479,8 +631,20 @@ MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx
       if (va && vb) launch_tiles<DGRAD, true, true>(a, stream);
       else if (vb) launch_tiles<DGRAD, false, true>(a, stream);
       else launch_tiles<DGRAD, false, false>(a, stream);
+      a.bp_base += stat_blocks(a.M);
     }
   return check_launch("conv2d_bwd_data");
+}
+
+// Number of per-m-tile BN statistic partials the fused epilogues write (host sizing helpers).
+MAUV_API int mauv_conv2d_fwd_stat_blocks(int G, int B, int H, int W, int Cin, int Cout, int R,
+                                         int S, int stride, int pad) {
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  return stat_blocks(B * Ho * Wo);
+}
+MAUV_API int mauv_conv2d_bwd_data_stat_blocks(int G, int B, int H, int W, int Cin, int Cout,
+                                              int R, int S, int stride, int pad) {
+  return dgrad_stat_blocks(B, H, W, stride);
 }
 
 // Split count used by mauv_conv2d_bwd_weight for a given problem (host helper so the caller
@@ -503,17 +667,20 @@ MAUV_API int mauv_conv2d_wgrad_splits(int G, int B, int H, int W, int Cin, int C
 
 // Weight gradient partial slabs: ws[split][g][Cout][R*S*Cin] (reduced by mauv_reparam_bwd).
 MAUV_API int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strides,
+                                        const float* x_scale, const float* x_shift, int x_relu,
                                         const float* dy, float* ws, int splits, int G, int B,
                                         int H, int W, int Cin, int Cout, int R, int S,
                                         int stride, int pad, hipStream_t stream) {
   ConvArgs a = make_args(G, B, H, W, Cin, Cout, R, S, stride, pad, x_strides);
   a.x = x; a.dy = dy; a.out = ws;
+  a.xsc = x_scale; a.xsh = x_shift; a.xrelu = x_relu;
   a.M = Cout; a.N = R * S * Cin; a.K = B * a.Ho * a.Wo;
   a.splits = splits;
   a.kchunk = ((a.K + splits - 1) / splits + 31) / 32 * 32;  // multiple of both tile depths
   const bool va = (Cout % 4 == 0);
   const bool vb = (Cin % 4 == 0) && a.xs_c == 1 && (a.xs_w % 4 == 0) && (a.xs_h % 4 == 0) &&
                   (a.xs_b % 4 == 0) && (a.xs_g % 4 == 0);
+  if (x_scale && !(va && vb)) { set_error("conv2d_bwd_weight: x transform needs the vector path"); return kErrArg; }
   if (va && vb) launch_tiles<WGRAD, true, true>(a, stream);
   else if (va) launch_tiles<WGRAD, true, false>(a, stream);
   else launch_tiles<WGRAD, false, false>(a, stream);

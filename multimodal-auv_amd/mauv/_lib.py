@@ -25,10 +25,12 @@ SIGNATURES = {
     "mauv_abi_version": [],
     "mauv_last_error": [],
     # conv_gemm.hip
-    "mauv_conv2d_fwd_f32": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
-    "mauv_conv2d_bwd_data_f32": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
+    "mauv_conv2d_fwd_f32": [P, P, P, P, I, P, P, P] + [I] * 10 + [P, P, P, P],
+    "mauv_conv2d_fwd_stat_blocks": [I] * 10,
+    "mauv_conv2d_bwd_data_f32": [P, P, P, P] + [I] * 11 + [P] * 6 + [I, P, P, P],
+    "mauv_conv2d_bwd_data_stat_blocks": [I] * 10,
     "mauv_conv2d_wgrad_splits": [I, I, I, I, I, I, I, I, I, I],
-    "mauv_conv2d_bwd_weight_f32": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
+    "mauv_conv2d_bwd_weight_f32": [P, P, P, P, I, P, P] + [I] * 11 + [P],
     # reparam.hip
     "mauv_reparam_sample": [P, P, P, U64, U64, U32, I, I, I, I, P, LL, P],
     "mauv_reparam_bwd": [P, I, LL, LL, P, P, P, U64, U64, U32, I, I, I, I, P, P, LL, P],
@@ -39,9 +41,10 @@ SIGNATURES = {
     # bn.hip
     "mauv_bn_workspace_floats": [I, LL, I],
     "mauv_bn_fwd_train": [P, I, LL, I, P, P, P, P, F, F, P, P, P, P, P, P, I, P, P],
+    "mauv_bn_stats_finalize": [I, I, I, P, P, P, P, P, P, P, F, F, P, P, P, P, P, P],
     "mauv_bn_apply": [P, P, P, P, I, P, I, LL, I, P],
     "mauv_bn_eval_params": [I, I, P, P, P, P, F, P, P, P],
-    "mauv_bn_bwd": [P, P, P, I, P, P, P, I, LL, I, P, P, P, P, P, P],
+    "mauv_bn_bwd": [P, P, P, I, P, P, P, P, I, LL, I, P, P, P, P, P, P, P, I, P],
     # pool.hip
     "mauv_maxpool_fwd": [P, I, I, I, I, P, P, P],
     "mauv_maxpool_bwd": [P, P, I, I, I, I, P, P],

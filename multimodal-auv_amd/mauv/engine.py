@@ -181,84 +181,141 @@ class _Runner:
 
 
 # ----------------------------------------------------------------------------- trunk
+class _BN:
+    """Saved state of one BatchNorm (+ReLU) for the backward."""
+    __slots__ = ("bn", "y", "out", "stats", "relu", "M", "C", "batch_stats")
+
+    def __init__(self, bn, y, out, stats, relu, M, C, batch_stats):
+        self.bn, self.y, self.out, self.stats, self.relu = bn, y, out, stats, relu
+        self.M, self.C, self.batch_stats = M, C, batch_stats
+
+    @property
+    def scale(self):
+        return self.stats[2]
+
+    @property
+    def shift(self):
+        return self.stats[3]
+
+    def lazy(self):
+        """(scale, shift, relu) for a consumer that applies this BN on load."""
+        return (self.stats[2], self.stats[3], int(self.relu))
+
+    def epilogue_args(self, G, dgrad_shape):
+        """Arguments for a dgrad whose output is this BN's output gradient: the epilogue then
+        writes this BN's backward partial sums (returned as pre=(p1, p2, nblk))."""
+        nblk = ops.dgrad_stat_blocks(G, *dgrad_shape)
+        p = torch.empty(2, G, nblk, self.C, device=self.y.device)
+        args = dict(y=self.y, out=self.out, scale=self.stats[2], shift=self.stats[3],
+                    mean=self.stats[0], invstd=self.stats[1], relu=int(self.relu),
+                    p1=p[0], p2=p[1])
+        return args, (p[0], p[1], nblk)
+
+
 class TrunkRunner(_Runner):
-    """torchvision ResNet-50 trunk (Bayesian convs, train-mode BN) for G MC samples."""
+    """torchvision ResNet-50 trunk (Bayesian convs, train-mode BN) for G MC samples.
+
+    Fusions (numerically the same BN/ReLU maths, fewer HBM passes):
+    * BN statistics come from the producing conv's epilogue (per-m-tile Welford partials);
+    * bn1/bn2 of every bottleneck are never materialised: conv2/conv3 apply
+      relu(y*scale + shift) while loading their input (forward and weight-gradient), and their
+      backward rebuilds the ReLU mask from y;
+    * the backward partial sums of each BN come from the epilogue of the dgrad that produces
+      its output gradient.
+    """
 
     def __init__(self, trunk, state, G, sample0, save):
         super().__init__(state, G, sample0, save)
         self.trunk = trunk
 
     # ---- conv / bn units ----
-    def _conv(self, conv, x, B, H, W, x_strides=None):
+    def _conv(self, conv, x, B, H, W, x_strides=None, x_bn=None, bn_stats=True):
         G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
         st, pd = conv.stride[0], conv.padding[0]
         w = torch.empty(G, Cout, k, k, Cin, device=x.device)
         self._sample(conv, conv.mu_kernel, conv.rho_kernel, "kernel", w, Cout, Cin, k * k)
         Ho, Wo = ops.out_hw(H, k, st, pd), ops.out_hw(W, k, st, pd)
         y = torch.empty(G, B, Ho, Wo, Cout, device=x.device)
-        ops.conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, k, st, pd, x_strides=x_strides)
-        rec = (conv, x, x_strides, w, B, H, W) if self.save else None
-        return y, rec
+        part = None
+        if bn_stats:
+            nblk = ops.fwd_stat_blocks(G, B, H, W, Cin, Cout, k, st, pd)
+            buf = torch.empty(2 * G * nblk * Cout + G * nblk, device=x.device)
+            part = (buf[:G * nblk * Cout], buf[G * nblk * Cout:2 * G * nblk * Cout],
+                    buf[2 * G * nblk * Cout:], nblk)
+        ops.conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, k, st, pd, x_strides=x_strides,
+                       x_bn=x_bn, stats=None if part is None else part[:3])
+        rec = (conv, x, x_strides, x_bn, w, B, H, W) if self.save else None
+        return y, rec, part
 
-    def _conv_bwd(self, rec, dy, need_dx=True, addend=None, dx=None, accumulate=False):
-        conv, x, xs, w, B, H, W = rec
+    def _conv_bwd(self, rec, dy, need_dx=True, addend=None, dx=None, accumulate=False,
+                  bn_out=None):
+        """bn_out: the _BN whose output gradient dx is (its partials come back as `pre`)."""
+        conv, x, xs, x_bn, w, B, H, W = rec
         G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
         st, pd = conv.stride[0], conv.padding[0]
         if conv.mu_kernel.requires_grad:
             splits = ops.wgrad_splits(G, B, H, W, Cin, Cout, k, st, pd)
             ws = torch.empty(splits, G, Cout, k * k * Cin, device=dy.device)
             ops.conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, k, st, pd,
-                                  x_strides=xs)
+                                  x_strides=xs, x_bn=x_bn)
             self._reparam_bwd(conv, conv.mu_kernel, conv.rho_kernel, ws, splits, Cout, Cin,
                               k * k, "kernel")
             del ws
         if not need_dx:
-            return None
+            return None, None
         if dx is None:
             dx = torch.empty(G, B, H, W, Cin, device=dy.device)
+        bn_args, pre = (None, None)
+        if bn_out is not None and bn_out.batch_stats:
+            bn_args, pre = bn_out.epilogue_args(G, (B, H, W, Cin, Cout, k, st, pd))
         ops.conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, k, st, pd, addend=addend,
-                            accumulate=accumulate)
-        return dx
+                            accumulate=accumulate, bn=bn_args)
+        return dx, pre
 
-    def _bn(self, bn, y, relu, res=None):
+    def _bn(self, bn, y, part, relu, res=None, materialize=True):
+        """Statistics (from the conv epilogue partials) + optional materialised output."""
         G, C = self.G, y.shape[-1]
         M = y.numel() // (G * C)
-        out = torch.empty_like(y)
         stats = torch.empty(4, G, C, device=y.device)
         mean, invstd, scale, shift = stats[0], stats[1], stats[2], stats[3]
-        if bn.training or not bn.track_running_stats:
+        batch_stats = bn.training or not bn.track_running_stats
+        if batch_stats:
             if bn.momentum is None:
                 raise NotImplementedError("mauv: cumulative-average BN (momentum=None)")
-            ws = torch.empty(ops.bn_workspace_floats(G, M, C), device=y.device)
             track = bn.training and bn.track_running_stats
-            ops.bn_fwd_train(y, G, M, C, bn.weight, bn.bias,
-                             bn.running_mean if track else None,
-                             bn.running_var if track else None, bn.momentum, bn.eps, ws, mean,
-                             invstd, scale, shift, res, relu, out)
+            pm, pm2, pcnt, nblk = part
+            ws = torch.empty(G * C, device=y.device)
+            ops.bn_stats_finalize(G, nblk, C, pm, pm2, pcnt, bn.weight, bn.bias,
+                                  bn.running_mean if track else None,
+                                  bn.running_var if track else None, bn.momentum, bn.eps, ws,
+                                  mean, invstd, scale, shift)
             if track:
                 bn.num_batches_tracked.add_(G)
-            batch_stats = True
         else:
             ops.bn_eval_params(G, C, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                bn.eps, scale, shift)
+        out = None
+        if materialize:
+            out = torch.empty_like(y)
             ops.bn_apply(y, scale, shift, res, relu, out, G, M, C)
-            batch_stats = False
-        rec = (bn, y, out, stats, relu, M, C, batch_stats) if self.save else None
+        rec = _BN(bn, y, out if relu else None, stats, relu, M, C, batch_stats) \
+            if self.save else None
+        self.last_lazy = (scale, shift, int(relu))  # for a consumer applying it on load
         return out, rec
 
-    def _bn_bwd(self, rec, dout, want_dres=False):
-        bn, y, out, stats, relu, M, C, batch_stats = rec
-        if not batch_stats:
+    def _bn_bwd(self, rec, dout, want_dres=False, pre=None):
+        if not rec.batch_stats:
             raise NotImplementedError("mauv: backward through eval-mode BN is not on the path "
                                       "(the reference trains and predicts in .train())")
-        G = self.G
-        dy = torch.empty_like(y)
-        dres = torch.empty_like(y) if want_dres else None
-        ws = torch.empty(ops.bn_workspace_floats(G, M, C), device=y.device)
+        G, M, C, bn = self.G, rec.M, rec.C, rec.bn
+        dy = torch.empty_like(rec.y)
+        dres = torch.empty_like(rec.y) if want_dres else None
+        ws = torch.empty(ops.bn_workspace_floats(G, M, C), device=dy.device)
         dg = bn.weight.grad if bn.weight.requires_grad else None
         db = bn.bias.grad if bn.bias.requires_grad else None
-        ops.bn_bwd(y, out, dout, relu, stats[0], stats[1], stats[2], G, M, C, ws, dy, dres, dg,
-                   db)
+        s = rec.stats
+        ops.bn_bwd(rec.y, rec.out, dout, rec.relu, s[0], s[1], s[2], G, M, C, ws, dy, dres, dg,
+                   db, shift=s[3], pre=pre)
         return dy, dres
 
     # ---- schedule ----
@@ -272,38 +329,37 @@ class TrunkRunner(_Runner):
             raise ValueError(f"trunk expects {t.conv1.in_channels} input channels, got {Cin}")
         self.B = B
         recs = self.recs = []
-        y, rc = self._conv(t.conv1, x, B, H, W, x_strides=(0, Cin * H * W, W, 1, H * W))
-        a, rb = self._bn(t.bn1, y, relu=True)
-        del y
+        y, rc, part = self._conv(t.conv1, x, B, H, W, x_strides=(0, Cin * H * W, W, 1, H * W))
+        a, rb = self._bn(t.bn1, y, part, relu=True)
+        del y, part
         H, W = a.shape[2], a.shape[3]
         Hp, Wp = ops.out_hw(H, 3, 2, 1), ops.out_hw(W, 3, 2, 1)
         p = torch.empty(G, B, Hp, Wp, 64, device=x.device)
         idx = torch.empty(G, B, Hp, Wp, 64, dtype=torch.uint8, device=x.device)
         ops.maxpool_fwd(a, G * B, H, W, 64, p, idx)
         self.stem = (rc, rb, idx, (H, W)) if self.save else None
-        if not self.save:
-            del a, idx
+        del a, idx
         cur, H, W = p, Hp, Wp
         for blk in t.blocks():
-            y1, r1 = self._conv(blk.conv1, cur, B, H, W)
-            a1, s1 = self._bn(blk.bn1, y1, relu=True)
-            del y1
-            y2, r2 = self._conv(blk.conv2, a1, B, H, W)
+            y1, r1, p1 = self._conv(blk.conv1, cur, B, H, W)
+            _, s1 = self._bn(blk.bn1, y1, p1, relu=True, materialize=False)
+            y2, r2, p2 = self._conv(blk.conv2, y1, B, H, W, x_bn=self.last_lazy)
             H2, W2 = y2.shape[2], y2.shape[3]
-            a2, s2 = self._bn(blk.bn2, y2, relu=True)
-            del y2
-            y3, r3 = self._conv(blk.conv3, a2, B, H2, W2)
+            _, s2 = self._bn(blk.bn2, y2, p2, relu=True, materialize=False)
+            y3, r3, p3 = self._conv(blk.conv3, y2, B, H2, W2, x_bn=self.last_lazy)
             rd = sd = None
             if blk.downsample is not None:
-                yd, rd = self._conv(blk.downsample[0], cur, B, H, W)
-                res, sd = self._bn(blk.downsample[1], yd, relu=False)
+                yd, rd, pd_ = self._conv(blk.downsample[0], cur, B, H, W)
+                res, sd = self._bn(blk.downsample[1], yd, pd_, relu=False)
                 del yd
             else:
                 res = cur
-            a3, s3 = self._bn(blk.bn3, y3, relu=True, res=res)
-            del y3, res
+            a3, s3 = self._bn(blk.bn3, y3, p3, relu=True, res=res)
+            del res
             if self.save:
                 recs.append((r1, s1, r2, s2, r3, s3, rd, sd))
+            else:
+                del y1, y2, y3
             cur, H, W = a3, H2, W2
         self.final_hw = (H, W)
         feat = torch.empty(G, B, 2048, device=x.device)
@@ -329,26 +385,28 @@ class TrunkRunner(_Runner):
         da = torch.empty(G, B, H, W, 2048, device=dout.device)
         ops.avgpool_bwd(dfeat, G * B, H * W, 2048, da)
         del dfeat
+        pre = None  # bn3 partials of the block being entered (from the previous dgrad epilogue)
         while self.recs:
             r1, s1, r2, s2, r3, s3, rd, sd = self.recs.pop()
-            dy3, dres = self._bn_bwd(s3, da, want_dres=True)
+            prev_bn3 = self.recs[-1][5] if self.recs else None  # BN whose output is this input
+            dy3, dres = self._bn_bwd(s3, da, want_dres=True, pre=pre)
             del da, s3
-            da2 = self._conv_bwd(r3, dy3)
+            da2, pre2 = self._conv_bwd(r3, dy3, bn_out=s2)
             del dy3, r3
-            dy2, _ = self._bn_bwd(s2, da2)
+            dy2, _ = self._bn_bwd(s2, da2, pre=pre2)
             del da2, s2
-            da1 = self._conv_bwd(r2, dy2)
+            da1, pre1 = self._conv_bwd(r2, dy2, bn_out=s1)
             del dy2, r2
-            dy1, _ = self._bn_bwd(s1, da1)
+            dy1, _ = self._bn_bwd(s1, da1, pre=pre1)
             del da1, s1
             if rd is not None:
                 dyd, _ = self._bn_bwd(sd, dres)
                 del dres, sd
-                dx = self._conv_bwd(r1, dy1)
-                self._conv_bwd(rd, dyd, dx=dx, accumulate=True)
+                dx, _ = self._conv_bwd(r1, dy1)
+                _, pre = self._conv_bwd(rd, dyd, dx=dx, accumulate=True, bn_out=prev_bn3)
                 del dyd, rd
             else:
-                dx = self._conv_bwd(r1, dy1, addend=dres)
+                dx, pre = self._conv_bwd(r1, dy1, addend=dres, bn_out=prev_bn3)
                 del dres
             del dy1, r1
             da = dx

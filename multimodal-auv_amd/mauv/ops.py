@@ -57,25 +57,45 @@ class _Prof:
 
 
 # ----------------------------------------------------------------------- convolutions
-def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_strides=None):
-    """y[G][B*Ho*Wo][Cout] = conv(x[g], w[g]) (+ bias[g]); w: [G][Cout][R][R][Cin]."""
+def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_strides=None,
+               x_bn=None, stats=None):
+    """y[G][B*Ho*Wo][Cout] = conv(x'[g], w[g]) (+ bias[g]); w: [G][Cout][R][R][Cin].
+    x_bn = (scale [G][Cin], shift [G][Cin], relu): x' = [relu](x*scale + shift) on load.
+    stats = (mean, m2, cnt) partial buffers for the epilogue BN statistics (see
+    fwd_stat_blocks)."""
     _f32(w, y, bias)
     assert x.is_cuda and x.dtype == torch.float32
     xs = None if x_strides is None else _LL5(*x_strides)
+    sc, sh, rl = x_bn if x_bn is not None else (None, None, 0)
+    sm, s2, sn = stats if stats is not None else (None, None, None)
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
     with _Prof("fwd", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin):
-        check(lib.mauv_conv2d_fwd_f32(_p(x), xs, _p(w), _p(bias), _p(y), G, B, H, W, Cin, Cout,
-                                      R, R, stride, pad, stream()), "conv2d_fwd")
+        check(lib.mauv_conv2d_fwd_f32(_p(x), xs, _p(sc), _p(sh), int(rl), _p(w), _p(bias), _p(y),
+                                      G, B, H, W, Cin, Cout, R, R, stride, pad, _p(sm), _p(s2),
+                                      _p(sn), stream()), "conv2d_fwd")
+
+
+def fwd_stat_blocks(G, B, H, W, Cin, Cout, R, stride, pad):
+    return lib.mauv_conv2d_fwd_stat_blocks(G, B, H, W, Cin, Cout, R, R, stride, pad)
+
+
+def dgrad_stat_blocks(G, B, H, W, Cin, Cout, R, stride, pad):
+    return lib.mauv_conv2d_bwd_data_stat_blocks(G, B, H, W, Cin, Cout, R, R, stride, pad)
 
 
 def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=None,
-                    accumulate=False):
+                    accumulate=False, bn=None):
+    """bn = dict(y, out|None, scale, shift, mean, invstd, relu, p1, p2): dx is the output
+    gradient of that BatchNorm; the epilogue writes its backward partial sums into p1/p2."""
     _f32(dy, w, dx, addend)
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
+    b = bn or {}
     with _Prof("dgrad", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin):
-        check(lib.mauv_conv2d_bwd_data_f32(_p(dy), _p(w), _p(dx), _p(addend), int(accumulate),
-                                           G, B, H, W, Cin, Cout, R, R, stride, pad, stream()),
-              "conv2d_bwd_data")
+        check(lib.mauv_conv2d_bwd_data_f32(
+            _p(dy), _p(w), _p(dx), _p(addend), int(accumulate), G, B, H, W, Cin, Cout, R, R,
+            stride, pad, _p(b.get("y")), _p(b.get("out")), _p(b.get("scale")),
+            _p(b.get("shift")), _p(b.get("mean")), _p(b.get("invstd")), int(b.get("relu", 0)),
+            _p(b.get("p1")), _p(b.get("p2")), stream()), "conv2d_bwd_data")
 
 
 def wgrad_splits(G, B, H, W, Cin, Cout, R, stride, pad):
@@ -83,15 +103,16 @@ def wgrad_splits(G, B, H, W, Cin, Cout, R, stride, pad):
 
 
 def conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, R, stride, pad,
-                      x_strides=None):
-    """ws[splits][G][Cout][R*R*Cin] partial slabs."""
+                      x_strides=None, x_bn=None):
+    """ws[splits][G][Cout][R*R*Cin] partial slabs (x' as in conv2d_fwd)."""
     _f32(dy, ws)
     xs = None if x_strides is None else _LL5(*x_strides)
+    sc, sh, rl = x_bn if x_bn is not None else (None, None, 0)
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
     with _Prof("wgrad", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin):
-        check(lib.mauv_conv2d_bwd_weight_f32(_p(x), xs, _p(dy), _p(ws), splits, G, B, H, W,
-                                             Cin, Cout, R, R, stride, pad, stream()),
-              "conv2d_bwd_weight")
+        check(lib.mauv_conv2d_bwd_weight_f32(_p(x), xs, _p(sc), _p(sh), int(rl), _p(dy), _p(ws),
+                                             splits, G, B, H, W, Cin, Cout, R, R, stride, pad,
+                                             stream()), "conv2d_bwd_weight")
 
 
 # ----------------------------------------------------------------------- reparam / KL
@@ -153,12 +174,23 @@ def bn_eval_params(G, C, gamma, beta, run_mean, run_var, eps, scale, shift):
                                   _p(scale), _p(shift), stream()), "bn_eval_params")
 
 
+def bn_stats_finalize(G, nblk, C, pmean, pm2, pcnt, gamma, beta, run_mean, run_var, momentum,
+                      eps, ws, mean, invstd, scale, shift):
+    check(lib.mauv_bn_stats_finalize(G, nblk, C, _p(pmean), _p(pm2), _p(pcnt), _p(gamma),
+                                     _p(beta), _p(run_mean), _p(run_var), momentum, eps, _p(ws),
+                                     _p(mean), _p(invstd), _p(scale), _p(shift), stream()),
+          "bn_stats_finalize")
+
+
 def bn_bwd(y, out, dout, relu, mean, invstd, scale, G, M, C, ws, dy, dres=None, dgamma=None,
-           dbeta=None):
-    _f32(y, out, dout, mean, invstd, scale, ws, dy, dres, dgamma, dbeta)
+           dbeta=None, shift=None, pre=None):
+    """out None + relu: mask from y*scale+shift.  pre = (p1, p2, nblk) partials from a dgrad
+    epilogue (skips the partial pass)."""
+    _f32(y, out, dout, mean, invstd, scale, shift, ws, dy, dres, dgamma, dbeta)
+    p1, p2, nb = pre if pre is not None else (None, None, 0)
     check(lib.mauv_bn_bwd(_p(y), _p(out), _p(dout), int(relu), _p(mean), _p(invstd), _p(scale),
-                          G, M, C, _p(ws), _p(dy), _p(dres), _p(dgamma), _p(dbeta), stream()),
-          "bn_bwd")
+                          _p(shift), G, M, C, _p(ws), _p(dy), _p(dres), _p(dgamma), _p(dbeta),
+                          _p(p1), _p(p2), nb, stream()), "bn_bwd")
 
 
 # ----------------------------------------------------------------------- pooling

@@ -28,6 +28,17 @@ def test_library_exports_every_header_symbol():
     assert set(SIGNATURES) == set(names), set(SIGNATURES) ^ set(names)
 
 
+def test_ctypes_arity_matches_header():
+    """Every prototype's parameter count in include/mauv.h equals the ctypes argtypes."""
+    from mauv._lib import SIGNATURES
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    protos = dict(re.findall(r"(mauv_\w+)\(([^)]*)\)\s*;", txt))
+    for name, params in protos.items():
+        params = params.strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        assert len(SIGNATURES[name]) == n, (name, n, len(SIGNATURES[name]))
+
+
 def test_library_reports_gfx950_only():
     from mauv._lib import LIB_PATH
     out = os.popen(f"/opt/rocm/lib/llvm/bin/llvm-readelf -n {LIB_PATH} 2>/dev/null | head -0; "
