@@ -106,9 +106,21 @@ __device__ __forceinline__ void chan_merge(double& nn, double& mu, double& mm, d
   nn = nt;
 }
 
-// Stage 2: grid (C/64, G); 64 channels x 4 lanes per block, each lane Chan-merging a strided
-// quarter of the block partials in double, then a 4-way merge in LDS.
-__global__ __launch_bounds__(256) void bn_stats_final(
+// Stage 2: grid (C/64, G), 1024 threads = 64 channels x 16 lanes.  Exact two-pass merge of
+// the (count, mean, M2) partials: N = sum n_b, mean = sum n_b*mean_b / N,
+// M2 = sum [M2_b + n_b*(mean_b - mean)^2] (double; no divisions in the loops).
+constexpr int FIN_L = 16;
+
+__device__ __forceinline__ double lane_sum16(double v, double (*red)[64], int tx, int ty) {
+  red[ty][tx] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int k = 0; k < FIN_L; ++k) s += red[k][tx];
+  __syncthreads();
+  return s;
+}
+
+__global__ __launch_bounds__(1024) void bn_stats_final(
     int G, int nblk, int C, const float* __restrict__ pmean, const float* __restrict__ pm2,
     const float* __restrict__ pcnt, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float* __restrict__ mean_out,
@@ -116,18 +128,27 @@ __global__ __launch_bounds__(256) void bn_stats_final(
     float* __restrict__ shift_out, float* __restrict__ uvar_out) {
   const int g = blockIdx.y, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
-  double nn = 0.0, mu = 0.0, mm = 0.0;
+  __shared__ double red[FIN_L][64];
+  double n = 0.0, s = 0.0;
   if (c < C) {
-    for (int b = ty; b < nblk; b += 4) {
-      const long long o = ((long long)g * nblk + b) * C + c;
-      chan_merge(nn, mu, mm, pcnt[(long long)g * nblk + b], pmean[o], pm2[o]);
+    for (int b = ty; b < nblk; b += FIN_L) {
+      const double nb = pcnt[(long long)g * nblk + b];
+      n += nb;
+      s += nb * (double)pmean[((long long)g * nblk + b) * C + c];
     }
   }
-  __shared__ double sn[4][64], smu[4][64], smm[4][64];
-  sn[ty][tx] = nn; smu[ty][tx] = mu; smm[ty][tx] = mm;
-  __syncthreads();
+  const double nn = lane_sum16(n, red, tx, ty);
+  const double mu = lane_sum16(s, red, tx, ty) / nn;
+  double q = 0.0;
+  if (c < C) {
+    for (int b = ty; b < nblk; b += FIN_L) {
+      const long long o = ((long long)g * nblk + b) * C + c;
+      const double d = (double)pmean[o] - mu;
+      q += (double)pm2[o] + pcnt[(long long)g * nblk + b] * d * d;
+    }
+  }
+  const double mm = lane_sum16(q, red, tx, ty);
   if (ty != 0 || c >= C) return;
-  for (int k = 1; k < 4; ++k) chan_merge(nn, mu, mm, sn[k][tx], smu[k][tx], smm[k][tx]);
   const double var = mm / nn;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const float sc = gamma[c] * invstd;
@@ -260,27 +281,25 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ 
 
 // Backward stage 2: grid (C/64, G), 64 channels x 4 lanes: k1 = sum dz / M, k2 = sum
 // dz*xhat / M per (g,c) (double sums, fixed order).
-__global__ __launch_bounds__(256) void bn_bwd_final(int G, int nblk, int C, long long M,
-                                                    const float* __restrict__ p1,
-                                                    const float* __restrict__ p2,
-                                                    float* __restrict__ k1,
-                                                    float* __restrict__ k2) {
+__global__ __launch_bounds__(1024) void bn_bwd_final(int G, int nblk, int C, long long M,
+                                                     const float* __restrict__ p1,
+                                                     const float* __restrict__ p2,
+                                                     float* __restrict__ k1,
+                                                     float* __restrict__ k2) {
   const int g = blockIdx.y, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
+  __shared__ double red[FIN_L][64];
   double a = 0.0, b = 0.0;
   if (c < C) {
-    for (int k = ty; k < nblk; k += 4) {
+    for (int k = ty; k < nblk; k += FIN_L) {
       const long long o = ((long long)g * nblk + k) * C + c;
       a += p1[o];
       b += p2[o];
     }
   }
-  __shared__ double sa[4][64], sb[4][64];
-  sa[ty][tx] = a; sb[ty][tx] = b;
-  __syncthreads();
+  a = lane_sum16(a, red, tx, ty);
+  b = lane_sum16(b, red, tx, ty);
   if (ty != 0 || c >= C) return;
-  a = sa[0][tx] + sa[1][tx] + sa[2][tx] + sa[3][tx];
-  b = sb[0][tx] + sb[1][tx] + sb[2][tx] + sb[3][tx];
   k1[g * C + c] = (float)(a / (double)M);
   k2[g * C + c] = (float)(b / (double)M);
 }
@@ -394,7 +413,7 @@ MAUV_API int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const 
   hipLaunchKernelGGL(bn_stats_partial, dim3(nblk, G), dim3(256), 0, stream, y, M, C, rpb, rm,
                      pmean, pm2, pcnt);
   float* uvar = pcnt + (long long)G * nblk;
-  hipLaunchKernelGGL(bn_stats_final, dim3((C + 63) / 64, G), dim3(256), 0, stream, G, nblk, C,
+  hipLaunchKernelGGL(bn_stats_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, nblk, C,
                      pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift, uvar);
   if (run_mean && run_var)
     hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
@@ -413,7 +432,7 @@ MAUV_API int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, 
                                     float* workspace, float* mean, float* invstd, float* scale,
                                     float* shift, hipStream_t stream) {
   if (G <= 0 || nblk <= 0 || C <= 0) { set_error("bn_stats_finalize: bad shape"); return kErrArg; }
-  hipLaunchKernelGGL(bn_stats_final, dim3((C + 63) / 64, G), dim3(256), 0, stream, G, nblk, C,
+  hipLaunchKernelGGL(bn_stats_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, nblk, C,
                      pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift, workspace);
   if (run_mean && run_var)
     hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
@@ -449,12 +468,12 @@ MAUV_API int mauv_bn_bwd(const float* y, const float* out, const float* dout, in
   float* k1 = p2 + (long long)G * nblk * C;
   float* k2 = k1 + (long long)G * C;
   if (pre_p1) {  // partial sums already produced by the dgrad epilogue (conv_gemm.hip)
-    hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(256), 0, stream, G, pre_nblk,
+    hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, pre_nblk,
                        C, M, pre_p1, pre_p2, k1, k2);
   } else {
     hipLaunchKernelGGL(bn_bwd_partial, dim3(nblk, G), dim3(256), 0, stream, y, out, dout, relu,
                        mean, invstd, scale, shift, M, C, rpb, rm, p1, p2);
-    hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(256), 0, stream, G, nblk, C,
+    hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, nblk, C,
                        M, p1, p2, k1, k2);
   }
   if (dgamma || dbeta)

@@ -16,10 +16,18 @@ per model, so the data-parallel all-reduce is a single bucketed RCCL call).
 Activations are NHWC ``[G][B][H][W][C]`` fp32.  The stems read the caller's NCHW images in
 place (strided loads, group stride 0 = image shared by all MC samples).
 """
+import os
+
 import torch
 
 from . import ops
 from .layers import is_bayesian, LinearReparameterization
+
+
+# BN-backward partial sums (sum dz, sum dz*xhat) from the dgrad epilogue instead of a separate
+# pass over (y, dout).  Measured slower on MI355X (the LDS reduction lengthens every dgrad
+# tile more than the standalone partial kernel costs), so it is opt-in.
+DGRAD_BN_EPILOGUE = os.environ.get("MAUV_DGRAD_BN_EPILOGUE", "0") == "1"
 
 
 # ----------------------------------------------------------------------------- root state
@@ -266,7 +274,7 @@ class TrunkRunner(_Runner):
         if dx is None:
             dx = torch.empty(G, B, H, W, Cin, device=dy.device)
         bn_args, pre = (None, None)
-        if bn_out is not None and bn_out.batch_stats:
+        if DGRAD_BN_EPILOGUE and bn_out is not None and bn_out.batch_stats:
             bn_args, pre = bn_out.epilogue_args(G, (B, H, W, Cin, Cout, k, st, pd))
         ops.conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, k, st, pd, addend=addend,
                             accumulate=accumulate, bn=bn_args)
