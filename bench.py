@@ -74,6 +74,20 @@ def cpu_baseline(args):
             "host": platform.processor() or platform.machine()}
 
 
+def pmc_traffic():
+    """HBM bytes per conv_gemm launch from the committed PMC summary of this same command
+    (tools/pmc_traffic.py; separate FETCH_SIZE and WRITE_SIZE passes, FETCH_SIZE doubled per
+    MI355X_MICROARCH.md's gfx950 correction).  PMC collection serialises kernels, so it runs
+    as its own profiled invocation; the newest profiles/round*_conv_traffic.json is used."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "round*_conv_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d["bytes_per_launch"], os.path.relpath(files[-1], REPO)
+
+
 def roofline_step(step_fn):
     from mauv import ops
     ops.PROFILE = []
@@ -82,19 +96,25 @@ def roofline_step(step_fn):
     torch.cuda.synchronize()
     rows, ops.PROFILE = ops.PROFILE, None
     by = {}
-    for kind, fl, e0, e1 in rows:
+    nbytes = 0.0
+    for kind, fl, nb, nl, e0, e1 in rows:
         ms = e0.elapsed_time(e1)
         d = by.setdefault(kind, [0, 0.0, 0.0])
-        d[0] += 1
+        d[0] += nl
         d[1] += fl
         d[2] += ms
+        nbytes += nb
     tot_fl = sum(v[1] for v in by.values())
     tot_ms = sum(v[2] for v in by.values())
     n = sum(v[0] for v in by.values())
     achieved = tot_fl / (tot_ms * 1e-3) / 1e12
+    traffic, tsrc = pmc_traffic()
     return {
         "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TF,
-        "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TF, 4), "traffic": None,
+        "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TF, 4), "traffic": traffic,
+        "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC)",
+        "traffic_source": tsrc,
+        "algorithmic_bytes_per_launch": round(nbytes / max(n, 1)),
         "kernel": "conv_gemm_f32 (implicit-GEMM fwd+dgrad+wgrad, all launches of one step)",
         "launches": n, "avg_launch_us": round(tot_ms * 1e3 / max(n, 1), 2),
         "algorithmic_gflop_per_launch": round(tot_fl / max(n, 1) / 1e9, 3),

@@ -34,15 +34,17 @@ def out_hw(H, R, stride, pad):
 
 # ----------------------------------------------------------------------- profiling hook
 # bench.py sets PROFILE to a list to time every implicit-GEMM launch with HIP events on the
-# stream the kernel runs on (torch's current stream); entries: (kind, flops, ev0, ev1).
+# stream the kernel runs on (torch's current stream); entries: (kind, flops, bytes, launches,
+# ev0, ev1) — a strided dgrad call is stride^2 kernel launches (one per output-parity class)
+# with the ALGORITHMIC bytes of the launch (every operand read once, every output written once).
 PROFILE = None
 
 
 class _Prof:
-    __slots__ = ("kind", "flops", "e0")
+    __slots__ = ("kind", "flops", "nbytes", "launches", "e0")
 
-    def __init__(self, kind, flops):
-        self.kind, self.flops = kind, flops
+    def __init__(self, kind, flops, nbytes=0.0, launches=1):
+        self.kind, self.flops, self.nbytes, self.launches = kind, flops, nbytes, launches
 
     def __enter__(self):
         if PROFILE is not None:
@@ -53,7 +55,7 @@ class _Prof:
         if PROFILE is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
-            PROFILE.append((self.kind, self.flops, self.e0, e1))
+            PROFILE.append((self.kind, self.flops, self.nbytes, self.launches, self.e0, e1))
 
 
 # ----------------------------------------------------------------------- convolutions
@@ -69,7 +71,9 @@ def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_stri
     sc, sh, rl = x_bn if x_bn is not None else (None, None, 0)
     sm, s2, sn = stats if stats is not None else (None, None, None)
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
-    with _Prof("fwd", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin):
+    xg = 1 if (x_strides is not None and x_strides[0] == 0) else G
+    nb = 4.0 * (xg * B * H * W * Cin + G * Cout * R * R * Cin + G * B * Ho * Wo * Cout)
+    with _Prof("fwd", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin, nb):
         check(lib.mauv_conv2d_fwd_f32(_p(x), xs, _p(sc), _p(sh), int(rl), _p(w), _p(bias), _p(y),
                                       G, B, H, W, Cin, Cout, R, R, stride, pad, _p(sm), _p(s2),
                                       _p(sn), stream()), "conv2d_fwd")
@@ -90,7 +94,11 @@ def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=Non
     _f32(dy, w, dx, addend)
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
     b = bn or {}
-    with _Prof("dgrad", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin):
+    nb = 4.0 * (G * B * Ho * Wo * Cout + G * Cout * R * R * Cin +
+                G * B * H * W * Cin * (1 + (addend is not None) + bool(accumulate)))
+    nl = sum(1 for ph in range(stride) for pw in range(stride)
+             if (H - ph + stride - 1) // stride > 0 and (W - pw + stride - 1) // stride > 0)
+    with _Prof("dgrad", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin, nb, nl):
         check(lib.mauv_conv2d_bwd_data_f32(
             _p(dy), _p(w), _p(dx), _p(addend), int(accumulate), G, B, H, W, Cin, Cout, R, R,
             stride, pad, _p(b.get("y")), _p(b.get("out")), _p(b.get("scale")),
@@ -109,7 +117,9 @@ def conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, R, stride, pad,
     xs = None if x_strides is None else _LL5(*x_strides)
     sc, sh, rl = x_bn if x_bn is not None else (None, None, 0)
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
-    with _Prof("wgrad", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin):
+    xg = 1 if (x_strides is not None and x_strides[0] == 0) else G
+    nb = 4.0 * (xg * B * H * W * Cin + G * B * Ho * Wo * Cout + ws.numel())
+    with _Prof("wgrad", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin, nb):
         check(lib.mauv_conv2d_bwd_weight_f32(_p(x), xs, _p(sc), _p(sh), int(rl), _p(dy), _p(ws),
                                              splits, G, B, H, W, Cin, Cout, R, R, stride, pad,
                                              stream()), "conv2d_bwd_weight")

@@ -34,7 +34,11 @@ def trunk_convs(cin, S):
     return out
 
 
-def timeit(fn, reps=5):
+REPS = 5
+
+
+def timeit(fn, reps=None):
+    reps = reps or REPS
     fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -53,7 +57,11 @@ def main():
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--trunks", default="opt,bathy,sss")
+    ap.add_argument("--shape", default="", help="one shape Cin,Cout,R,stride,pad,H (profiling)")
+    ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
+    global REPS
+    REPS = a.reps
     G, B, dev = a.G, a.B, "cuda"
     kinds = a.only.split(",")
     rows = []
@@ -61,7 +69,10 @@ def main():
     for trunk, cin, S in (("opt", 3, 224), ("bathy", 3, 256), ("sss", 1, 256)):
         if trunk not in a.trunks:
             continue
-        for name, Cin, Cout, R, st, pd, H in trunk_convs(cin, S):
+        convs = trunk_convs(cin, S)
+        if a.shape:
+            convs = [("shape",) + tuple(int(v) for v in a.shape.split(","))]
+        for name, Cin, Cout, R, st, pd, H in convs:
             key = (Cin, Cout, R, st, pd, H)
             Ho = ops.out_hw(H, R, st, pd)
             fl = 2.0 * G * B * Ho * Ho * Cout * R * R * Cin
