@@ -76,6 +76,28 @@ int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strides, const
                                int splits, int G, int B, int H, int W, int Cin, int Cout, int R,
                                int S, int stride, int pad, hipStream_t stream);
 
+/* ---- 16-bit implicit-GEMM convs (conv_gemm16.hip) -----------------------------------------
+ * Same three GEMM views on v_mfma_f32_32x32x16_{bf16,f16}: dtype 0 = bf16 (BASELINE configs[2]
+ * training), 1 = f16 (the reference predictor's torch.amp.autocast on a GPU,
+ * inference/predictors.py:55).  x / w / y / dy / dx / addend are 16-bit words, statistics
+ * partials and weight-gradient slabs fp32.  Cin and Cout must be multiples of 8 (the stems'
+ * 1/3-channel inputs are zero-padded to 8 channels), dgrad needs Cout % 32 == 0; x strides
+ * are channel-contiguous multiples of 8.  Statistics partials: mauv_conv2d_fwd_stat_blocks. */
+int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_strides,
+                        const float* x_scale, const float* x_shift, int x_relu, const void* w,
+                        void* y, int G, int B, int H, int W, int Cin, int Cout, int R, int S,
+                        int stride, int pad, float* st_mean, float* st_m2, float* st_cnt,
+                        hipStream_t stream);
+int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, void* dx,
+                             const void* addend, int accumulate, int G, int B, int H, int W,
+                             int Cin, int Cout, int R, int S, int stride, int pad,
+                             hipStream_t stream);
+int mauv_conv2d_bwd_weight_h16(int dtype, const void* x, const long long* x_strides,
+                               const float* x_scale, const float* x_shift, int x_relu,
+                               const void* dy, float* ws, int splits, int G, int B, int H, int W,
+                               int Cin, int Cout, int R, int S, int stride, int pad,
+                               hipStream_t stream);
+
 /* ---- variational sampling / KL (reparam.hip) --------------------------------------------
  * bayesian-torch Conv2dReparameterization/LinearReparameterization.forward:
  *   sigma = log1p(exp(rho)); eps.normal_(); w = mu + sigma*eps      (per MC sample g)

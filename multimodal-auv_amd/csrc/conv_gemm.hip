@@ -526,12 +526,12 @@ static void launch(const ConvArgs& a, hipStream_t st) {
 
 template <int MODE, bool VA, bool VB>
 static void launch_tiles(const ConvArgs& a, hipStream_t st) {
-  // BN = 64 when the N extent is 64 or less (Cout=64 convs / Cin=64 dgrad), else 128.
-  const bool smallN = a.N <= 64;
-  const bool smallM = a.M <= 64;
-  if (smallM && smallN) launch<MODE, 64, 64, VA, VB>(a, st);
-  else if (smallM) launch<MODE, 64, 128, VA, VB>(a, st);
-  else if (smallN) launch<MODE, 128, 64, VA, VB>(a, st);
+  // measured: halving the row tile for launches with fewer blocks than resident slots does
+  // not pay (co-resident blocks share the MFMA pipes, so a partial last wave runs faster)
+  const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
+  if (bm == 64 && bn == 64) launch<MODE, 64, 64, VA, VB>(a, st);
+  else if (bm == 64) launch<MODE, 64, 128, VA, VB>(a, st);
+  else if (bn == 64) launch<MODE, 128, 64, VA, VB>(a, st);
   else launch<MODE, 128, 128, VA, VB>(a, st);
 }
 
@@ -539,14 +539,14 @@ static void launch_tiles(const ConvArgs& a, hipStream_t st) {
 
 using namespace mauv;
 
-// m-tiles of a launch (launch_tiles picks BM = 64 for M <= 64, else 128)
-static int stat_blocks(int M) { return ceil_div(M, M <= 64 ? 64 : 128); }
-static int dgrad_stat_blocks(int B, int H, int W, int stride) {
+// m-tiles of a launch (BM = conv_tile_rows(M)), = per-m-tile BN statistic partials
+static int stat_blocks(int M, int N, int G) { return ceil_div(M, conv_tile_rows(M)); }
+static int dgrad_stat_blocks(int G, int B, int H, int W, int N, int stride) {
   int n = 0;
   for (int ph = 0; ph < stride; ++ph)
     for (int pw = 0; pw < stride; ++pw) {
       const int M = B * ((H - ph + stride - 1) / stride) * ((W - pw + stride - 1) / stride);
-      if (M > 0) n += stat_blocks(M);
+      if (M > 0) n += stat_blocks(M, N, G);
     }
   return n;
 }
@@ -585,7 +585,7 @@ MAUV_API int mauv_conv2d_fwd_f32(const float* x, const long long* x_strides,
   a.M = B * a.Ho * a.Wo; a.N = Cout; a.K = R * S * Cin;
   a.out_sg = (long long)a.M * a.N;
   a.st_mean = st_mean; a.st_m2 = st_m2; a.st_cnt = st_cnt;
-  a.st_nblk = stat_blocks(a.M); a.st_base = 0;
+  a.st_nblk = stat_blocks(a.M, a.N, G); a.st_base = 0;
   const bool va = (Cin % 32 == 0) && a.xs_c == 1 && (a.xs_w % 4 == 0) && (a.xs_h % 4 == 0) &&
                   (a.xs_b % 4 == 0) && (a.xs_g % 4 == 0);
   const bool vb = (a.K % 4 == 0);
@@ -611,7 +611,7 @@ MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx
   a.bp_y = bn_y; a.bp_out = bn_out; a.bp_sc = bn_scale; a.bp_sh = bn_shift;
   a.bp_mean = bn_mean; a.bp_invstd = bn_invstd; a.bp_relu = bn_relu;
   a.bp_p1 = bn_p1; a.bp_p2 = bn_p2;
-  a.bp_nblk = dgrad_stat_blocks(B, H, W, stride);
+  a.bp_nblk = dgrad_stat_blocks(G, B, H, W, Cin, stride);
   a.bp_base = 0;
   if (bn_p1 && bn_relu && !bn_out && !bn_shift) { set_error("conv2d_bwd_data: mask source"); return kErrArg; }
   const bool va = (Cout % 32 == 0), vb = (Cin % 4 == 0);
@@ -631,7 +631,7 @@ MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx
       if (va && vb) launch_tiles<DGRAD, true, true>(a, stream);
       else if (vb) launch_tiles<DGRAD, false, true>(a, stream);
       else launch_tiles<DGRAD, false, false>(a, stream);
-      a.bp_base += stat_blocks(a.M);
+      a.bp_base += stat_blocks(a.M, a.N, G);
     }
   return check_launch("conv2d_bwd_data");
 }
@@ -640,11 +640,11 @@ MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx
 MAUV_API int mauv_conv2d_fwd_stat_blocks(int G, int B, int H, int W, int Cin, int Cout, int R,
                                          int S, int stride, int pad) {
   const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
-  return stat_blocks(B * Ho * Wo);
+  return stat_blocks(B * Ho * Wo, Cout, G);
 }
 MAUV_API int mauv_conv2d_bwd_data_stat_blocks(int G, int B, int H, int W, int Cin, int Cout,
                                               int R, int S, int stride, int pad) {
-  return dgrad_stat_blocks(B, H, W, stride);
+  return dgrad_stat_blocks(G, B, H, W, Cin, stride);
 }
 
 // Split count used by mauv_conv2d_bwd_weight for a given problem (host helper so the caller

@@ -1,0 +1,68 @@
+// 16-bit storage helpers (bf16 / f16) for the reduced-precision path.
+//
+// Activations, activation gradients and sampled weights are stored as 16-bit words; every
+// reduction (GEMM accumulation, BatchNorm statistics, weight gradients) runs in fp32.  DT
+// selects the format: 0 = bf16 (training, BASELINE configs[2]), 1 = f16 (what the reference's
+// predictor computes in under torch.amp.autocast on a GPU, inference/predictors.py:55).
+#pragma once
+#include "mauv_common.h"
+
+typedef unsigned short u16;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx8 __attribute__((ext_vector_type(8)));
+
+namespace mauv {
+
+enum { DT_BF16 = 0, DT_F16 = 1 };
+
+template <int DT>
+struct H16;
+
+template <>
+struct H16<DT_BF16> {
+  typedef bf16x8 V8;
+  static __device__ __forceinline__ float to_f(u16 v) { return __uint_as_float((unsigned)v << 16); }
+  static __device__ __forceinline__ u16 from_f(float f) {
+    return __builtin_bit_cast(u16, (__bf16)f);  // round-to-nearest-even (v_cvt_pk_bf16_f32)
+  }
+  static __device__ __forceinline__ floatx16 mfma(u32x4 a, u32x4 b, floatx16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(V8, a),
+                                                   __builtin_bit_cast(V8, b), c, 0, 0, 0);
+  }
+};
+
+template <>
+struct H16<DT_F16> {
+  typedef f16x8 V8;
+  static __device__ __forceinline__ float to_f(u16 v) { return (float)__builtin_bit_cast(_Float16, v); }
+  static __device__ __forceinline__ u16 from_f(float f) { return __builtin_bit_cast(u16, (_Float16)f); }
+  static __device__ __forceinline__ floatx16 mfma(u32x4 a, u32x4 b, floatx16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(V8, a),
+                                                  __builtin_bit_cast(V8, b), c, 0, 0, 0);
+  }
+};
+
+// 8 packed 16-bit values <-> 8 floats
+template <int DT>
+__device__ __forceinline__ floatx8 unpack8(u32x4 v) {
+  floatx8 f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = H16<DT>::to_f((u16)(v[i] & 0xffffu));
+    f[2 * i + 1] = H16<DT>::to_f((u16)(v[i] >> 16));
+  }
+  return f;
+}
+template <int DT>
+__device__ __forceinline__ u32x4 pack8(floatx8 f) {
+  u32x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    v[i] = (unsigned)H16<DT>::from_f(f[2 * i]) | ((unsigned)H16<DT>::from_f(f[2 * i + 1]) << 16);
+  return v;
+}
+
+}  // namespace mauv

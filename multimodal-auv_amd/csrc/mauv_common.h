@@ -24,6 +24,11 @@ constexpr int kErrLaunch = -2;   // hipGetLastError() after launch
 
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// Block-tile extent along a GEMM dimension of the implicit-GEMM convs (fp32 and 16-bit):
+// 64 when the extent is 64 or less, else 128.  The per-m-tile BN statistics partials the FWD
+// epilogues write are counted with the same rule (mauv_conv2d_fwd_stat_blocks).
+inline int conv_tile_rows(int extent) { return extent <= 64 ? 64 : 128; }
+
 // ---------------- Philox4x32-10 + Box-Muller (counter-based, recomputable) --------------
 // Standard constants (Salmon et al. 2011).  ctr = (quad index, sample lo, layer id,
 // sample hi), key = seed.  The oracle restates this bit-exactly in numpy

@@ -31,6 +31,10 @@ SIGNATURES = {
     "mauv_conv2d_bwd_data_stat_blocks": [I] * 10,
     "mauv_conv2d_wgrad_splits": [I, I, I, I, I, I, I, I, I, I],
     "mauv_conv2d_bwd_weight_f32": [P, P, P, P, I, P, P] + [I] * 11 + [P],
+    # conv_gemm16.hip
+    "mauv_conv2d_fwd_h16": [I, P, P, P, P, I, P, P] + [I] * 10 + [P, P, P, P],
+    "mauv_conv2d_bwd_data_h16": [I, P, P, P, P, I] + [I] * 10 + [P],
+    "mauv_conv2d_bwd_weight_h16": [I, P, P, P, P, I, P, P, I] + [I] * 10 + [P],
     # reparam.hip
     "mauv_reparam_sample": [P, P, P, U64, U64, U32, I, I, I, I, P, LL, P],
     "mauv_reparam_bwd": [P, I, LL, LL, P, P, P, U64, U64, U32, I, I, I, I, P, P, LL, P],

@@ -21,6 +21,16 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+H16 = {torch.bfloat16: 0, torch.float16: 1}   # C-ABI dtype codes of the 16-bit path
+
+
+def _h16(dt, *ts):
+    for t in ts:
+        if t is not None:
+            assert t.is_cuda and t.dtype == dt and t.is_contiguous(), \
+                (t.device, t.dtype, dt, t.is_contiguous(), t.shape)
+
+
 def _f32(*ts):
     for t in ts:
         if t is not None:
@@ -65,15 +75,26 @@ def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_stri
     x_bn = (scale [G][Cin], shift [G][Cin], relu): x' = [relu](x*scale + shift) on load.
     stats = (mean, m2, cnt) partial buffers for the epilogue BN statistics (see
     fwd_stat_blocks)."""
-    _f32(w, y, bias)
-    assert x.is_cuda and x.dtype == torch.float32
     xs = None if x_strides is None else _LL5(*x_strides)
     sc, sh, rl = x_bn if x_bn is not None else (None, None, 0)
     sm, s2, sn = stats if stats is not None else (None, None, None)
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
     xg = 1 if (x_strides is not None and x_strides[0] == 0) else G
-    nb = 4.0 * (xg * B * H * W * Cin + G * Cout * R * R * Cin + G * B * Ho * Wo * Cout)
-    with _Prof("fwd", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin, nb):
+    fl = 2.0 * G * B * Ho * Wo * Cout * R * R * Cin
+    esz = w.element_size()
+    nb = esz * (xg * B * H * W * Cin + G * Cout * R * R * Cin + G * B * Ho * Wo * Cout)
+    if w.dtype in H16:
+        assert bias is None, "16-bit convs carry no bias (the trunks' convs are bias=False)"
+        _h16(w.dtype, w, y)
+        assert x.is_cuda and x.dtype == w.dtype
+        with _Prof("fwd_" + str(w.dtype)[6:], fl, nb):
+            check(lib.mauv_conv2d_fwd_h16(H16[w.dtype], _p(x), xs, _p(sc), _p(sh), int(rl), _p(w),
+                                          _p(y), G, B, H, W, Cin, Cout, R, R, stride, pad,
+                                          _p(sm), _p(s2), _p(sn), stream()), "conv2d_fwd_h16")
+        return
+    _f32(w, y, bias)
+    assert x.is_cuda and x.dtype == torch.float32
+    with _Prof("fwd", fl, nb):
         check(lib.mauv_conv2d_fwd_f32(_p(x), xs, _p(sc), _p(sh), int(rl), _p(w), _p(bias), _p(y),
                                       G, B, H, W, Cin, Cout, R, R, stride, pad, _p(sm), _p(s2),
                                       _p(sn), stream()), "conv2d_fwd")
@@ -91,14 +112,23 @@ def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=Non
                     accumulate=False, bn=None):
     """bn = dict(y, out|None, scale, shift, mean, invstd, relu, p1, p2): dx is the output
     gradient of that BatchNorm; the epilogue writes its backward partial sums into p1/p2."""
-    _f32(dy, w, dx, addend)
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
     b = bn or {}
-    nb = 4.0 * (G * B * Ho * Wo * Cout + G * Cout * R * R * Cin +
-                G * B * H * W * Cin * (1 + (addend is not None) + bool(accumulate)))
+    fl = 2.0 * G * B * Ho * Wo * Cout * R * R * Cin
+    nb = w.element_size() * (G * B * Ho * Wo * Cout + G * Cout * R * R * Cin +
+                             G * B * H * W * Cin * (1 + (addend is not None) + bool(accumulate)))
     nl = sum(1 for ph in range(stride) for pw in range(stride)
              if (H - ph + stride - 1) // stride > 0 and (W - pw + stride - 1) // stride > 0)
-    with _Prof("dgrad", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin, nb, nl):
+    if w.dtype in H16:
+        assert bn is None, "16-bit dgrad has no BN-partials epilogue"
+        _h16(w.dtype, dy, w, dx, addend)
+        with _Prof("dgrad_" + str(w.dtype)[6:], fl, nb, nl):
+            check(lib.mauv_conv2d_bwd_data_h16(H16[w.dtype], _p(dy), _p(w), _p(dx), _p(addend),
+                                               int(accumulate), G, B, H, W, Cin, Cout, R, R,
+                                               stride, pad, stream()), "conv2d_bwd_data_h16")
+        return
+    _f32(dy, w, dx, addend)
+    with _Prof("dgrad", fl, nb, nl):
         check(lib.mauv_conv2d_bwd_data_f32(
             _p(dy), _p(w), _p(dx), _p(addend), int(accumulate), G, B, H, W, Cin, Cout, R, R,
             stride, pad, _p(b.get("y")), _p(b.get("out")), _p(b.get("scale")),
@@ -113,13 +143,24 @@ def wgrad_splits(G, B, H, W, Cin, Cout, R, stride, pad):
 def conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, R, stride, pad,
                       x_strides=None, x_bn=None):
     """ws[splits][G][Cout][R*R*Cin] partial slabs (x' as in conv2d_fwd)."""
-    _f32(dy, ws)
     xs = None if x_strides is None else _LL5(*x_strides)
     sc, sh, rl = x_bn if x_bn is not None else (None, None, 0)
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
     xg = 1 if (x_strides is not None and x_strides[0] == 0) else G
-    nb = 4.0 * (xg * B * H * W * Cin + G * B * Ho * Wo * Cout + ws.numel())
-    with _Prof("wgrad", 2.0 * G * B * Ho * Wo * Cout * R * R * Cin, nb):
+    fl = 2.0 * G * B * Ho * Wo * Cout * R * R * Cin
+    nb = dy.element_size() * (xg * B * H * W * Cin + G * B * Ho * Wo * Cout) + 4.0 * ws.numel()
+    if dy.dtype in H16:
+        _h16(dy.dtype, dy)
+        _f32(ws)
+        assert x.is_cuda and x.dtype == dy.dtype
+        with _Prof("wgrad_" + str(dy.dtype)[6:], fl, nb):
+            check(lib.mauv_conv2d_bwd_weight_h16(H16[dy.dtype], _p(x), xs, _p(sc), _p(sh), int(rl),
+                                                 _p(dy), _p(ws), splits, G, B, H, W, Cin, Cout,
+                                                 R, R, stride, pad, stream()),
+                  "conv2d_bwd_weight_h16")
+        return
+    _f32(dy, ws)
+    with _Prof("wgrad", fl, nb):
         check(lib.mauv_conv2d_bwd_weight_f32(_p(x), xs, _p(sc), _p(sh), int(rl), _p(dy), _p(ws),
                                              splits, G, B, H, W, Cin, Cout, R, R, stride, pad,
                                              stream()), "conv2d_bwd_weight")

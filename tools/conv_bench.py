@@ -59,10 +59,12 @@ def main():
     ap.add_argument("--trunks", default="opt,bathy,sss")
     ap.add_argument("--shape", default="", help="one shape Cin,Cout,R,stride,pad,H (profiling)")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "f16"])
     a = ap.parse_args()
     global REPS
     REPS = a.reps
     G, B, dev = a.G, a.B, "cuda"
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[a.dtype]
     kinds = a.only.split(",")
     rows = []
     cache = {}
@@ -81,12 +83,14 @@ def main():
                     rows.append((trunk, name, kind, key, ms, fl))
                 continue
             res = []
-            x = torch.randn(G, B, H, H, Cin, device=dev)
-            w = torch.randn(G, Cout, R, R, Cin, device=dev) * 0.05
-            y = torch.empty(G, B, Ho, Ho, Cout, device=dev)
+            if dt != torch.float32 and Cin % 8:
+                Cin = 8   # the 16-bit path zero-pads the stems' input channels to 8
+            x = torch.randn(G, B, H, H, Cin, device=dev).to(dt)
+            w = (torch.randn(G, Cout, R, R, Cin, device=dev) * 0.05).to(dt)
+            y = torch.empty(G, B, Ho, Ho, Cout, device=dev, dtype=dt)
             if "fwd" in kinds:
                 res.append(("fwd", timeit(lambda: ops.conv2d_fwd(x, w, y, G, B, H, H, Cin, Cout, R, st, pd))))
-            if "dgrad" in kinds and name != "stem":
+            if "dgrad" in kinds and name != "stem" and (dt == torch.float32 or Cout % 32 == 0):
                 dx = torch.empty_like(x)
                 res.append(("dgrad", timeit(lambda: ops.conv2d_bwd_data(y, w, dx, G, B, H, H, Cin, Cout, R, st, pd))))
                 del dx
