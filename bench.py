@@ -10,10 +10,12 @@ cross-entropy, backward, RCCL gradient all-reduce (N>1), NaN/Inf guard, Adam ste
 Workload per GPU: B=64 triplets, optical 3x224x224 ~N(0,1), bathy 3x256x256 ~U[0,1) with
 channel 2 = 0, SSS 1x256x256 ~U[0,1), 7 classes, fp32 (weak scaling: 64 per GPU).
 
-Also reported: MC inference (configs[3]: 100 passes over 256 triplets, MC-sharded across
-ranks), the roofline of the dominant kernel family (implicit-GEMM conv fwd/dgrad/wgrad,
-HIP-event timed inside this run), and the reference-semantics CPU path (oracle/, torch-CPU
-fp32, sequential MC loop) timed on a bounded sample on this host.
+Also reported: the same step with bf16 trunks (configs[2]'s per-GPU slice, `bf16_train`),
+MC inference (configs[3]: 100 passes over 256 triplets, MC-sharded across ranks, under
+torch.autocast as the reference predictor runs it -> f16 trunks), the roofline of the dominant
+kernel family (implicit-GEMM conv fwd/dgrad/wgrad, HIP-event timed inside this run), and the
+reference-semantics CPU path (oracle/, torch-CPU fp32, sequential MC loop) timed on a bounded
+sample on this host.
 """
 import argparse
 import json
@@ -32,6 +34,7 @@ for _p in (REPO, os.path.join(REPO, "multimodal-auv_amd")):
 
 METRIC = "triplets/sec training + MC-samples/sec inference, 7-class BNN, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md: f32-in MFMA = vector peak (spec)
+BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: dense bf16/f16 MFMA (no sparsity)
 
 
 def synthetic_batch(B, S_opt, S_son, device, seed):
@@ -88,7 +91,8 @@ def pmc_traffic():
     return d["bytes_per_launch"], os.path.relpath(files[-1], REPO)
 
 
-def roofline_step(step_fn):
+def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic=True,
+                  kernel="conv_gemm_f32 (implicit-GEMM fwd+dgrad+wgrad, all launches of one step)"):
     from mauv import ops
     ops.PROFILE = []
     torch.cuda.synchronize()
@@ -108,14 +112,14 @@ def roofline_step(step_fn):
     tot_ms = sum(v[2] for v in by.values())
     n = sum(v[0] for v in by.values())
     achieved = tot_fl / (tot_ms * 1e-3) / 1e12
-    traffic, tsrc = pmc_traffic()
+    traffic, tsrc = pmc_traffic() if traffic else (None, None)
     return {
-        "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TF,
-        "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TF, 4), "traffic": traffic,
+        "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+        "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
         "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC)",
         "traffic_source": tsrc,
         "algorithmic_bytes_per_launch": round(nbytes / max(n, 1)),
-        "kernel": "conv_gemm_f32 (implicit-GEMM fwd+dgrad+wgrad, all launches of one step)",
+        "kernel": kernel,
         "launches": n, "avg_launch_us": round(tot_ms * 1e3 / max(n, 1), 2),
         "algorithmic_gflop_per_launch": round(tot_fl / max(n, 1) / 1e9, 3),
         "conv_ms_per_step": round(tot_ms, 2),
@@ -139,6 +143,11 @@ def main():
     ap.add_argument("--no-infer", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-bf16", action="store_true",
+                    help="skip the bf16 training measurement (configs[2] per-GPU slice)")
+    ap.add_argument("--bf16-steps", type=int, default=5)
+    ap.add_argument("--infer-fp32", action="store_true",
+                    help="also time MC inference with fp32 trunks (default: autocast f16 only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,23 +198,58 @@ def main():
     triplets_s = args.batch * world * args.steps / dt
     roof = None if args.no_roofline else roofline_step(step)
 
+    def timed(fn, steps):
+        barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        barrier()
+        t = time.perf_counter() - t
+        if world > 1:
+            tt = torch.tensor([t], device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t = tt.item()
+        return t
+
+    bf16 = None
+    if not args.no_bf16:
+        from mauv.engine import set_precision
+        set_precision(model.module if world > 1 else model, torch.bfloat16)
+        step()                                   # warm-up (16-bit kernels, allocator)
+        tb = timed(step, args.bf16_steps)
+        bf16 = {"value": round(args.batch * world * args.bf16_steps / tb, 3),
+                "unit": "triplets/s", "ms_per_step": round(tb / args.bf16_steps * 1e3, 2),
+                "steps": args.bf16_steps, "dtype": "bf16",
+                "config": f"configs[2] per-GPU slice: B={args.batch}/GPU (global "
+                          f"{args.batch * world}), bf16 trunks (fp32 accumulation, BN "
+                          f"statistics, master weights, head), num_mc={args.num_mc}"}
+        if not args.no_roofline:
+            bf16["roofline"] = roofline_step(
+                step, peak=BF16_MFMA_PEAK_TF, traffic=False,
+                kernel="conv_gemm_h16<bf16> (implicit-GEMM fwd+dgrad+wgrad, one step)")
+        set_precision(model.module if world > 1 else model, None)
+
     infer = None
     if not args.no_infer:
         opt.zero_grad(set_to_none=True)
         xi, bi, si, _ = synthetic_batch(args.infer_batch, args.optical, args.sonar, dev, 99)
         group = dist.group.WORLD if world > 1 else None
-        with torch.no_grad():
-            mc_statistics(model, xi, bi, si, max(world, 2), group=group)   # warm-up
-            barrier()
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            mc_statistics(model, xi, bi, si, args.infer_mc, group=group)
-            torch.cuda.synchronize()
-            barrier()
-            di = time.perf_counter() - t1
-        infer = {"value": round(args.infer_mc * args.infer_batch / di, 2), "unit": "MC-samples/s",
-                 "batch": args.infer_batch, "num_mc": args.infer_mc,
-                 "ms_per_batch": round(di * 1e3, 1), "sharding": "mc" if world > 1 else "none"}
+
+        def infer_run(autocast):
+            # the reference predictor wraps its MC loop in torch.amp.autocast (predictors.py:55):
+            # on a GPU that is f16, which the trunks follow; autocast=False -> fp32 trunks
+            with torch.no_grad(), torch.autocast("cuda", enabled=autocast):
+                mc_statistics(model, xi, bi, si, max(world, 2), group=group)   # warm-up
+                di = timed(lambda: mc_statistics(model, xi, bi, si, args.infer_mc, group=group), 1)
+            return {"value": round(args.infer_mc * args.infer_batch / di, 2),
+                    "unit": "MC-samples/s", "batch": args.infer_batch, "num_mc": args.infer_mc,
+                    "ms_per_batch": round(di * 1e3, 1), "sharding": "mc" if world > 1 else "none",
+                    "dtype": "f16 (torch.autocast, as predictors.py:55)" if autocast else "fp32"}
+        infer = infer_run(True)
+        if args.infer_fp32:
+            infer["fp32"] = infer_run(False)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -223,7 +267,7 @@ def main():
                                    f"{args.optical}px + bathy/SSS {args.sonar}px",
                        "global_batch": args.batch * world, "num_mc": args.num_mc,
                        "parallelism": f"dp{world}"},
-            "inference": infer, "roofline": roof, "cpu_baseline": cpu,
+            "inference": infer, "bf16_train": bf16, "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

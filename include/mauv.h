@@ -110,12 +110,20 @@ int mauv_reparam_sample(const float* mu, const float* rho, const float* eps,
 /* Backward of the above: dmu += sum_g dW_g; drho += sum_g dW_g * eps_g' * sigmoid(rho),
  * g' = g (fixed_sample < 0) or the sample `fixed_sample` for every g (bayesian-torch 0.5.0
  * semantics: its eps buffer is overwritten in place by later MC forwards while autograd
- * still references it).  dw element (s, g, i) at dw[s*dw_sstride + g*dw_gstride + i]. */
+ * still references it).  dw element (s, g, i) at dw[s*dw_sstride + g*dw_gstride + i], i in
+ * KRSC order with dw_cin (>= Cin; the 16-bit stems' padded channel count) channels. */
 int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride, long long dw_sstride,
                      const float* mu, const float* rho, const float* eps,
                      unsigned long long seed, unsigned long long sample0, unsigned int layer,
-                     int G, int Cout, int Cin, int RS, float* dmu, float* drho,
+                     int G, int Cout, int Cin, int RS, int dw_cin, float* dmu, float* drho,
                      long long fixed_sample, hipStream_t stream);
+/* 16-bit sampled weights (dtype 0 = bf16, 1 = f16) for the 16-bit convs: KRSC with cin_pad
+ * (>= Cin) input channels; pad channels are not written (zero-fill them once).  The sampling
+ * arithmetic is fp32, only the stored weight is rounded.  out_gstride 0 = Cout*RS*cin_pad. */
+int mauv_reparam_sample_h16(int dtype, const float* mu, const float* rho, const float* eps,
+                            unsigned long long seed, unsigned long long sample0,
+                            unsigned int layer, int G, int Cout, int Cin, int RS, int cin_pad,
+                            void* out, long long out_gstride, hipStream_t stream);
 
 /* get_kl_loss (bayesian-torch 0.5.0; called at train/multimodal.py:114,284 and
  * train/unimodal.py:130,262): sum over entries of mean(log s_p - log s + (s^2 + (mu-m_p)^2)
@@ -170,6 +178,15 @@ int mauv_bn_bwd(const float* y, const float* out, const float* dout, int relu,
                 int G, long long M, int C, float* workspace, float* dy, float* dres,
                 float* dgamma, float* dbeta, const float* pre_p1, const float* pre_p2,
                 int pre_nblk, hipStream_t stream);
+/* 16-bit activations (dtype 0 = bf16, 1 = f16): y/res/out/dout/dy/dres are 16-bit words;
+ * statistics, scale/shift, workspace and dgamma/dbeta fp32 (same maths as above). */
+int mauv_bn_apply_h16(int dtype, const void* y, const float* scale, const float* shift,
+                      const void* res, int relu, void* out, int G, long long M, int C,
+                      hipStream_t stream);
+int mauv_bn_bwd_h16(int dtype, const void* y, const void* out, const void* dout, int relu,
+                    const float* mean, const float* invstd, const float* scale,
+                    const float* shift, int G, long long M, int C, float* workspace, void* dy,
+                    void* dres, float* dgamma, float* dbeta, hipStream_t stream);
 
 /* ---- pooling (pool.hip): torchvision stem maxpool 3x3/2 pad 1 and adaptive avgpool ------ */
 int mauv_maxpool_fwd(const float* x, int N, int H, int W, int C, float* y, unsigned char* idx,
@@ -178,6 +195,19 @@ int mauv_maxpool_bwd(const float* dy, const unsigned char* idx, int N, int H, in
                      float* dx, hipStream_t stream);
 int mauv_avgpool_fwd(const float* x, int N, int HW, int C, float* y, hipStream_t stream);
 int mauv_avgpool_bwd(const float* dy, int N, int HW, int C, float* dx, hipStream_t stream);
+/* 16-bit activations; the pooled features / their gradient stay fp32 (the head is fp32). */
+int mauv_maxpool_fwd_h16(int dtype, const void* x, int N, int H, int W, int C, void* y,
+                         unsigned char* idx, hipStream_t stream);
+int mauv_maxpool_bwd_h16(int dtype, const void* dy, const unsigned char* idx, int N, int H,
+                         int W, int C, void* dx, hipStream_t stream);
+int mauv_avgpool_fwd_h16(int dtype, const void* x, int N, int HW, int C, float* y,
+                         hipStream_t stream);
+int mauv_avgpool_bwd_h16(int dtype, const float* dy, int N, int HW, int C, void* dx,
+                         hipStream_t stream);
+/* Stem input of the 16-bit path: fp32 NCHW [B][C][H][W] -> 16-bit NHWC [B][H][W][Cp], channels
+ * C..Cp-1 zero (the caller's images are read once per trunk, shared by all MC samples). */
+int mauv_pack_nchw_h16(int dtype, const float* x, int B, int C, int H, int W, int Cp, void* y,
+                       hipStream_t stream);
 
 /* ---- fusion head + MC head (head.hip) ----------------------------------------------------
  * AdditiveAttention.forward (models/base_models.py:43-52) epilogues around the q|k|v and

@@ -10,7 +10,7 @@
 // Layout: y/out/dout [G][M][C] (NHWC rows, M = B*H*W), per-group stats [G][C].
 // Statistics: per-thread Welford over a row slab, Chan merges across threads and blocks
 // (double in the final merge) — no E[x^2]-E[x]^2 cancellation.
-#include "mauv_common.h"
+#include "h16.h"
 
 using namespace mauv;
 
@@ -175,40 +175,42 @@ __global__ void bn_running_kernel(int G, int C, const float* __restrict__ mean,
 }
 
 // out = [relu]( y * scale[g][c] + shift[g][c] (+ res) )
-__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ y,
+template <class S>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const typename S::T* __restrict__ y,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
-                                                       const float* __restrict__ res, int relu,
-                                                       float* __restrict__ out, long long M,
-                                                       int C) {
+                                                       const typename S::T* __restrict__ res,
+                                                       int relu, typename S::T* __restrict__ out,
+                                                       long long M, int C) {
   const int c4n = C / 4;
   const long long per_g = M * c4n;
   const int g = blockIdx.y;
-  const float* yg = y + (long long)g * M * C;
-  float* og = out + (long long)g * M * C;
-  const float* rg = res ? res + (long long)g * M * C : nullptr;
+  const typename S::T* yg = y + (long long)g * M * C;
+  typename S::T* og = out + (long long)g * M * C;
+  const typename S::T* rg = res ? res + (long long)g * M * C : nullptr;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < per_g; i += (long long)gridDim.x * 256) {
     const int c = 4 * (int)(i % c4n);
-    floatx4 v = *(const floatx4*)(yg + 4 * i);
+    floatx4 v = S::ld4(yg + 4 * i);
     const floatx4 sc = *(const floatx4*)(scale + g * C + c);
     const floatx4 sh = *(const floatx4*)(shift + g * C + c);
     v = v * sc + sh;
-    if (rg) v += *(const floatx4*)(rg + 4 * i);
+    if (rg) v += S::ld4(rg + 4 * i);
     if (relu) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
     }
-    *(floatx4*)(og + 4 * i) = v;
+    S::st4(og + 4 * i, v);
   }
 }
 
 // ReLU mask of the BN output: from the stored output when there is one (residual blocks),
 // else recomputed from y (lazily-applied BN: out = relu(y*scale + shift) was never stored).
-__device__ __forceinline__ floatx4 relu_mask(floatx4 dz, const float* out, long long o,
+template <class S>
+__device__ __forceinline__ floatx4 relu_mask(floatx4 dz, const typename S::T* out, long long o,
                                              floatx4 yv, const float* scale,
                                              const float* shift, int gc) {
   floatx4 pre;
-  if (out) pre = *(const floatx4*)(out + o);
+  if (out) pre = S::ld4(out + o);
   else pre = yv * *(const floatx4*)(scale + gc) + *(const floatx4*)(shift + gc);
 #pragma unroll
   for (int e = 0; e < 4; ++e) dz[e] = pre[e] > 0.f ? dz[e] : 0.f;
@@ -217,9 +219,11 @@ __device__ __forceinline__ floatx4 relu_mask(floatx4 dz, const float* out, long 
 
 // Backward stage 1: per (g, block) partial sums of dz and dz*xhat per channel,
 // dz = dout * (relu ? out > 0 : 1), xhat = (y - mean) * invstd.
-__global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ y,
-                                                      const float* __restrict__ out,
-                                                      const float* __restrict__ dout, int relu,
+template <class S>
+__global__ __launch_bounds__(256) void bn_bwd_partial(const typename S::T* __restrict__ y,
+                                                      const typename S::T* __restrict__ out,
+                                                      const typename S::T* __restrict__ dout,
+                                                      int relu,
                                                       const float* __restrict__ mean,
                                                       const float* __restrict__ invstd,
                                                       const float* __restrict__ scale,
@@ -248,9 +252,9 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ 
     for (int j = 0; j < MAXCPT; ++j) {
       if (j >= rm.cpt) break;
       const long long o = go + r * C + 4 * (t_c + j * rm.tpr);
-      const floatx4 yv = *(const floatx4*)(y + o);
-      floatx4 dz = *(const floatx4*)(dout + o);
-      if (relu) dz = relu_mask(dz, out, o, yv, scale, shift, g * C + 4 * (t_c + j * rm.tpr));
+      const floatx4 yv = S::ld4(y + o);
+      floatx4 dz = S::ld4(dout + o);
+      if (relu) dz = relu_mask<S>(dz, out, o, yv, scale, shift, g * C + 4 * (t_c + j * rm.tpr));
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         s1[j][e] += dz[e];
@@ -317,17 +321,20 @@ __global__ void bn_bwd_param_kernel(int G, int C, long long M, const float* __re
 }
 
 // dy = gamma*invstd * (dz - k1 - xhat*k2); dres = dz (optional)
-__global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ y,
-                                                    const float* __restrict__ out,
-                                                    const float* __restrict__ dout, int relu,
+template <class S>
+__global__ __launch_bounds__(256) void bn_bwd_apply(const typename S::T* __restrict__ y,
+                                                    const typename S::T* __restrict__ out,
+                                                    const typename S::T* __restrict__ dout,
+                                                    int relu,
                                                     const float* __restrict__ mean,
                                                     const float* __restrict__ invstd,
                                                     const float* __restrict__ scale,
                                                     const float* __restrict__ shift,
                                                     const float* __restrict__ k1,
                                                     const float* __restrict__ k2,
-                                                    float* __restrict__ dy,
-                                                    float* __restrict__ dres, long long M, int C) {
+                                                    typename S::T* __restrict__ dy,
+                                                    typename S::T* __restrict__ dres, long long M,
+                                                    int C) {
   const int c4n = C / 4;
   const long long per_g = M * c4n;
   const int g = blockIdx.y;
@@ -335,17 +342,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ y,
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < per_g; i += (long long)gridDim.x * 256) {
     const int c = 4 * (int)(i % c4n);
     const long long o = go + 4 * i;
-    floatx4 dz = *(const floatx4*)(dout + o);
-    const floatx4 yv = *(const floatx4*)(y + o);
-    if (relu) dz = relu_mask(dz, out, o, yv, scale, shift, g * C + c);
+    floatx4 dz = S::ld4(dout + o);
+    const floatx4 yv = S::ld4(y + o);
+    if (relu) dz = relu_mask<S>(dz, out, o, yv, scale, shift, g * C + c);
     const floatx4 mu = *(const floatx4*)(mean + g * C + c);
     const floatx4 is = *(const floatx4*)(invstd + g * C + c);
     const floatx4 sc = *(const floatx4*)(scale + g * C + c);
     const floatx4 a = *(const floatx4*)(k1 + g * C + c);
     const floatx4 b = *(const floatx4*)(k2 + g * C + c);
     const floatx4 xh = (yv - mu) * is;
-    *(floatx4*)(dy + o) = sc * (dz - a - xh * b);
-    if (dres) *(floatx4*)(dres + o) = dz;
+    S::st4(dy + o, sc * (dz - a - xh * b));
+    if (dres) S::st4(dres + o, dz);
   }
 }
 
@@ -419,7 +426,7 @@ MAUV_API int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const 
     hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
                        mean, uvar, run_mean, run_var, momentum);
   if (out) {
-    hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C / 4 / 1), G), dim3(256), 0, stream,
+    hipLaunchKernelGGL(bn_apply_kernel<SF32>, dim3(ew_grid(M * C / 4 / 1), G), dim3(256), 0, stream,
                        y, scale, shift, res, relu, out, M, C);
   }
   return check_launch("bn_fwd_train");
@@ -444,20 +451,18 @@ MAUV_API int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, 
 MAUV_API int mauv_bn_apply(const float* y, const float* scale, const float* shift,
                            const float* res, int relu, float* out, int G, long long M, int C,
                            hipStream_t stream) {
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C / 4), G), dim3(256), 0, stream, y,
+  hipLaunchKernelGGL(bn_apply_kernel<SF32>, dim3(ew_grid(M * C / 4), G), dim3(256), 0, stream, y,
                      scale, shift, res, relu, out, M, C);
   return check_launch("bn_apply");
 }
 
-// Training-mode BN backward (+ReLU mask from `out`, + residual split):
-//   dy = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)),  dres = dz (nullable),
-//   dgamma += sum dz*xhat, dbeta += sum dz (over all groups; nullable).
-MAUV_API int mauv_bn_bwd(const float* y, const float* out, const float* dout, int relu,
-                         const float* mean, const float* invstd, const float* scale,
-                         const float* shift, int G, long long M, int C, float* workspace,
-                         float* dy, float* dres, float* dgamma, float* dbeta,
-                         const float* pre_p1, const float* pre_p2, int pre_nblk,
-                         hipStream_t stream) {
+template <class S>
+static int bn_bwd_impl(const typename S::T* y, const typename S::T* out,
+                       const typename S::T* dout, int relu, const float* mean,
+                       const float* invstd, const float* scale, const float* shift, int G,
+                       long long M, int C, float* workspace, typename S::T* dy,
+                       typename S::T* dres, float* dgamma, float* dbeta, const float* pre_p1,
+                       const float* pre_p2, int pre_nblk, hipStream_t stream) {
   if (C % 4 != 0 || C > 2048) { set_error("bn_bwd: unsupported C"); return kErrArg; }
   if (relu && !out && !shift) { set_error("bn_bwd: relu mask needs out or scale/shift"); return kErrArg; }
   int nblk, rpb;
@@ -471,15 +476,52 @@ MAUV_API int mauv_bn_bwd(const float* y, const float* out, const float* dout, in
     hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, pre_nblk,
                        C, M, pre_p1, pre_p2, k1, k2);
   } else {
-    hipLaunchKernelGGL(bn_bwd_partial, dim3(nblk, G), dim3(256), 0, stream, y, out, dout, relu,
-                       mean, invstd, scale, shift, M, C, rpb, rm, p1, p2);
+    hipLaunchKernelGGL(bn_bwd_partial<S>, dim3(nblk, G), dim3(256), 0, stream, y, out, dout,
+                       relu, mean, invstd, scale, shift, M, C, rpb, rm, p1, p2);
     hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, nblk, C,
                        M, p1, p2, k1, k2);
   }
   if (dgamma || dbeta)
     hipLaunchKernelGGL(bn_bwd_param_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C, M,
                        k1, k2, dgamma, dbeta);
-  hipLaunchKernelGGL(bn_bwd_apply, dim3(ew_grid(M * C / 4), G), dim3(256), 0, stream, y, out,
+  hipLaunchKernelGGL(bn_bwd_apply<S>, dim3(ew_grid(M * C / 4), G), dim3(256), 0, stream, y, out,
                      dout, relu, mean, invstd, scale, shift, k1, k2, dy, dres, M, C);
   return check_launch("bn_bwd");
+}
+
+// Training-mode BN backward (+ReLU mask from `out`, + residual split):
+//   dy = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)),  dres = dz (nullable),
+//   dgamma += sum dz*xhat, dbeta += sum dz (over all groups; nullable).
+MAUV_API int mauv_bn_bwd(const float* y, const float* out, const float* dout, int relu,
+                         const float* mean, const float* invstd, const float* scale,
+                         const float* shift, int G, long long M, int C, float* workspace,
+                         float* dy, float* dres, float* dgamma, float* dbeta,
+                         const float* pre_p1, const float* pre_p2, int pre_nblk,
+                         hipStream_t stream) {
+  return bn_bwd_impl<SF32>(y, out, dout, relu, mean, invstd, scale, shift, G, M, C, workspace,
+                           dy, dres, dgamma, dbeta, pre_p1, pre_p2, pre_nblk, stream);
+}
+
+// 16-bit activations (dtype 0 = bf16, 1 = f16): y/out/dout/dy/dres are 16-bit, statistics,
+// scale/shift, workspace and parameter gradients fp32.
+MAUV_API int mauv_bn_apply_h16(int dtype, const void* y, const float* scale, const float* shift,
+                               const void* res, int relu, void* out, int G, long long M, int C,
+                               hipStream_t stream) {
+#define L(D) hipLaunchKernelGGL(bn_apply_kernel<S16<D>>, dim3(ew_grid(M * C / 4), G), dim3(256), 0, \
+                                stream, (const u16*)y, scale, shift, (const u16*)res, relu, (u16*)out, M, C);
+  MAUV_DT_DISPATCH(dtype, "bn_apply_h16", L)
+#undef L
+  return check_launch("bn_apply_h16");
+}
+
+MAUV_API int mauv_bn_bwd_h16(int dtype, const void* y, const void* out, const void* dout,
+                             int relu, const float* mean, const float* invstd, const float* scale,
+                             const float* shift, int G, long long M, int C, float* workspace,
+                             void* dy, void* dres, float* dgamma, float* dbeta,
+                             hipStream_t stream) {
+#define L(D) return bn_bwd_impl<S16<D>>((const u16*)y, (const u16*)out, (const u16*)dout, relu, mean, \
+                                        invstd, scale, shift, G, M, C, workspace, (u16*)dy,       \
+                                        (u16*)dres, dgamma, dbeta, nullptr, nullptr, 0, stream);
+  MAUV_DT_DISPATCH(dtype, "bn_bwd_h16", L)
+#undef L
 }

@@ -66,3 +66,45 @@ __device__ __forceinline__ u32x4 pack8(floatx8 f) {
 }
 
 }  // namespace mauv
+
+namespace mauv {
+
+// Storage policies for kernels shared by the fp32 and 16-bit paths: values are always
+// computed in fp32; S::T is what sits in HBM.
+struct SF32 {
+  typedef float T;
+  static __device__ __forceinline__ float ld(const T* p) { return *p; }
+  static __device__ __forceinline__ void st(T* p, float v) { *p = v; }
+  static __device__ __forceinline__ floatx4 ld4(const T* p) { return *(const floatx4*)p; }
+  static __device__ __forceinline__ void st4(T* p, floatx4 v) { *(floatx4*)p = v; }
+};
+
+template <int DT>
+struct S16 {
+  typedef u16 T;
+  static __device__ __forceinline__ float ld(const T* p) { return H16<DT>::to_f(*p); }
+  static __device__ __forceinline__ void st(T* p, float v) { *p = H16<DT>::from_f(v); }
+  static __device__ __forceinline__ floatx4 ld4(const T* p) {
+    const uint2 u = *(const uint2*)p;
+    floatx4 f;
+    f[0] = H16<DT>::to_f((u16)(u.x & 0xffffu));
+    f[1] = H16<DT>::to_f((u16)(u.x >> 16));
+    f[2] = H16<DT>::to_f((u16)(u.y & 0xffffu));
+    f[3] = H16<DT>::to_f((u16)(u.y >> 16));
+    return f;
+  }
+  static __device__ __forceinline__ void st4(T* p, floatx4 v) {
+    uint2 u;
+    u.x = (unsigned)H16<DT>::from_f(v[0]) | ((unsigned)H16<DT>::from_f(v[1]) << 16);
+    u.y = (unsigned)H16<DT>::from_f(v[2]) | ((unsigned)H16<DT>::from_f(v[3]) << 16);
+    *(uint2*)p = u;
+  }
+};
+
+}  // namespace mauv
+
+// Dispatch a C-ABI dtype code to a launch macro L(DT) (returns kErrArg on a bad code).
+#define MAUV_DT_DISPATCH(dtype, what, L)                                      \
+  if (dtype == mauv::DT_BF16) { L(mauv::DT_BF16) }                            \
+  else if (dtype == mauv::DT_F16) { L(mauv::DT_F16) }                         \
+  else { mauv::set_error(std::string(what) + ": dtype must be 0 (bf16) or 1 (f16)"); return mauv::kErrArg; }

@@ -1,16 +1,19 @@
 // ResNet-50 stem max-pool (3x3 / 2, pad 1) and the adaptive average pool to 1x1, NHWC,
 // forward + backward (torchvision resnet50 as used at models/base_models.py:15 and
 // models/model_utils.py:57).  N = G*B images (the MC groups are just more images here).
-#include "mauv_common.h"
+// Templated on the activation storage (fp32 or 16-bit, h16.h); arithmetic in fp32.  The
+// average pool's pooled features are always fp32 (the fusion head runs in fp32).
+#include "h16.h"
 
 using namespace mauv;
 
 namespace mauv {
 
 // Tie-break as torch's max_pool2d: first maximum in (kh, kw) scan order; NaN wins.
-__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restrict__ x, int N,
-                                                          int H, int W, int C, int Ho, int Wo,
-                                                          float* __restrict__ y,
+template <class S>
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const typename S::T* __restrict__ x,
+                                                          int N, int H, int W, int C, int Ho,
+                                                          int Wo, typename S::T* __restrict__ y,
                                                           unsigned char* __restrict__ idx) {
   const long long total = (long long)N * Ho * Wo * C;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
@@ -27,19 +30,20 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restric
       for (int s = 0; s < 3; ++s) {
         const int iw = ow * 2 - 1 + s;
         if (iw < 0 || iw >= W) continue;
-        const float v = x[(((long long)n * H + ih) * W + iw) * C + c];
+        const float v = S::ld(x + (((long long)n * H + ih) * W + iw) * C + c);
         if (v > best || isnan(v)) { best = v; bi = r * 3 + s; }
       }
     }
-    y[i] = best;
+    S::st(y + i, best);
     idx[i] = (unsigned char)bi;
   }
 }
 
-__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ dy,
+template <class S>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const typename S::T* __restrict__ dy,
                                                           const unsigned char* __restrict__ idx,
                                                           int N, int H, int W, int C, int Ho,
-                                                          int Wo, float* __restrict__ dx) {
+                                                          int Wo, typename S::T* __restrict__ dx) {
   const long long total = (long long)N * H * W * C;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const int c = (int)(i % C);
@@ -57,35 +61,53 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
         const int s = iw - (ow * 2 - 1);
         if (s < 0 || s > 2) continue;
         const long long o = (((long long)n * Ho + oh) * Wo + ow) * C + c;
-        if (idx[o] == r * 3 + s) acc += dy[o];
+        if (idx[o] == r * 3 + s) acc += S::ld(dy + o);
       }
     }
-    dx[i] = acc;
+    S::st(dx + i, acc);
   }
 }
 
-__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restrict__ x, int N,
-                                                          int HW, int C, float* __restrict__ y) {
+template <class S>
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const typename S::T* __restrict__ x,
+                                                          int N, int HW, int C,
+                                                          float* __restrict__ y) {
   const long long total = (long long)N * C;
   const float inv = 1.0f / (float)HW;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const int c = (int)(i % C);
     const long long n = i / C;
-    const float* src = x + n * HW * C + c;
+    const typename S::T* src = x + n * HW * C + c;
     float acc = 0.f;
-    for (int p = 0; p < HW; ++p) acc += src[(long long)p * C];
+    for (int p = 0; p < HW; ++p) acc += S::ld(src + (long long)p * C);
     y[i] = acc * inv;
   }
 }
 
+template <class S>
 __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restrict__ dy, int N,
-                                                          int HW, int C, float* __restrict__ dx) {
+                                                          int HW, int C,
+                                                          typename S::T* __restrict__ dx) {
   const long long total = (long long)N * HW * C;
   const float inv = 1.0f / (float)HW;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const int c = (int)(i % C);
     const long long n = i / ((long long)HW * C);
-    dx[i] = dy[n * C + c] * inv;
+    S::st(dx + i, dy[n * C + c] * inv);
+  }
+}
+
+// Stem input for the 16-bit path: the caller's fp32 NCHW images -> 16-bit NHWC with the
+// channels zero-padded to Cp (8), so the stem conv runs on 16-byte channel chunks.
+template <int DT>
+__global__ __launch_bounds__(256) void pack_nchw_kernel(const float* __restrict__ x, int B, int C,
+                                                        int HW, int Cp, u16* __restrict__ y) {
+  const long long total = (long long)B * HW * Cp;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % Cp);
+    const long long p = i / Cp;
+    const long long b = p / HW, hw = p - b * HW;
+    y[i] = c < C ? H16<DT>::from_f(x[(b * C + c) * HW + hw]) : (u16)0;
   }
 }
 
@@ -100,28 +122,78 @@ static int grid1(long long n) {
 MAUV_API int mauv_maxpool_fwd(const float* x, int N, int H, int W, int C, float* y,
                               unsigned char* idx, hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid1((long long)N * Ho * Wo * C)), dim3(256), 0,
-                     stream, x, N, H, W, C, Ho, Wo, y, idx);
+  hipLaunchKernelGGL(maxpool_fwd_kernel<SF32>, dim3(grid1((long long)N * Ho * Wo * C)), dim3(256),
+                     0, stream, x, N, H, W, C, Ho, Wo, y, idx);
   return check_launch("maxpool_fwd");
 }
 
 MAUV_API int mauv_maxpool_bwd(const float* dy, const unsigned char* idx, int N, int H, int W,
                               int C, float* dx, hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid1((long long)N * H * W * C)), dim3(256), 0,
-                     stream, dy, idx, N, H, W, C, Ho, Wo, dx);
+  hipLaunchKernelGGL(maxpool_bwd_kernel<SF32>, dim3(grid1((long long)N * H * W * C)), dim3(256),
+                     0, stream, dy, idx, N, H, W, C, Ho, Wo, dx);
   return check_launch("maxpool_bwd");
 }
 
 MAUV_API int mauv_avgpool_fwd(const float* x, int N, int HW, int C, float* y, hipStream_t stream) {
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid1((long long)N * C)), dim3(256), 0, stream, x,
-                     N, HW, C, y);
+  hipLaunchKernelGGL(avgpool_fwd_kernel<SF32>, dim3(grid1((long long)N * C)), dim3(256), 0,
+                     stream, x, N, HW, C, y);
   return check_launch("avgpool_fwd");
 }
 
 MAUV_API int mauv_avgpool_bwd(const float* dy, int N, int HW, int C, float* dx,
                               hipStream_t stream) {
-  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid1((long long)N * HW * C)), dim3(256), 0,
+  hipLaunchKernelGGL(avgpool_bwd_kernel<SF32>, dim3(grid1((long long)N * HW * C)), dim3(256), 0,
                      stream, dy, N, HW, C, dx);
   return check_launch("avgpool_bwd");
+}
+
+// ---- 16-bit activations (dtype 0 = bf16, 1 = f16) ----
+
+MAUV_API int mauv_maxpool_fwd_h16(int dtype, const void* x, int N, int H, int W, int C, void* y,
+                                  unsigned char* idx, hipStream_t stream) {
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+#define L(D) hipLaunchKernelGGL(maxpool_fwd_kernel<S16<D>>, dim3(grid1((long long)N * Ho * Wo * C)), \
+                                dim3(256), 0, stream, (const u16*)x, N, H, W, C, Ho, Wo, (u16*)y, idx);
+  MAUV_DT_DISPATCH(dtype, "maxpool_fwd_h16", L)
+#undef L
+  return check_launch("maxpool_fwd_h16");
+}
+
+MAUV_API int mauv_maxpool_bwd_h16(int dtype, const void* dy, const unsigned char* idx, int N,
+                                  int H, int W, int C, void* dx, hipStream_t stream) {
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+#define L(D) hipLaunchKernelGGL(maxpool_bwd_kernel<S16<D>>, dim3(grid1((long long)N * H * W * C)), \
+                                dim3(256), 0, stream, (const u16*)dy, idx, N, H, W, C, Ho, Wo, (u16*)dx);
+  MAUV_DT_DISPATCH(dtype, "maxpool_bwd_h16", L)
+#undef L
+  return check_launch("maxpool_bwd_h16");
+}
+
+MAUV_API int mauv_avgpool_fwd_h16(int dtype, const void* x, int N, int HW, int C, float* y,
+                                  hipStream_t stream) {
+#define L(D) hipLaunchKernelGGL(avgpool_fwd_kernel<S16<D>>, dim3(grid1((long long)N * C)), dim3(256), \
+                                0, stream, (const u16*)x, N, HW, C, y);
+  MAUV_DT_DISPATCH(dtype, "avgpool_fwd_h16", L)
+#undef L
+  return check_launch("avgpool_fwd_h16");
+}
+
+MAUV_API int mauv_avgpool_bwd_h16(int dtype, const float* dy, int N, int HW, int C, void* dx,
+                                  hipStream_t stream) {
+#define L(D) hipLaunchKernelGGL(avgpool_bwd_kernel<S16<D>>, dim3(grid1((long long)N * HW * C)), \
+                                dim3(256), 0, stream, dy, N, HW, C, (u16*)dx);
+  MAUV_DT_DISPATCH(dtype, "avgpool_bwd_h16", L)
+#undef L
+  return check_launch("avgpool_bwd_h16");
+}
+
+MAUV_API int mauv_pack_nchw_h16(int dtype, const float* x, int B, int C, int H, int W, int Cp,
+                                void* y, hipStream_t stream) {
+  if (Cp < C) { set_error("pack_nchw_h16: Cp < C"); return kErrArg; }
+#define L(D) hipLaunchKernelGGL(pack_nchw_kernel<D>, dim3(grid1((long long)B * H * W * Cp)), dim3(256), \
+                                0, stream, x, B, C, H * W, Cp, (u16*)y);
+  MAUV_DT_DISPATCH(dtype, "pack_nchw_h16", L)
+#undef L
+  return check_launch("pack_nchw_h16");
 }

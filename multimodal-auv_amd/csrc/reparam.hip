@@ -13,16 +13,17 @@
 // Sampled weights are written in the GEMM layout [G][Cout][R][S][Cin] (KRSC) consumed by
 // conv_gemm.hip; parameters / gradients stay in the reference's OIHW layout so state_dicts
 // keep bayesian-torch's shapes.
-#include "mauv_common.h"
+#include "h16.h"
 
 using namespace mauv;
 
 namespace mauv {
 
+template <class S>
 __global__ __launch_bounds__(256) void reparam_sample_kernel(
     const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
-    uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS,
-    float* __restrict__ out, long long out_gs) {
+    uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS, int cin_pad,
+    typename S::T* __restrict__ out, long long out_gs) {
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
   for (long long q = blockIdx.x * 256LL + threadIdx.x; q < nq; q += (long long)gridDim.x * 256) {
@@ -37,7 +38,7 @@ __global__ __launch_bounds__(256) void reparam_sample_kernel(
         const long long o = i / ((long long)Cin * RS);
         const long long rem = i - o * Cin * RS;
         const int c = (int)(rem / RS), rs = (int)(rem - (long long)c * RS);
-        dst[e] = (o * RS + rs) * Cin + c;
+        dst[e] = (o * RS + rs) * cin_pad + c;
       } else {
         m[e] = 0.f; s[e] = 0.f; dst[e] = -1;
       }
@@ -50,10 +51,10 @@ __global__ __launch_bounds__(256) void reparam_sample_kernel(
       } else {
         ep = normal4(seed, sample0 + g, layer, (uint32_t)q);
       }
-      float* og = out + (long long)g * out_gs;
+      typename S::T* og = out + (long long)g * out_gs;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        if (dst[e] >= 0) og[dst[e]] = m[e] + s[e] * ep[e];
+        if (dst[e] >= 0) S::st(og + dst[e], m[e] + s[e] * ep[e]);
     }
   }
 }
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(256) void reparam_bwd_kernel(
     const float* __restrict__ dw, int splits, long long dw_gs, long long dw_ss,
     const float* __restrict__ mu,
     const float* __restrict__ rho, const float* __restrict__ eps, uint64_t seed,
-    uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS,
+    uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS, int cin_pad,
     float* __restrict__ dmu, float* __restrict__ drho, long long fixed) {
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(256) void reparam_bwd_kernel(
         const long long o = i / ((long long)Cin * RS);
         const long long rem = i - o * Cin * RS;
         const int c = (int)(rem / RS), rs = (int)(rem - (long long)c * RS);
-        src[e] = (o * RS + rs) * Cin + c;
+        src[e] = (o * RS + rs) * cin_pad + c;
       } else {
         sg[e] = 0.f; src[e] = -1;
       }
@@ -197,10 +198,30 @@ MAUV_API int mauv_reparam_sample(const float* mu, const float* rho, const float*
                                  float* out, long long out_gstride, hipStream_t stream) {
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
-  hipLaunchKernelGGL(reparam_sample_kernel, dim3(grid_for(nq)), dim3(256), 0, stream, mu, rho,
-                     eps, seed, sample0, layer, G, Cout, Cin, RS, out,
+  hipLaunchKernelGGL(reparam_sample_kernel<SF32>, dim3(grid_for(nq)), dim3(256), 0, stream, mu,
+                     rho, eps, seed, sample0, layer, G, Cout, Cin, RS, Cin, out,
                      out_gstride ? out_gstride : numel);
   return check_launch("reparam_sample");
+}
+
+// 16-bit sampled weights (dtype 0 = bf16, 1 = f16) for the 16-bit convs, KRSC with the input
+// channels padded to cin_pad (pad channels are left untouched: the caller zero-fills them
+// once).  Sampling arithmetic is fp32; only the stored weight is rounded.
+MAUV_API int mauv_reparam_sample_h16(int dtype, const float* mu, const float* rho,
+                                     const float* eps, unsigned long long seed,
+                                     unsigned long long sample0, unsigned int layer, int G,
+                                     int Cout, int Cin, int RS, int cin_pad, void* out,
+                                     long long out_gstride, hipStream_t stream) {
+  if (cin_pad < Cin) { set_error("reparam_sample_h16: cin_pad < Cin"); return kErrArg; }
+  const long long numel = (long long)Cout * Cin * RS;
+  const long long nq = (numel + 3) / 4;
+  const long long gs = out_gstride ? out_gstride : (long long)Cout * RS * cin_pad;
+#define L(D) hipLaunchKernelGGL(reparam_sample_kernel<S16<D>>, dim3(grid_for(nq)), dim3(256), 0, \
+                                stream, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS,   \
+                                cin_pad, (u16*)out, gs);
+  MAUV_DT_DISPATCH(dtype, "reparam_sample_h16", L)
+#undef L
+  return check_launch("reparam_sample_h16");
 }
 
 // dmu += sum_g sum_s dw[s][g];  drho += sum_g (sum_s dw[s][g]) * eps_g' * sigmoid(rho), where
@@ -209,19 +230,21 @@ MAUV_API int mauv_reparam_sample(const float* mu, const float* rho, const float*
 // `eps = self.eps_kernel.data.normal_()`, so when several MC forwards precede one backward
 // autograd's saved eps aliases the buffer and every pass's rho-gradient sees the LAST draw).
 // dw element (s, g, i) at dw[s*dw_sstride + g*dw_gstride + i] (strides 0 = dense
-// [splits][G][numel]); i in the KRSC weight layout.
+// [splits][G][Cout*RS*dw_cin]); i in the KRSC weight layout with dw_cin (>= Cin) channels
+// (the 16-bit stems' zero-padded input channels are skipped).
 MAUV_API int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride,
                               long long dw_sstride, const float* mu, const float* rho,
                               const float* eps, unsigned long long seed,
                               unsigned long long sample0, unsigned int layer, int G, int Cout,
-                              int Cin, int RS, float* dmu, float* drho,
+                              int Cin, int RS, int dw_cin, float* dmu, float* drho,
                               long long fixed_sample, hipStream_t stream) {
+  if (dw_cin < Cin) { set_error("reparam_bwd: dw_cin < Cin"); return kErrArg; }
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
-  const long long gs = dw_gstride ? dw_gstride : numel;
+  const long long gs = dw_gstride ? dw_gstride : (long long)Cout * RS * dw_cin;
   const long long ss = dw_sstride ? dw_sstride : gs * G;
   hipLaunchKernelGGL(reparam_bwd_kernel, dim3(grid_for(nq)), dim3(256), 0, stream, dw, splits,
-                     gs, ss, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS, dmu, drho,
+                     gs, ss, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS, dw_cin, dmu, drho,
                      fixed_sample >= 0 ? (long long)(fixed_sample - (long long)sample0) : -1LL);
   return check_launch("reparam_bwd");
 }

@@ -37,7 +37,8 @@ SIGNATURES = {
     "mauv_conv2d_bwd_weight_h16": [I, P, P, P, P, I, P, P, I] + [I] * 10 + [P],
     # reparam.hip
     "mauv_reparam_sample": [P, P, P, U64, U64, U32, I, I, I, I, P, LL, P],
-    "mauv_reparam_bwd": [P, I, LL, LL, P, P, P, U64, U64, U32, I, I, I, I, P, P, LL, P],
+    "mauv_reparam_bwd": [P, I, LL, LL, P, P, P, U64, U64, U32, I, I, I, I, I, P, P, LL, P],
+    "mauv_reparam_sample_h16": [I, P, P, P, U64, U64, U32, I, I, I, I, I, P, LL, P],
     "mauv_kl_workspace_bytes": [I],
     "mauv_kl_fwd": [P, I, P, F, P, P],
     "mauv_kl_bwd": [P, I, P, F, P],
@@ -49,11 +50,18 @@ SIGNATURES = {
     "mauv_bn_apply": [P, P, P, P, I, P, I, LL, I, P],
     "mauv_bn_eval_params": [I, I, P, P, P, P, F, P, P, P],
     "mauv_bn_bwd": [P, P, P, I, P, P, P, P, I, LL, I, P, P, P, P, P, P, P, I, P],
+    "mauv_bn_apply_h16": [I, P, P, P, P, I, P, I, LL, I, P],
+    "mauv_bn_bwd_h16": [I, P, P, P, I, P, P, P, P, I, LL, I, P, P, P, P, P, P],
     # pool.hip
     "mauv_maxpool_fwd": [P, I, I, I, I, P, P, P],
     "mauv_maxpool_bwd": [P, P, I, I, I, I, P, P],
     "mauv_avgpool_fwd": [P, I, I, I, P, P],
     "mauv_avgpool_bwd": [P, I, I, I, P, P],
+    "mauv_maxpool_fwd_h16": [I, P, I, I, I, I, P, P, P],
+    "mauv_maxpool_bwd_h16": [I, P, P, I, I, I, I, P, P],
+    "mauv_avgpool_fwd_h16": [I, P, I, I, I, P, P],
+    "mauv_avgpool_bwd_h16": [I, P, I, I, I, P, P],
+    "mauv_pack_nchw_h16": [I, P, I, I, I, I, I, P, P],
     # head.hip
     "mauv_attn_t": [P, I, P, P],
     "mauv_attn_t_bwd": [P, P, I, P, P],

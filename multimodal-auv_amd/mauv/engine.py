@@ -77,6 +77,18 @@ class RootState:
         # the LAST forward before backward — its eps buffer is overwritten in place while
         # autograd still references it); "exact": per-sample reparameterisation gradient.
         self.rho_grad = "reference"
+        # trunk activation/weight storage: None = follow torch.autocast (the reference's
+        # predictor runs under torch.amp.autocast, inference/predictors.py:55), else a dtype
+        self.precision = None
+
+    def trunk_dtype(self):
+        if self.precision is not None:
+            return self.precision
+        if torch.is_autocast_enabled("cuda"):
+            dt = torch.get_autocast_dtype("cuda")
+            if dt in (torch.bfloat16, torch.float16):
+                return dt
+        return torch.float32
 
     def layer_id(self, m, bias=False):
         return 2 * self.ids[id(m)] + int(bias)
@@ -111,6 +123,15 @@ def set_rho_grad_mode(root, mode):
     root_state(root).rho_grad = mode
 
 
+def set_precision(root, dtype):
+    """Storage/compute format of the three trunks: torch.float32 (exact fp32 MFMA),
+    torch.bfloat16 (BASELINE configs[2] training) or torch.float16 (16-bit MFMA, fp32
+    accumulation, BN statistics, weight gradients and master parameters); None follows
+    torch.autocast("cuda") like the reference's own ops do.  The fusion head is fp32."""
+    assert dtype in (None, torch.float32, torch.bfloat16, torch.float16)
+    root_state(root).precision = dtype
+
+
 def needs_grad(params):
     return torch.is_grad_enabled() and any(p.requires_grad for p in params)
 
@@ -142,19 +163,21 @@ class _Runner:
         return None if fn is None else fn(m, name, self.G)
 
     # ---- Bayesian parameter sampling (mauv_reparam_sample) ----
-    def _sample(self, m, mu, rho, name, out, Cout, Cin, RS, bias=False, out_gstride=0):
+    def _sample(self, m, mu, rho, name, out, Cout, Cin, RS, bias=False, out_gstride=0,
+                cin_pad=None):
         ops.reparam_sample(mu, rho, out, self.G, self.st.seed, self.s0,
                            self.st.layer_id(m, bias), Cout, Cin, RS, eps=self._eps(m, name),
-                           out_gstride=out_gstride)
+                           out_gstride=out_gstride, cin_pad=cin_pad)
 
     def _reparam_bwd(self, m, mu, rho, dw, splits, Cout, Cin, RS, name, bias=False,
-                     dw_gstride=0, dw_sstride=0):
+                     dw_gstride=0, dw_sstride=0, dw_cin=None):
         if not mu.requires_grad:
             return
         fixed = self.st.offset - 1 if self.st.rho_grad == "reference" else -1
         ops.reparam_bwd(dw, splits, mu, rho, mu.grad, rho.grad, self.G, self.st.seed, self.s0,
                         self.st.layer_id(m, bias), Cout, Cin, RS, eps=self._eps(m, name),
-                        dw_gstride=dw_gstride, dw_sstride=dw_sstride, fixed_sample=fixed)
+                        dw_gstride=dw_gstride, dw_sstride=dw_sstride, fixed_sample=fixed,
+                        dw_cin=dw_cin)
 
     # ---- linear = 1x1 conv on [G][rows][K] ----
     def _linear(self, lin, x, rows):
@@ -232,25 +255,33 @@ class TrunkRunner(_Runner):
       its output gradient.
     """
 
-    def __init__(self, trunk, state, G, sample0, save):
+    def __init__(self, trunk, state, G, sample0, save, dtype=torch.float32):
         super().__init__(state, G, sample0, save)
         self.trunk = trunk
+        self.dt = dtype   # activation / sampled-weight storage (fp32, bf16 or f16)
+
+    def _cin_pad(self, Cin):
+        """16-bit convs move 8-channel chunks: the stems' 1/3 input channels pad to 8."""
+        return Cin if self.dt == torch.float32 or Cin % 8 == 0 else (Cin + 7) // 8 * 8
 
     # ---- conv / bn units ----
     def _conv(self, conv, x, B, H, W, x_strides=None, x_bn=None, bn_stats=True):
         G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
         st, pd = conv.stride[0], conv.padding[0]
-        w = torch.empty(G, Cout, k, k, Cin, device=x.device)
-        self._sample(conv, conv.mu_kernel, conv.rho_kernel, "kernel", w, Cout, Cin, k * k)
+        cp = self._cin_pad(Cin)
+        alloc = torch.zeros if cp != Cin else torch.empty
+        w = alloc(G, Cout, k, k, cp, device=x.device, dtype=self.dt)
+        self._sample(conv, conv.mu_kernel, conv.rho_kernel, "kernel", w, Cout, Cin, k * k,
+                     cin_pad=cp)
         Ho, Wo = ops.out_hw(H, k, st, pd), ops.out_hw(W, k, st, pd)
-        y = torch.empty(G, B, Ho, Wo, Cout, device=x.device)
+        y = torch.empty(G, B, Ho, Wo, Cout, device=x.device, dtype=self.dt)
         part = None
         if bn_stats:
             nblk = ops.fwd_stat_blocks(G, B, H, W, Cin, Cout, k, st, pd)
             buf = torch.empty(2 * G * nblk * Cout + G * nblk, device=x.device)
             part = (buf[:G * nblk * Cout], buf[G * nblk * Cout:2 * G * nblk * Cout],
                     buf[2 * G * nblk * Cout:], nblk)
-        ops.conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, k, st, pd, x_strides=x_strides,
+        ops.conv2d_fwd(x, w, y, G, B, H, W, cp, Cout, k, st, pd, x_strides=x_strides,
                        x_bn=x_bn, stats=None if part is None else part[:3])
         rec = (conv, x, x_strides, x_bn, w, B, H, W) if self.save else None
         return y, rec, part
@@ -261,20 +292,22 @@ class TrunkRunner(_Runner):
         conv, x, xs, x_bn, w, B, H, W = rec
         G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
         st, pd = conv.stride[0], conv.padding[0]
+        cp = self._cin_pad(Cin)
         if conv.mu_kernel.requires_grad:
-            splits = ops.wgrad_splits(G, B, H, W, Cin, Cout, k, st, pd)
-            ws = torch.empty(splits, G, Cout, k * k * Cin, device=dy.device)
-            ops.conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, k, st, pd,
+            splits = ops.wgrad_splits(G, B, H, W, cp, Cout, k, st, pd)
+            ws = torch.empty(splits, G, Cout, k * k * cp, device=dy.device)
+            ops.conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, cp, Cout, k, st, pd,
                                   x_strides=xs, x_bn=x_bn)
             self._reparam_bwd(conv, conv.mu_kernel, conv.rho_kernel, ws, splits, Cout, Cin,
-                              k * k, "kernel")
+                              k * k, "kernel", dw_cin=cp)
             del ws
         if not need_dx:
             return None, None
         if dx is None:
-            dx = torch.empty(G, B, H, W, Cin, device=dy.device)
+            dx = torch.empty(G, B, H, W, Cin, device=dy.device, dtype=self.dt)
         bn_args, pre = (None, None)
-        if DGRAD_BN_EPILOGUE and bn_out is not None and bn_out.batch_stats:
+        if DGRAD_BN_EPILOGUE and self.dt == torch.float32 and bn_out is not None \
+                and bn_out.batch_stats:
             bn_args, pre = bn_out.epilogue_args(G, (B, H, W, Cin, Cout, k, st, pd))
         ops.conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, k, st, pd, addend=addend,
                             accumulate=accumulate, bn=bn_args)
@@ -337,12 +370,19 @@ class TrunkRunner(_Runner):
             raise ValueError(f"trunk expects {t.conv1.in_channels} input channels, got {Cin}")
         self.B = B
         recs = self.recs = []
-        y, rc, part = self._conv(t.conv1, x, B, H, W, x_strides=(0, Cin * H * W, W, 1, H * W))
+        if self.dt == torch.float32:   # the stem reads the caller's NCHW images in place
+            xs = (0, Cin * H * W, W, 1, H * W)
+        else:                          # 16-bit NHWC copy, channels zero-padded to 8
+            cp = self._cin_pad(Cin)
+            xh = torch.empty(B, H, W, cp, device=x.device, dtype=self.dt)
+            ops.pack_nchw(x, B, Cin, H, W, cp, xh)
+            x, xs = xh, (0, H * W * cp, W * cp, cp, 1)
+        y, rc, part = self._conv(t.conv1, x, B, H, W, x_strides=xs)
         a, rb = self._bn(t.bn1, y, part, relu=True)
         del y, part
         H, W = a.shape[2], a.shape[3]
         Hp, Wp = ops.out_hw(H, 3, 2, 1), ops.out_hw(W, 3, 2, 1)
-        p = torch.empty(G, B, Hp, Wp, 64, device=x.device)
+        p = torch.empty(G, B, Hp, Wp, 64, device=x.device, dtype=self.dt)
         idx = torch.empty(G, B, Hp, Wp, 64, dtype=torch.uint8, device=x.device)
         ops.maxpool_fwd(a, G * B, H, W, 64, p, idx)
         self.stem = (rc, rb, idx, (H, W)) if self.save else None
@@ -390,7 +430,7 @@ class TrunkRunner(_Runner):
         else:
             dfeat = dout
         H, W = self.final_hw
-        da = torch.empty(G, B, H, W, 2048, device=dout.device)
+        da = torch.empty(G, B, H, W, 2048, device=dout.device, dtype=self.dt)
         ops.avgpool_bwd(dfeat, G * B, H * W, 2048, da)
         del dfeat
         pre = None  # bn3 partials of the block being entered (from the previous dgrad epilogue)
@@ -420,7 +460,7 @@ class TrunkRunner(_Runner):
             da = dx
         rc, rb, idx, (H, W) = self.stem
         self.stem = None
-        da0 = torch.empty(G, B, H, W, 64, device=da.device)
+        da0 = torch.empty(G, B, H, W, 64, device=da.device, dtype=self.dt)
         ops.maxpool_bwd(da, idx, G * B, H, W, 64, da0)
         del da, idx
         dy0, _ = self._bn_bwd(rb, da0)
@@ -546,8 +586,11 @@ def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None):
     s0 = st.next_samples(num_mc) if sample0 is None else sample0
     params = list(trunk.parameters())
     save = needs_grad(params)
-    runner = TrunkRunner(trunk, st, num_mc, s0, save)
-    return _run(runner, params, (_to_device(x, dev),), save)
+    runner = TrunkRunner(trunk, st, num_mc, s0, save, st.trunk_dtype())
+    x = _to_device(x, dev)
+    if x.dtype != torch.float32:   # autocast callers may hand 16-bit images; stems read fp32
+        x = x.float()
+    return _run(runner, params, (x,), save)
 
 
 def run_multimodal_mc(model, inputs, bathy, sss, num_mc):

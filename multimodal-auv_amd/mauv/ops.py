@@ -168,20 +168,29 @@ def conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, R, stride, pad,
 
 # ----------------------------------------------------------------------- reparam / KL
 def reparam_sample(mu, rho, out, G, seed, sample0, layer, Cout, Cin, RS, eps=None,
-                   out_gstride=0):
-    """out[g] (KRSC, group stride out_gstride or numel) = mu + softplus(rho) * eps_g."""
+                   out_gstride=0, cin_pad=None):
+    """out[g] (KRSC, group stride out_gstride or numel) = mu + softplus(rho) * eps_g.
+    A bf16/f16 `out` gets 16-bit weights with cin_pad (>= Cin) channels (pad untouched)."""
     _f32(mu, rho, eps)
+    if out.dtype in H16:
+        check(lib.mauv_reparam_sample_h16(H16[out.dtype], _p(mu), _p(rho), _p(eps), seed, sample0,
+                                          layer, G, Cout, Cin, RS, cin_pad or Cin, _p(out),
+                                          out_gstride, stream()), "reparam_sample_h16")
+        return
+    assert cin_pad in (None, Cin)
     check(lib.mauv_reparam_sample(_p(mu), _p(rho), _p(eps), seed, sample0, layer, G, Cout, Cin,
                                   RS, _p(out), out_gstride, stream()), "reparam_sample")
 
 
 def reparam_bwd(dw, splits, mu, rho, dmu, drho, G, seed, sample0, layer, Cout, Cin, RS,
-                eps=None, dw_gstride=0, dw_sstride=0, fixed_sample=-1):
+                eps=None, dw_gstride=0, dw_sstride=0, fixed_sample=-1, dw_cin=None):
     """fixed_sample >= 0: bayesian-torch semantics (rho-gradient uses that sample's eps for
-    every MC group); -1: exact per-sample reparameterisation gradient."""
-    _f32(mu, rho, dmu, drho, eps)
+    every MC group); -1: exact per-sample reparameterisation gradient.  dw_cin: channel count
+    of the dw slabs' KRSC layout (the padded stems of the 16-bit path)."""
+    _f32(mu, rho, dmu, drho, eps)   # dw may be a strided view (q|k|v slabs)
     check(lib.mauv_reparam_bwd(_p(dw), splits, dw_gstride, dw_sstride, _p(mu), _p(rho), _p(eps),
-                               seed, sample0, layer, G, Cout, Cin, RS, _p(dmu), _p(drho),
+                               seed, sample0, layer, G, Cout, Cin, RS, dw_cin or Cin, _p(dmu),
+                               _p(drho),
                                fixed_sample, stream()), "reparam_bwd")
 
 
@@ -216,6 +225,12 @@ def bn_fwd_train(y, G, M, C, gamma, beta, run_mean, run_var, momentum, eps, ws, 
 
 
 def bn_apply(y, scale, shift, res, relu, out, G, M, C):
+    if y.dtype in H16:
+        _h16(y.dtype, y, res, out)
+        check(lib.mauv_bn_apply_h16(H16[y.dtype], _p(y), _p(scale), _p(shift), _p(res), int(relu),
+                                    _p(out), G, M, C, stream()), "bn_apply_h16")
+        return
+    _f32(y, res, out)
     check(lib.mauv_bn_apply(_p(y), _p(scale), _p(shift), _p(res), int(relu), _p(out), G, M, C,
                             stream()), "bn_apply")
 
@@ -237,6 +252,14 @@ def bn_bwd(y, out, dout, relu, mean, invstd, scale, G, M, C, ws, dy, dres=None, 
            dbeta=None, shift=None, pre=None):
     """out None + relu: mask from y*scale+shift.  pre = (p1, p2, nblk) partials from a dgrad
     epilogue (skips the partial pass)."""
+    if y.dtype in H16:
+        assert pre is None
+        _h16(y.dtype, y, out, dout, dy, dres)
+        _f32(mean, invstd, scale, shift, ws, dgamma, dbeta)
+        check(lib.mauv_bn_bwd_h16(H16[y.dtype], _p(y), _p(out), _p(dout), int(relu), _p(mean),
+                                  _p(invstd), _p(scale), _p(shift), G, M, C, _p(ws), _p(dy),
+                                  _p(dres), _p(dgamma), _p(dbeta), stream()), "bn_bwd_h16")
+        return
     _f32(y, out, dout, mean, invstd, scale, shift, ws, dy, dres, dgamma, dbeta)
     p1, p2, nb = pre if pre is not None else (None, None, 0)
     check(lib.mauv_bn_bwd(_p(y), _p(out), _p(dout), int(relu), _p(mean), _p(invstd), _p(scale),
@@ -246,19 +269,49 @@ def bn_bwd(y, out, dout, relu, mean, invstd, scale, G, M, C, ws, dy, dres=None, 
 
 # ----------------------------------------------------------------------- pooling
 def maxpool_fwd(x, N, H, W, C, y, idx):
+    if x.dtype in H16:
+        _h16(x.dtype, x, y)
+        check(lib.mauv_maxpool_fwd_h16(H16[x.dtype], _p(x), N, H, W, C, _p(y), _p(idx), stream()),
+              "maxpool_fwd_h16")
+        return
+    _f32(x, y)
     check(lib.mauv_maxpool_fwd(_p(x), N, H, W, C, _p(y), _p(idx), stream()), "maxpool_fwd")
 
 
 def maxpool_bwd(dy, idx, N, H, W, C, dx):
+    if dy.dtype in H16:
+        _h16(dy.dtype, dy, dx)
+        check(lib.mauv_maxpool_bwd_h16(H16[dy.dtype], _p(dy), _p(idx), N, H, W, C, _p(dx),
+                                       stream()), "maxpool_bwd_h16")
+        return
+    _f32(dy, dx)
     check(lib.mauv_maxpool_bwd(_p(dy), _p(idx), N, H, W, C, _p(dx), stream()), "maxpool_bwd")
 
 
 def avgpool_fwd(x, N, HW, C, y):
+    """y fp32 [N][C] (pooled features feed the fp32 head) from fp32 or 16-bit x."""
+    _f32(y)
+    if x.dtype in H16:
+        check(lib.mauv_avgpool_fwd_h16(H16[x.dtype], _p(x), N, HW, C, _p(y), stream()),
+              "avgpool_fwd_h16")
+        return
     check(lib.mauv_avgpool_fwd(_p(x), N, HW, C, _p(y), stream()), "avgpool_fwd")
 
 
 def avgpool_bwd(dy, N, HW, C, dx):
+    _f32(dy)
+    if dx.dtype in H16:
+        check(lib.mauv_avgpool_bwd_h16(H16[dx.dtype], _p(dy), N, HW, C, _p(dx), stream()),
+              "avgpool_bwd_h16")
+        return
     check(lib.mauv_avgpool_bwd(_p(dy), N, HW, C, _p(dx), stream()), "avgpool_bwd")
+
+
+def pack_nchw(x, B, C, H, W, Cp, y):
+    """fp32 NCHW images -> 16-bit NHWC with Cp (zero-padded) channels (16-bit stems)."""
+    _f32(x)
+    check(lib.mauv_pack_nchw_h16(H16[y.dtype], _p(x), B, C, H, W, Cp, _p(y), stream()),
+          "pack_nchw_h16")
 
 
 # ----------------------------------------------------------------------- head

@@ -148,3 +148,103 @@ def test_conv16_lazy_bn_input_and_stats(dt):
             dy[g].permute(0, 3, 1, 2).double())
         dw.append(wg.grad.permute(0, 2, 3, 1))
     close(ws.sum(0).view(G, Cout, 3, 3, Cin), torch.stack(dw), 1e-3)
+
+
+@pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
+@pytest.mark.parametrize("C,relu,res,lazy", [(64, True, False, True), (256, True, True, False),
+                                             (2048, False, False, False)])
+def test_bn16_apply_bwd_matches_fp32_kernels(dt, C, relu, res, lazy):
+    """16-bit BN apply / backward == the fp32 kernels on the same 16-bit-rounded tensors, up
+    to the final rounding of the 16-bit outputs."""
+    from mauv import ops
+    G, M = 3, 4 * 5 * 5
+    torch.manual_seed(5)
+    y = (torch.randn(G, M, C) * 3 + 2).to(dt).to(dev)
+    r = torch.randn(G, M, C).to(dt).to(dev) if res else None
+    dout = torch.randn(G, M, C).to(dt).to(dev)
+    mean = y.float().mean(1)
+    invstd = (y.float().var(1, unbiased=False) + 1e-5).rsqrt()
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev)
+    scale = (gamma * invstd).contiguous()
+    shift = (beta - mean * scale).contiguous()
+    out16 = torch.empty(G, M, C, device=dev, dtype=dt)
+    ops.bn_apply(y, scale, shift, r, relu, out16, G, M, C)
+    out32 = torch.empty(G, M, C, device=dev)
+    ops.bn_apply(y.float(), scale, shift, None if r is None else r.float(), relu, out32, G, M, C)
+    close(out16, out32, 2 * ULP[dt])
+    ws = torch.empty(ops.bn_workspace_floats(G, M, C), device=dev)
+    res16 = [torch.empty(G, M, C, device=dev, dtype=dt), torch.empty(G, M, C, device=dev, dtype=dt)
+             if res else None, torch.zeros(C, device=dev), torch.zeros(C, device=dev)]
+    res32 = [torch.empty(G, M, C, device=dev), torch.empty(G, M, C, device=dev) if res else None,
+             torch.zeros(C, device=dev), torch.zeros(C, device=dev)]
+    o16 = None if lazy else out16
+    o32 = None if lazy else out16.float()   # the same (rounded) mask source
+    ops.bn_bwd(y, o16, dout, relu, mean, invstd, scale, G, M, C, ws, *res16, shift=shift)
+    ws2 = torch.empty_like(ws)
+    ops.bn_bwd(y.float(), o32, dout.float(), relu, mean, invstd, scale, G, M, C, ws2, *res32,
+               shift=shift)
+    close(res16[0], res32[0], 4 * ULP[dt])
+    if res:
+        close(res16[1], res32[1], 2 * ULP[dt])
+    close(res16[2], res32[2], 1e-5)
+    close(res16[3], res32[3], 1e-5)
+
+
+@pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
+def test_pools16_and_stem_pack(dt):
+    from mauv import ops
+    N, H, C = 3, 9, 64
+    torch.manual_seed(6)
+    x = torch.randn(N, H, H, C).to(dt)
+    x[0, :3, :3, :] = 0.0
+    Ho = ops.out_hw(H, 3, 2, 1)
+    y = torch.empty(N, Ho, Ho, C, device=dev, dtype=dt)
+    idx = torch.empty(N, Ho, Ho, C, dtype=torch.uint8, device=dev)
+    ops.maxpool_fwd(x.to(dev), N, H, H, C, y, idx)
+    xr = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    close(y, yr.permute(0, 2, 3, 1), 0.0)          # max is exact
+    dy = torch.randn(N, Ho, Ho, C).to(dt)
+    yr.backward(dy.double().permute(0, 3, 1, 2))
+    dx = torch.empty(N, H, H, C, device=dev, dtype=dt)
+    ops.maxpool_bwd(dy.to(dev), idx, N, H, H, C, dx)
+    close(dx, xr.grad.permute(0, 2, 3, 1), 2 * ULP[dt])
+    a = torch.empty(N, C, device=dev)
+    ops.avgpool_fwd(x.to(dev), N, H * H, C, a)
+    close(a, x.double().mean((1, 2)), 1e-5)
+    da = torch.randn(N, C)
+    dxa = torch.empty(N, H, H, C, device=dev, dtype=dt)
+    ops.avgpool_bwd(da.to(dev), N, H * H, C, dxa)
+    close(dxa, (da.double() / (H * H))[:, None, None, :].expand(N, H, H, C), 2 * ULP[dt])
+    img = torch.randn(2, 3, 7, 5)
+    packed = torch.empty(2, 7, 5, 8, device=dev, dtype=dt)
+    ops.pack_nchw(img.to(dev), 2, 3, 7, 5, 8, packed)
+    ref = torch.zeros(2, 7, 5, 8)
+    ref[..., :3] = img.permute(0, 2, 3, 1)
+    assert torch.equal(packed.cpu(), ref.to(dt))
+
+
+@pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
+def test_reparam16_padded_sample_and_bwd(dt):
+    """16-bit sampled weights (cin padded 3 -> 8) == round(fp32 sample); reparam_bwd over
+    padded slabs == over dense slabs."""
+    from mauv import ops
+    G, Cout, Cin, RS, cp = 3, 16, 3, 49, 8
+    torch.manual_seed(7)
+    mu = torch.randn(Cout, Cin, RS, device=dev) * 0.1
+    rho = torch.randn(Cout, Cin, RS, device=dev) - 3
+    w32 = torch.empty(G, Cout, RS, Cin, device=dev)
+    ops.reparam_sample(mu, rho, w32, G, 42, 5, 9, Cout, Cin, RS)
+    w16 = torch.zeros(G, Cout, RS, cp, device=dev, dtype=dt)
+    ops.reparam_sample(mu, rho, w16, G, 42, 5, 9, Cout, Cin, RS, cin_pad=cp)
+    assert torch.equal(w16[..., :Cin], w32.to(dt)) and not w16[..., Cin:].any()
+    dwp = torch.zeros(2, G, Cout, RS, cp, device=dev)
+    dwp[..., :Cin] = torch.randn(2, G, Cout, RS, Cin, device=dev)
+    dwp[..., Cin:] = 1e9    # padded channels must be ignored
+    dmu_a, drho_a = torch.zeros_like(mu), torch.zeros_like(rho)
+    ops.reparam_bwd(dwp, 2, mu, rho, dmu_a, drho_a, G, 42, 5, 9, Cout, Cin, RS, dw_cin=cp)
+    dmu_b, drho_b = torch.zeros_like(mu), torch.zeros_like(rho)
+    ops.reparam_bwd(dwp[..., :Cin].contiguous(), 2, mu, rho, dmu_b, drho_b, G, 42, 5, 9, Cout,
+                    Cin, RS)
+    assert torch.equal(dmu_a, dmu_b) and torch.equal(drho_a, drho_b)

@@ -1,0 +1,154 @@
+"""16-bit trunks (bf16 training = BASELINE configs[2]; f16 under torch.autocast = the reference
+predictor's own precision, inference/predictors.py:55) vs the fp32 oracle on identical weights
+and epsilons.
+
+Tolerances: logits |d| <= 5e-2 * max(1, |ref|); predictive entropy /
+aleatoric |d| <= 1e-2.  Gradients: 16-bit activations through 53 BN layers per trunk cannot be
+held to the fp32 bar; the check is that the training signal is preserved — cosine similarity
+of every parameter tensor's gradient with the float64 truth (median >= 0.98, 10th percentile
+>= 0.9) and the loss within 5e-2 relative.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import bayes_ref, loops_ref
+from tests.golden.common import make_batches, SEED_DATA
+from tests.helpers import build_pair, EpsBridge, oracle64
+
+pytestmark = pytest.mark.gpu
+DTS = [torch.bfloat16, torch.float16]
+
+
+def _cuda(*ts):
+    return [t.cuda() for t in ts]
+
+
+def _close16(a, ref, tol=5e-2):
+    d = (a.detach().double().cpu() - ref.detach().double().cpu()).abs().max().item()
+    assert d <= tol * max(1.0, ref.detach().abs().max().item()), d
+    return d
+
+
+def _kinds(fn):
+    from mauv import ops
+    ops.PROFILE = []
+    try:
+        fn()
+    finally:
+        rows, ops.PROFILE = ops.PROFILE, None
+    from collections import Counter
+    return Counter(r[0] for r in rows)
+
+
+@pytest.mark.parametrize("dt", DTS, ids=["bf16", "f16"])
+def test_forward16_logits(dt):
+    from mauv.engine import root_state, set_precision
+    o, m = build_pair()
+    set_precision(m, dt)
+    batch = make_batches(SEED_DATA, 1, B=2, S_opt=64, S_son=64)[0]
+    x, b, s = batch["main_image"], batch["bathy_image"], batch["sss_image"]
+    bridge = EpsBridge(o, m, 21)
+    with bridge, torch.no_grad():
+        o_logits = torch.stack([o(x, b, s) for _ in range(3)])
+    bridge.collect()
+    root_state(m).eps_provider = bridge.provider
+    with torch.no_grad():
+        kinds = _kinds(lambda: m.mc_forward(*_cuda(x, b, s), 3))
+    # the 3 x 53 trunk convs ran 16-bit; only the fusion head's 9 GEMMs stay fp32
+    assert kinds["fwd_" + str(dt)[6:]] == 159 and kinds["fwd"] == 9, kinds
+    root_state(m).offset = 0
+    with torch.no_grad():
+        logits = m.mc_forward(*_cuda(x, b, s), 3)
+    _close16(logits, o_logits)
+
+
+@pytest.mark.parametrize("dt", DTS, ids=["bf16", "f16"])
+def test_train_step16(dt):
+    from mauv.engine import root_state, set_precision
+    from mauv.kl import get_kl_loss
+    from mauv import mchead
+    o, m = build_pair()
+    set_precision(m, dt)
+    B, N = 2, 3
+    batch = make_batches(SEED_DATA, 1, B=B, S_opt=64, S_son=64)[0]
+    x, b, s, y = batch["main_image"], batch["bathy_image"], batch["sss_image"], batch["label"]
+
+    def oracle_loss(model, dtp=torch.float32):
+        lg = torch.stack([model(x.to(dtp), b.to(dtp), s.to(dtp)) for _ in range(N)])
+        loss = F.cross_entropy(lg.mean(0), y) + bayes_ref.get_kl_loss(model) / B * 0.5
+        loss.backward()
+        return lg, loss
+
+    bridge = EpsBridge(o, m, 99)
+    with bridge:
+        o_logits, loss_o = oracle_loss(o)
+    bridge.collect()
+    o64, _ = oracle64(o, bridge.store, lambda mm: oracle_loss(mm, torch.float64))
+    root_state(m).eps_provider = bridge.provider
+    logits = m.mc_forward(*_cuda(x, b, s), N)
+    _close16(logits, o_logits)
+    ce, _, _ = mchead.mc_mean_ce(logits, y.cuda())
+    loss = ce + get_kl_loss(m) / B * 0.5
+    assert abs(loss.item() - loss_o.item()) <= 5e-2 * abs(loss_o.item())
+    loss.backward()
+    cos = []
+    for ph, pt in zip(m.parameters(), o64.parameters()):
+        if pt.grad is None:
+            continue
+        a, t = ph.grad.double().cpu().flatten(), pt.grad.flatten()
+        if t.norm() == 0:
+            continue
+        cos.append(float(a @ t / (a.norm() * t.norm() + 1e-300)))
+        assert torch.isfinite(ph.grad).all()
+    cos = np.array(cos)
+    print(f"grad cosine vs fp64: median {np.median(cos):.4f} p10 {np.quantile(cos, 0.1):.4f} "
+          f"min {cos.min():.4f}")
+    assert np.median(cos) >= 0.98 and np.quantile(cos, 0.1) >= 0.9, cos
+
+
+def test_predict_under_autocast_runs_f16():
+    """multimodal_predict's maths under torch.autocast("cuda") (as predictors.py:55 does): the
+    trunks switch to f16 by themselves; uncertainties within the bf16-row tolerances."""
+    from mauv.engine import root_state
+    from mauv.predict import mc_statistics
+    o, m = build_pair()
+    batch = make_batches(SEED_DATA, 1, B=4, S_opt=64, S_son=64)[0]
+    x, b, s = batch["main_image"], batch["bathy_image"], batch["sss_image"]
+    N = 6
+    bridge = EpsBridge(o, m, 5)
+    with bridge:
+        pred_o, var_o, alea_o, P = loops_ref.predict_batch(o, x, b, s, N)
+    bridge.collect()
+    root_state(m).eps_provider = bridge.provider
+    with torch.no_grad(), torch.autocast("cuda"):
+        kinds = _kinds(lambda: mc_statistics(m, *_cuda(x, b, s), N, chunk=N))
+    assert kinds["fwd_float16"] == 159, kinds
+    root_state(m).offset = 0
+    with torch.no_grad(), torch.autocast("cuda"):
+        st = mc_statistics(m, *_cuda(x, b, s), N, chunk=N)
+    np.testing.assert_allclose(st["aleatoric"].cpu().numpy(), alea_o.numpy(), atol=1e-2)
+    np.testing.assert_allclose(st["var"].cpu().numpy(), var_o.numpy(), atol=1e-2)
+    agree = (st["pred"].cpu() == pred_o).float().mean().item()
+    print(f"argmax agreement {agree:.3f}")
+    assert agree >= 0.75
+
+
+@pytest.mark.parametrize("dt", DTS, ids=["bf16", "f16"])
+def test_full_resolution_forward16(dt):
+    """BASELINE shapes (224 optical, 256 sonar), B=2, N=2."""
+    from mauv.engine import root_state, set_precision
+    o, m = build_pair()
+    set_precision(m, dt)
+    batch = make_batches(SEED_DATA, 1, B=2, S_opt=224, S_son=256)[0]
+    x, b, s = batch["main_image"], batch["bathy_image"], batch["sss_image"]
+    bridge = EpsBridge(o, m, 3)
+    with bridge, torch.no_grad():
+        o_logits = torch.stack([o(x, b, s) for _ in range(2)])
+    bridge.collect()
+    root_state(m).eps_provider = bridge.provider
+    with torch.no_grad():
+        logits = m.mc_forward(*_cuda(x, b, s), 2)
+    d = _close16(logits, o_logits)
+    print(f"{dt}: max |dlogit| {d:.3e}")
