@@ -348,46 +348,21 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(const ConvArgs16 a) {
   }
 
   // ---------------- epilogue ----------------
-  const bool fst = (MODE == H_FWD) && a.st_mean;
-  float s1[NI];
+  // FWD statistics (from the fp32 accumulators, before any rounding)
+  if ((MODE == H_FWD) && a.st_mean) {
+    const int nvalid = min(BM, a.M - m0);
+    float s1[NI], s2[NI], mean[NI];
 #pragma unroll
-  for (int ni = 0; ni < NI; ++ni) s1[ni] = 0.f;
-  const int nvalid = min(BM, a.M - m0);
+    for (int ni = 0; ni < NI; ++ni) { s1[ni] = 0.f; s2[ni] = 0.f; }
 #pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int col = n0 + wn * WN + ni * 32 + li;
-      if (col >= a.N) continue;
+      for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row >= a.M) continue;
-        float v = acc[mi][ni][r];
-        if constexpr (MODE == H_WGRAD) {
-          float* outg = (float*)a.out + ((long long)sp * a.G + g) * ((long long)a.M * a.N);
-          outg[(long long)row * a.N + col] = v;
-        } else {
-          long long orow = row;
-          if constexpr (MODE == H_DGRAD) {
-            if (a.stride != 1) {
-              const int HW = a.Hc * a.Wc, b = row / HW, rem = row - b * HW;
-              const int i = rem / a.Wc, jj = rem - i * a.Wc;
-              orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
-            }
-          }
-          const long long o = (long long)g * a.out_sg + orow * a.N + col;
-          u16* outp = (u16*)a.out;
-          if constexpr (MODE == H_DGRAD) {
-            if (a.addend) v += H16<DT>::to_f(a.addend[o]);
-            if (a.accumulate) v += H16<DT>::to_f(outp[o]);
-          }
-          if constexpr (MODE == H_FWD) s1[ni] += v;
-          outp[o] = H16<DT>::from_f(v);
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row < a.M) s1[ni] += acc[mi][ni][r];
         }
-      }
-    }
-  if (fst) {
     float* red = (float*)smem;  // LDS is free: the main loop ended with a barrier
     const int tcol = wn * WN + li;
 #pragma unroll
@@ -397,12 +372,9 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(const ConvArgs16 a) {
       for (int ni = 0; ni < NI; ++ni) red[wm * BN + tcol + ni * 32] = s1[ni];
     }
     __syncthreads();
-    float mean[NI], s2[NI];
 #pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
+    for (int ni = 0; ni < NI; ++ni)
       mean[ni] = (red[tcol + ni * 32] + red[BN + tcol + ni * 32]) / (float)nvalid;
-      s2[ni] = 0.f;
-    }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -429,6 +401,71 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(const ConvArgs16 a) {
       a.st_mean[so] = t1 / (float)nvalid;
       a.st_m2[so] = t2;
       if (n0 + tid == 0) a.st_cnt[(long long)g * a.st_nblk + mt] = (float)nvalid;
+    }
+    __syncthreads();  // red is overwritten by the staged store below
+  }
+
+  if constexpr (MODE == H_WGRAD) {  // fp32 split-K slabs: 32 lanes x 4 B contiguous per store
+    float* outg = (float*)a.out + ((long long)sp * a.G + g) * ((long long)a.M * a.N);
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int col = n0 + wn * WN + ni * 32 + li;
+        if (col >= a.N) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row < a.M) outg[(long long)row * a.N + col] = acc[mi][ni][r];
+        }
+      }
+  } else {
+    // 16-bit output through LDS: each wave row (wm = 0, 1) in turn parks its fp32 accumulators
+    // as a [WM][BN+4] tile, then all 256 threads write it out as 16-byte rows of 8 channels
+    // (adding the residual addend / previous dx in fp32, one rounding).
+    constexpr int SLD = BN + 4;
+    static_assert(WM * SLD * 4 <= 2 * STG * 2, "staging tile exceeds LDS");
+    float* stile = (float*)smem;
+    constexpr int CPR = BN / 8, NCH = WM * CPR;
+    u16* outp = (u16*)a.out;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if (wm == pass) {
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              stile[(mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SLD + wn * WN + ni * 32 + li] =
+                  acc[mi][ni][r];
+      }
+      __syncthreads();
+      for (int c = tid; c < NCH; c += 256) {
+        const int rl = c / CPR, cc = c - rl * CPR;
+        const int row = m0 + pass * WM + rl, col = n0 + 8 * cc;
+        if (row >= a.M || col >= a.N) continue;
+        floatx4 v0 = *(const floatx4*)(stile + rl * SLD + 8 * cc);
+        floatx4 v1 = *(const floatx4*)(stile + rl * SLD + 8 * cc + 4);
+        floatx8 f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { f[e] = v0[e]; f[4 + e] = v1[e]; }
+        long long orow = row;
+        if constexpr (MODE == H_DGRAD) {
+          if (a.stride != 1) {
+            const int HW = a.Hc * a.Wc, b = row / HW, rem = row - b * HW;
+            const int i = rem / a.Wc, jj = rem - i * a.Wc;
+            orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
+          }
+        }
+        const long long o = (long long)g * a.out_sg + orow * a.N + col;
+        if constexpr (MODE == H_DGRAD) {
+          if (a.addend) f += unpack8<DT>(*(const u32x4*)(a.addend + o));
+          if (a.accumulate) f += unpack8<DT>(*(const u32x4*)(outp + o));
+        }
+        *(u32x4*)(outp + o) = pack8<DT>(f);
+      }
+      __syncthreads();
     }
   }
 }

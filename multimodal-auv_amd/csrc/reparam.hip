@@ -59,66 +59,59 @@ __global__ __launch_bounds__(256) void reparam_sample_kernel(
   }
 }
 
+// One block per output channel o: its P = Cin*RS parameters are the same index set in the
+// KRSC slab layout and in the OIHW parameter layout, so the block
+//   (A) streams the slab rows coalesced in KRSC order, summing split-K partials (and, in
+//       reference mode, the G samples) into an LDS image stored in OIHW order, then
+//   (B) walks OIHW quads (the Philox counter unit) and applies the chain rule:
+//       dmu += sum,  drho += sum_g d_g * eps_g' * sigmoid(rho).
+// Reference mode (fixed >= 0): one epsilon for every g, so drho += (sum_g d_g) * eps * sig —
+// one LDS pass.  Exact mode: one pass per g.
 __global__ __launch_bounds__(256) void reparam_bwd_kernel(
     const float* __restrict__ dw, int splits, long long dw_gs, long long dw_ss,
-    const float* __restrict__ mu,
-    const float* __restrict__ rho, const float* __restrict__ eps, uint64_t seed,
-    uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS, int cin_pad,
+    const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
+    uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS, int cin_pad,
     float* __restrict__ dmu, float* __restrict__ drho, long long fixed) {
-  const long long numel = (long long)Cout * Cin * RS;
-  const long long nq = (numel + 3) / 4;
-  for (long long q = blockIdx.x * 256LL + threadIdx.x; q < nq; q += (long long)gridDim.x * 256) {
-    long long src[4];
-    float sg[4], gm[4] = {0.f, 0.f, 0.f, 0.f}, gr[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const long long i = 4 * q + e;
-      if (i < numel) {
-        sg[e] = sigmoidf_(rho[i]);
-        const long long o = i / ((long long)Cin * RS);
-        const long long rem = i - o * Cin * RS;
-        const int c = (int)(rem / RS), rs = (int)(rem - (long long)c * RS);
-        src[e] = (o * RS + rs) * cin_pad + c;
-      } else {
-        sg[e] = 0.f; src[e] = -1;
-      }
+  extern __shared__ float sd[];  // [P] in OIHW-local order (c*RS + rs)
+  const int o = blockIdx.x, tid = threadIdx.x;
+  const int P = Cin * RS;
+  const long long numel = (long long)Cout * P;
+  const long long i0 = (long long)o * P;
+  const long long q0 = i0 >> 2, q1 = (i0 + P - 1) >> 2;  // quads touching this channel
+  const int npass = fixed >= 0 ? 1 : G;
+  for (int pass = 0; pass < npass; ++pass) {
+    const int g0 = fixed >= 0 ? 0 : pass, g1 = fixed >= 0 ? G : pass + 1;
+    for (int k = tid; k < P; k += 256) {  // k = rs*Cin + c (KRSC-local, coalesced in c)
+      const int rs = k / Cin, c = k - rs * Cin;
+      const long long src = ((long long)o * RS + rs) * cin_pad + c;
+      float d = 0.f;
+      for (int g = g0; g < g1; ++g)
+        for (int s = 0; s < splits; ++s) d += dw[s * dw_ss + g * dw_gs + src];
+      sd[c * RS + rs] = d;
     }
-    floatx4 efix = {0.f, 0.f, 0.f, 0.f};
-    if (fixed >= 0) {  // reference mode: one epsilon (the last drawn sample) for every g
+    __syncthreads();
+    const long long esample = fixed >= 0 ? fixed : pass;
+    for (long long q = q0 + tid; q <= q1; q += 256) {
+      floatx4 ep;
       if (eps) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) efix[e] = src[e] >= 0 ? eps[fixed * numel + 4 * q + e] : 0.f;
-      } else {
-        efix = normal4(seed, sample0 + fixed, layer, (uint32_t)q);
-      }
-    }
-    for (int g = 0; g < G; ++g) {
-      floatx4 ep = efix;
-      if (fixed < 0) {
-        if (eps) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) ep[e] = src[e] >= 0 ? eps[(long long)g * numel + 4 * q + e] : 0.f;
-        } else {
-          ep = normal4(seed, sample0 + g, layer, (uint32_t)q);
+        for (int e = 0; e < 4; ++e) {
+          const long long i = 4 * q + e;
+          ep[e] = (i < numel) ? eps[esample * numel + i] : 0.f;
         }
+      } else {
+        ep = normal4(seed, sample0 + esample, layer, (uint32_t)q);
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        if (src[e] < 0) continue;
-        float d = 0.f;
-        for (int s = 0; s < splits; ++s) d += dw[s * dw_ss + g * dw_gs + src[e]];
-        gm[e] += d;
-        gr[e] += d * ep[e];
+        const long long i = 4 * q + e;
+        if (i < i0 || i >= i0 + P) continue;
+        const float d = sd[(int)(i - i0)];
+        dmu[i] += d;
+        drho[i] += d * ep[e] * sigmoidf_(rho[i]);
       }
     }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const long long i = 4 * q + e;
-      if (i < numel) {
-        dmu[i] += gm[e];
-        drho[i] += gr[e] * sg[e];
-      }
-    }
+    __syncthreads();
   }
 }
 
@@ -243,7 +236,9 @@ MAUV_API int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride,
   const long long nq = (numel + 3) / 4;
   const long long gs = dw_gstride ? dw_gstride : (long long)Cout * RS * dw_cin;
   const long long ss = dw_sstride ? dw_sstride : gs * G;
-  hipLaunchKernelGGL(reparam_bwd_kernel, dim3(grid_for(nq)), dim3(256), 0, stream, dw, splits,
+  if ((long long)Cin * RS > 16384) { set_error("reparam_bwd: Cin*R*S > 16384"); return kErrArg; }
+  (void)nq;
+  hipLaunchKernelGGL(reparam_bwd_kernel, dim3(Cout), dim3(256), (size_t)Cin * RS * 4, stream, dw, splits,
                      gs, ss, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS, dw_cin, dmu, drho,
                      fixed_sample >= 0 ? (long long)(fixed_sample - (long long)sample0) : -1LL);
   return check_launch("reparam_bwd");

@@ -60,6 +60,9 @@ def main():
     ap.add_argument("--shape", default="", help="one shape Cin,Cout,R,stride,pad,H (profiling)")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "f16"])
+    ap.add_argument("--fused", action="store_true",
+                    help="as in the model: BN+ReLU applied on load (fwd, wgrad) and BN "
+                         "statistics partials from the fwd epilogue")
     a = ap.parse_args()
     global REPS
     REPS = a.reps
@@ -88,8 +91,15 @@ def main():
             x = torch.randn(G, B, H, H, Cin, device=dev).to(dt)
             w = (torch.randn(G, Cout, R, R, Cin, device=dev) * 0.05).to(dt)
             y = torch.empty(G, B, Ho, Ho, Cout, device=dev, dtype=dt)
+            xbn, stats = None, None
+            if a.fused and name != "stem":
+                xbn = (torch.rand(G, Cin, device=dev) + 0.5, torch.randn(G, Cin, device=dev), 1)
+                nblk = ops.fwd_stat_blocks(G, B, H, H, Cin, Cout, R, st, pd)
+                stats = (torch.empty(G, nblk, Cout, device=dev), torch.empty(G, nblk, Cout, device=dev),
+                         torch.empty(G, nblk, device=dev))
             if "fwd" in kinds:
-                res.append(("fwd", timeit(lambda: ops.conv2d_fwd(x, w, y, G, B, H, H, Cin, Cout, R, st, pd))))
+                res.append(("fwd", timeit(lambda: ops.conv2d_fwd(x, w, y, G, B, H, H, Cin, Cout, R, st, pd,
+                                                                 x_bn=xbn, stats=stats))))
             if "dgrad" in kinds and name != "stem" and (dt == torch.float32 or Cout % 32 == 0):
                 dx = torch.empty_like(x)
                 res.append(("dgrad", timeit(lambda: ops.conv2d_bwd_data(y, w, dx, G, B, H, H, Cin, Cout, R, st, pd))))
@@ -97,7 +107,8 @@ def main():
             if "wgrad" in kinds:
                 sp = ops.wgrad_splits(G, B, H, H, Cin, Cout, R, st, pd)
                 ws = torch.empty(sp, G, Cout, R * R * Cin, device=dev)
-                res.append(("wgrad", timeit(lambda: ops.conv2d_bwd_weight(x, y, ws, sp, G, B, H, H, Cin, Cout, R, st, pd))))
+                res.append(("wgrad", timeit(lambda: ops.conv2d_bwd_weight(x, y, ws, sp, G, B, H, H, Cin, Cout, R, st, pd,
+                                                                          x_bn=xbn))))
                 del ws
             del x, w, y
             torch.cuda.empty_cache()
