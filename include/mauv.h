@@ -165,8 +165,12 @@ int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, const flo
                            float* run_mean, float* run_var, float momentum, float eps,
                            float* workspace, float* mean, float* invstd, float* scale,
                            float* shift, hipStream_t stream);
+/* out = [relu](y*scale + shift (+ res')); res' = res*res_scale + res_shift when res_scale is
+ * non-NULL — the bottleneck's downsample BatchNorm applied inside the residual add (its output
+ * is never materialised). */
 int mauv_bn_apply(const float* y, const float* scale, const float* shift, const float* res,
-                  int relu, float* out, int G, long long M, int C, hipStream_t stream);
+                  const float* res_scale, const float* res_shift, int relu, float* out, int G,
+                  long long M, int C, hipStream_t stream);
 int mauv_bn_eval_params(int G, int C, const float* gamma, const float* beta,
                         const float* run_mean, const float* run_var, float eps, float* scale,
                         float* shift, hipStream_t stream);
@@ -181,8 +185,8 @@ int mauv_bn_bwd(const float* y, const float* out, const float* dout, int relu,
 /* 16-bit activations (dtype 0 = bf16, 1 = f16): y/res/out/dout/dy/dres are 16-bit words;
  * statistics, scale/shift, workspace and dgamma/dbeta fp32 (same maths as above). */
 int mauv_bn_apply_h16(int dtype, const void* y, const float* scale, const float* shift,
-                      const void* res, int relu, void* out, int G, long long M, int C,
-                      hipStream_t stream);
+                      const void* res, const float* res_scale, const float* res_shift, int relu,
+                      void* out, int G, long long M, int C, hipStream_t stream);
 int mauv_bn_bwd_h16(int dtype, const void* y, const void* out, const void* dout, int relu,
                     const float* mean, const float* invstd, const float* scale,
                     const float* shift, int G, long long M, int C, float* workspace, void* dy,

@@ -174,12 +174,16 @@ __global__ void bn_running_kernel(int G, int C, const float* __restrict__ mean,
   run_var[c] = rv;
 }
 
-// out = [relu]( y * scale[g][c] + shift[g][c] (+ res) )
+// out = [relu]( y * scale[g][c] + shift[g][c] (+ res') ),  res' = res, or — when the residual
+// is itself a pending BatchNorm (the bottleneck's downsample branch, never materialised) —
+// res' = res * res_scale[g][c] + res_shift[g][c]
 template <class S>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const typename S::T* __restrict__ y,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const typename S::T* __restrict__ res,
+                                                       const float* __restrict__ res_scale,
+                                                       const float* __restrict__ res_shift,
                                                        int relu, typename S::T* __restrict__ out,
                                                        long long M, int C) {
   const int c4n = C / 4;
@@ -194,7 +198,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const typename S::T* __re
     const floatx4 sc = *(const floatx4*)(scale + g * C + c);
     const floatx4 sh = *(const floatx4*)(shift + g * C + c);
     v = v * sc + sh;
-    if (rg) v += S::ld4(rg + 4 * i);
+    if (rg) {
+      floatx4 rv = S::ld4(rg + 4 * i);
+      if (res_scale)
+        rv = rv * *(const floatx4*)(res_scale + g * C + c) + *(const floatx4*)(res_shift + g * C + c);
+      v += rv;
+    }
     if (relu) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
@@ -427,7 +436,7 @@ MAUV_API int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const 
                        mean, uvar, run_mean, run_var, momentum);
   if (out) {
     hipLaunchKernelGGL(bn_apply_kernel<SF32>, dim3(ew_grid(M * C / 4 / 1), G), dim3(256), 0, stream,
-                       y, scale, shift, res, relu, out, M, C);
+                       y, scale, shift, res, nullptr, nullptr, relu, out, M, C);
   }
   return check_launch("bn_fwd_train");
 }
@@ -447,12 +456,13 @@ MAUV_API int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, 
   return check_launch("bn_stats_finalize");
 }
 
-// out = [relu](y * scale + shift (+ res)) with precomputed per-group scale/shift.
+// out = [relu](y * scale + shift (+ res')) with precomputed per-group scale/shift;
+// res' = res * res_scale + res_shift when res_scale is given (pending BN on the residual).
 MAUV_API int mauv_bn_apply(const float* y, const float* scale, const float* shift,
-                           const float* res, int relu, float* out, int G, long long M, int C,
-                           hipStream_t stream) {
+                           const float* res, const float* res_scale, const float* res_shift,
+                           int relu, float* out, int G, long long M, int C, hipStream_t stream) {
   hipLaunchKernelGGL(bn_apply_kernel<SF32>, dim3(ew_grid(M * C / 4), G), dim3(256), 0, stream, y,
-                     scale, shift, res, relu, out, M, C);
+                     scale, shift, res, res_scale, res_shift, relu, out, M, C);
   return check_launch("bn_apply");
 }
 
@@ -505,10 +515,12 @@ MAUV_API int mauv_bn_bwd(const float* y, const float* out, const float* dout, in
 // 16-bit activations (dtype 0 = bf16, 1 = f16): y/out/dout/dy/dres are 16-bit, statistics,
 // scale/shift, workspace and parameter gradients fp32.
 MAUV_API int mauv_bn_apply_h16(int dtype, const void* y, const float* scale, const float* shift,
-                               const void* res, int relu, void* out, int G, long long M, int C,
+                               const void* res, const float* res_scale, const float* res_shift,
+                               int relu, void* out, int G, long long M, int C,
                                hipStream_t stream) {
 #define L(D) hipLaunchKernelGGL(bn_apply_kernel<S16<D>>, dim3(ew_grid(M * C / 4), G), dim3(256), 0, \
-                                stream, (const u16*)y, scale, shift, (const u16*)res, relu, (u16*)out, M, C);
+                                stream, (const u16*)y, scale, shift, (const u16*)res, res_scale,    \
+                                res_shift, relu, (u16*)out, M, C);
   MAUV_DT_DISPATCH(dtype, "bn_apply_h16", L)
 #undef L
   return check_launch("bn_apply_h16");

@@ -167,6 +167,21 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
 
   floatx4 ra[NVA], rb[NVB];
   floatx4 bsc[NVB], bsh[NVB];  // WGRAD: per-thread channel transform (fixed columns)
+  // tile-uniform tap counters: FWD (r, s, c0), DGRAD (tr, ts, n0) — advanced by load_b
+  int t_r = 0, t_s = 0, t_c = 0;
+  // WGRAD B: (b, oh, ow) of each loader row's pixel, advanced by BKT per tile
+  int px_b[NVB], px_h[NVB], px_w[NVB];
+  if constexpr (MODE == WGRAD) {
+#pragma unroll
+    for (int j = 0; j < NVB; ++j) {
+      const int p = kbeg + (tid + 256 * j) / (BN / 4);
+      const int HW = a.Ho * a.Wo;
+      px_b[j] = p / HW;
+      const int rem = p - px_b[j] * HW;
+      px_h[j] = rem / a.Wo;
+      px_w[j] = rem - px_h[j] * a.Wo;
+    }
+  }
   if constexpr (MODE == WGRAD && VB) {
 #pragma unroll
     for (int j = 0; j < NVB; ++j) {
@@ -184,10 +199,8 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if constexpr (MODE == FWD) {
         const int kq = idx % KQ;
-        if constexpr (VA) {
-          const int SC = a.S * a.Cin;
-          const int r = k0 / SC, rem = k0 - r * SC, s = rem / a.Cin;
-          const int c = rem - s * a.Cin + 4 * kq;
+        if constexpr (VA) {  // Cin % 32 == 0: the tile's k slice is one (r, s) tap
+          const int r = t_r, s = t_s, c = t_c + 4 * kq;
           const int ih = a_p0[j] + r, iw = a_p1[j] + s;
           if (a_ok[j] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
             v = *(const floatx4*)(xg + a_off[j] + (long long)ih * a.xs_h + (long long)iw * a.xs_w + c);
@@ -212,9 +225,8 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
         const int kq = idx % KQ;
         // k = (tap t = (tr, ts), n); tap (tr, ts) -> (r0 + stride*tr, s0 + stride*ts), so
         // ih + pad - r is a multiple of the stride by construction
-        if constexpr (VA) {
-          const int t = k0 / a.Cout, n = k0 - t * a.Cout + 4 * kq;
-          const int tr = t / a.ns, ts = t - tr * a.ns;
+        if constexpr (VA) {  // Cout % 32 == 0: the tile's k slice is one tap (tr, ts)
+          const int n = t_c + 4 * kq, tr = t_r, ts = t_s;
           const int ohn = a_p0[j] - a.r0 - a.stride * tr, own = a_p1[j] - a.s0 - a.stride * ts;
           if (a_ok[j] && ohn >= 0 && own >= 0) {
             const int oh = a.stride == 1 ? ohn : ohn / a.stride;
@@ -275,7 +287,13 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
         const int k = k0 + b_r[j];
         const int c = b_c[j];
         if (k < kend) {
-          const int t = k / a.Cout, n = k - t * a.Cout, tr = t / a.ns, ts = t - tr * a.ns;
+          int n, tr, ts;
+          if constexpr (VA) {  // tile-uniform tap (Cout % 32 == 0)
+            n = t_c + b_r[j]; tr = t_r; ts = t_s;
+          } else {
+            const int t = k / a.Cout;
+            n = k - t * a.Cout; tr = t / a.ns; ts = t - tr * a.ns;
+          }
           const int r = a.r0 + a.stride * tr, s = a.s0 + a.stride * ts;
           const float* src = wg + (((long long)n * a.R + r) * a.S + s) * a.Cin;
           if constexpr (VB) {
@@ -289,8 +307,7 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
       } else {  // WGRAD B: im2col(x), rows=(r,s,c), k = pixel
         const int p = k0 + (idx / (BN / 4));
         if (p < kend && b_ok[j]) {
-          const int HW = a.Ho * a.Wo;
-          const int b = p / HW, rem = p - b * HW, oh = rem / a.Wo, ow = rem - oh * a.Wo;
+          const int b = px_b[j], oh = px_h[j], ow = px_w[j];
           if constexpr (VB) {
             const int ih = oh * a.stride - a.pad + b_r[j], iw = ow * a.stride - a.pad + b_s[j];
             if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
@@ -315,6 +332,19 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
         }
       }
       rb[j] = v;
+      if constexpr (MODE == WGRAD) {  // advance this row's pixel by one tile
+        px_w[j] += BKT;
+        while (px_w[j] >= a.Wo) { px_w[j] -= a.Wo; ++px_h[j]; }
+        while (px_h[j] >= a.Ho) { px_h[j] -= a.Ho; ++px_b[j]; }
+      }
+    }
+    // advance the tile-uniform tap counters (FWD / DGRAD vector paths)
+    if constexpr (MODE == FWD && VA) {
+      t_c += BKT;
+      if (t_c >= a.Cin) { t_c = 0; if (++t_s == a.S) { t_s = 0; ++t_r; } }
+    } else if constexpr (MODE == DGRAD && VA) {
+      t_c += BKT;
+      if (t_c >= a.Cout) { t_c = 0; if (++t_s == a.ns) { t_s = 0; ++t_r; } }
     }
   };
 

@@ -10,32 +10,36 @@ using namespace mauv;
 namespace mauv {
 
 // Tie-break as torch's max_pool2d: first maximum in (kh, kw) scan order; NaN wins.
+// One thread per 4 channels of one output pixel (C % 4 == 0; the stem has C = 64).
 template <class S>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const typename S::T* __restrict__ x,
                                                           int N, int H, int W, int C, int Ho,
                                                           int Wo, typename S::T* __restrict__ y,
                                                           unsigned char* __restrict__ idx) {
-  const long long total = (long long)N * Ho * Wo * C;
+  const int C4 = C / 4;
+  const long long total = (long long)N * Ho * Wo * C4;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c = (int)(i % C);
-    long long p = i / C;
+    const int c = 4 * (int)(i % C4);
+    long long p = i / C4;
     const int ow = (int)(p % Wo); p /= Wo;
     const int oh = (int)(p % Ho);
     const int n = (int)(p / Ho);
-    float best = -INFINITY;
-    int bi = 0;
+    floatx4 best = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int bi[4] = {0, 0, 0, 0};
     for (int r = 0; r < 3; ++r) {
       const int ih = oh * 2 - 1 + r;
       if (ih < 0 || ih >= H) continue;
       for (int s = 0; s < 3; ++s) {
         const int iw = ow * 2 - 1 + s;
         if (iw < 0 || iw >= W) continue;
-        const float v = S::ld(x + (((long long)n * H + ih) * W + iw) * C + c);
-        if (v > best || isnan(v)) { best = v; bi = r * 3 + s; }
+        const floatx4 v = S::ld4(x + (((long long)n * H + ih) * W + iw) * C + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (v[e] > best[e] || isnan(v[e])) { best[e] = v[e]; bi[e] = r * 3 + s; }
       }
     }
-    S::st(y + i, best);
-    idx[i] = (unsigned char)bi;
+    S::st4(y + 4 * i, best);
+    *(uchar4*)(idx + 4 * i) = make_uchar4(bi[0], bi[1], bi[2], bi[3]);
   }
 }
 
@@ -44,14 +48,15 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const typename S::T* _
                                                           const unsigned char* __restrict__ idx,
                                                           int N, int H, int W, int C, int Ho,
                                                           int Wo, typename S::T* __restrict__ dx) {
-  const long long total = (long long)N * H * W * C;
+  const int C4 = C / 4;
+  const long long total = (long long)N * H * W * C4;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c = (int)(i % C);
-    long long p = i / C;
+    const int c = 4 * (int)(i % C4);
+    long long p = i / C4;
     const int iw = (int)(p % W); p /= W;
     const int ih = (int)(p % H);
     const int n = (int)(p / H);
-    float acc = 0.f;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     const int oh_lo = max(0, ih / 2), oh_hi = min(Ho - 1, (ih + 1) / 2);
     const int ow_lo = max(0, iw / 2), ow_hi = min(Wo - 1, (iw + 1) / 2);
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
@@ -61,10 +66,16 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const typename S::T* _
         const int s = iw - (ow * 2 - 1);
         if (s < 0 || s > 2) continue;
         const long long o = (((long long)n * Ho + oh) * Wo + ow) * C + c;
-        if (idx[o] == r * 3 + s) acc += S::ld(dy + o);
+        const uchar4 k = *(const uchar4*)(idx + o);
+        const floatx4 g = S::ld4(dy + o);
+        const int t = r * 3 + s;
+        if (k.x == t) acc[0] += g[0];
+        if (k.y == t) acc[1] += g[1];
+        if (k.z == t) acc[2] += g[2];
+        if (k.w == t) acc[3] += g[3];
       }
     }
-    S::st(dx + i, acc);
+    S::st4(dx + 4 * i, acc);
   }
 }
 
@@ -122,7 +133,8 @@ static int grid1(long long n) {
 MAUV_API int mauv_maxpool_fwd(const float* x, int N, int H, int W, int C, float* y,
                               unsigned char* idx, hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  hipLaunchKernelGGL(maxpool_fwd_kernel<SF32>, dim3(grid1((long long)N * Ho * Wo * C)), dim3(256),
+  if (C % 4) { set_error("maxpool_fwd: C % 4 != 0"); return kErrArg; }
+  hipLaunchKernelGGL(maxpool_fwd_kernel<SF32>, dim3(grid1((long long)N * Ho * Wo * C / 4)), dim3(256),
                      0, stream, x, N, H, W, C, Ho, Wo, y, idx);
   return check_launch("maxpool_fwd");
 }
@@ -130,7 +142,8 @@ MAUV_API int mauv_maxpool_fwd(const float* x, int N, int H, int W, int C, float*
 MAUV_API int mauv_maxpool_bwd(const float* dy, const unsigned char* idx, int N, int H, int W,
                               int C, float* dx, hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  hipLaunchKernelGGL(maxpool_bwd_kernel<SF32>, dim3(grid1((long long)N * H * W * C)), dim3(256),
+  if (C % 4) { set_error("maxpool_bwd: C % 4 != 0"); return kErrArg; }
+  hipLaunchKernelGGL(maxpool_bwd_kernel<SF32>, dim3(grid1((long long)N * H * W * C / 4)), dim3(256),
                      0, stream, dy, idx, N, H, W, C, Ho, Wo, dx);
   return check_launch("maxpool_bwd");
 }
@@ -153,7 +166,8 @@ MAUV_API int mauv_avgpool_bwd(const float* dy, int N, int HW, int C, float* dx,
 MAUV_API int mauv_maxpool_fwd_h16(int dtype, const void* x, int N, int H, int W, int C, void* y,
                                   unsigned char* idx, hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-#define L(D) hipLaunchKernelGGL(maxpool_fwd_kernel<S16<D>>, dim3(grid1((long long)N * Ho * Wo * C)), \
+  if (C % 4) { set_error("maxpool_fwd_h16: C % 4 != 0"); return kErrArg; }
+#define L(D) hipLaunchKernelGGL(maxpool_fwd_kernel<S16<D>>, dim3(grid1((long long)N * Ho * Wo * C / 4)), \
                                 dim3(256), 0, stream, (const u16*)x, N, H, W, C, Ho, Wo, (u16*)y, idx);
   MAUV_DT_DISPATCH(dtype, "maxpool_fwd_h16", L)
 #undef L
@@ -163,7 +177,8 @@ MAUV_API int mauv_maxpool_fwd_h16(int dtype, const void* x, int N, int H, int W,
 MAUV_API int mauv_maxpool_bwd_h16(int dtype, const void* dy, const unsigned char* idx, int N,
                                   int H, int W, int C, void* dx, hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-#define L(D) hipLaunchKernelGGL(maxpool_bwd_kernel<S16<D>>, dim3(grid1((long long)N * H * W * C)), \
+  if (C % 4) { set_error("maxpool_bwd_h16: C % 4 != 0"); return kErrArg; }
+#define L(D) hipLaunchKernelGGL(maxpool_bwd_kernel<S16<D>>, dim3(grid1((long long)N * H * W * C / 4)), \
                                 dim3(256), 0, stream, (const u16*)dy, idx, N, H, W, C, Ho, Wo, (u16*)dx);
   MAUV_DT_DISPATCH(dtype, "maxpool_bwd_h16", L)
 #undef L

@@ -47,10 +47,10 @@ SIGNATURES = {
     "mauv_bn_workspace_floats": [I, LL, I],
     "mauv_bn_fwd_train": [P, I, LL, I, P, P, P, P, F, F, P, P, P, P, P, P, I, P, P],
     "mauv_bn_stats_finalize": [I, I, I, P, P, P, P, P, P, P, F, F, P, P, P, P, P, P],
-    "mauv_bn_apply": [P, P, P, P, I, P, I, LL, I, P],
+    "mauv_bn_apply": [P, P, P, P, P, P, I, P, I, LL, I, P],
     "mauv_bn_eval_params": [I, I, P, P, P, P, F, P, P, P],
     "mauv_bn_bwd": [P, P, P, I, P, P, P, P, I, LL, I, P, P, P, P, P, P, P, I, P],
-    "mauv_bn_apply_h16": [I, P, P, P, P, I, P, I, LL, I, P],
+    "mauv_bn_apply_h16": [I, P, P, P, P, P, P, I, P, I, LL, I, P],
     "mauv_bn_bwd_h16": [I, P, P, P, I, P, P, P, P, I, LL, I, P, P, P, P, P, P],
     # pool.hip
     "mauv_maxpool_fwd": [P, I, I, I, I, P, P, P],

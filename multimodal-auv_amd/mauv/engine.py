@@ -313,7 +313,7 @@ class TrunkRunner(_Runner):
                             accumulate=accumulate, bn=bn_args)
         return dx, pre
 
-    def _bn(self, bn, y, part, relu, res=None, materialize=True):
+    def _bn(self, bn, y, part, relu, res=None, materialize=True, res_bn=None):
         """Statistics (from the conv epilogue partials) + optional materialised output."""
         G, C = self.G, y.shape[-1]
         M = y.numel() // (G * C)
@@ -338,7 +338,7 @@ class TrunkRunner(_Runner):
         out = None
         if materialize:
             out = torch.empty_like(y)
-            ops.bn_apply(y, scale, shift, res, relu, out, G, M, C)
+            ops.bn_apply(y, scale, shift, res, relu, out, G, M, C, res_bn=res_bn)
         rec = _BN(bn, y, out if relu else None, stats, relu, M, C, batch_stats) \
             if self.save else None
         self.last_lazy = (scale, shift, int(relu))  # for a consumer applying it on load
@@ -395,14 +395,14 @@ class TrunkRunner(_Runner):
             H2, W2 = y2.shape[2], y2.shape[3]
             _, s2 = self._bn(blk.bn2, y2, p2, relu=True, materialize=False)
             y3, r3, p3 = self._conv(blk.conv3, y2, B, H2, W2, x_bn=self.last_lazy)
-            rd = sd = None
-            if blk.downsample is not None:
-                yd, rd, pd_ = self._conv(blk.downsample[0], cur, B, H, W)
-                res, sd = self._bn(blk.downsample[1], yd, pd_, relu=False)
-                del yd
+            rd = sd = res_bn = None
+            if blk.downsample is not None:   # its BN is applied inside bn3's residual add
+                res, rd, pd_ = self._conv(blk.downsample[0], cur, B, H, W)
+                _, sd = self._bn(blk.downsample[1], res, pd_, relu=False, materialize=False)
+                res_bn = self.last_lazy[:2]
             else:
                 res = cur
-            a3, s3 = self._bn(blk.bn3, y3, p3, relu=True, res=res)
+            a3, s3 = self._bn(blk.bn3, y3, p3, relu=True, res=res, res_bn=res_bn)
             del res
             if self.save:
                 recs.append((r1, s1, r2, s2, r3, s3, rd, sd))

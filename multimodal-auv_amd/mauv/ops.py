@@ -224,15 +224,18 @@ def bn_fwd_train(y, G, M, C, gamma, beta, run_mean, run_var, momentum, eps, ws, 
           "bn_fwd_train")
 
 
-def bn_apply(y, scale, shift, res, relu, out, G, M, C):
+def bn_apply(y, scale, shift, res, relu, out, G, M, C, res_bn=None):
+    """out = [relu](y*scale + shift (+ res')); res_bn = (res_scale, res_shift): the residual
+    is a pending BN applied here (res' = res*res_scale + res_shift)."""
+    rs, rh = res_bn if res_bn is not None else (None, None)
     if y.dtype in H16:
         _h16(y.dtype, y, res, out)
-        check(lib.mauv_bn_apply_h16(H16[y.dtype], _p(y), _p(scale), _p(shift), _p(res), int(relu),
-                                    _p(out), G, M, C, stream()), "bn_apply_h16")
+        check(lib.mauv_bn_apply_h16(H16[y.dtype], _p(y), _p(scale), _p(shift), _p(res), _p(rs),
+                                    _p(rh), int(relu), _p(out), G, M, C, stream()), "bn_apply_h16")
         return
     _f32(y, res, out)
-    check(lib.mauv_bn_apply(_p(y), _p(scale), _p(shift), _p(res), int(relu), _p(out), G, M, C,
-                            stream()), "bn_apply")
+    check(lib.mauv_bn_apply(_p(y), _p(scale), _p(shift), _p(res), _p(rs), _p(rh), int(relu),
+                            _p(out), G, M, C, stream()), "bn_apply")
 
 
 def bn_eval_params(G, C, gamma, beta, run_mean, run_var, eps, scale, shift):

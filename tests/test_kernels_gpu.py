@@ -321,3 +321,18 @@ def test_mc_head_kernels():
     x[777] = float("nan")
     ops.nonfinite_count(x, cnt)
     assert cnt.item() > 0
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+def test_bn_apply_pending_residual_bn(dt):
+    """bn3 apply with the downsample BN folded in: relu(y*s+h + r*rs+rh)."""
+    from mauv import ops
+    G, M, C = 2, 50, 256
+    torch.manual_seed(9)
+    y, r = (torch.randn(G, M, C).to(dt).to(dev) for _ in range(2))
+    s, h, rs, rh = (torch.randn(G, C, device=dev) for _ in range(4))
+    out = torch.empty(G, M, C, device=dev, dtype=dt)
+    ops.bn_apply(y, s, h, r, True, out, G, M, C, res_bn=(rs, rh))
+    ref = torch.relu(y.float() * s[:, None] + h[:, None] + r.float() * rs[:, None] + rh[:, None])
+    tol = 1e-5 if dt == torch.float32 else 2 ** -7
+    close(out.float(), ref, rtol=tol, atol=tol)
