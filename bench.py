@@ -167,7 +167,8 @@ def main():
     if world > 1:
         from mauv.ddp import DistributedMC
         model = DistributedMC(model)
-    opt = torch.optim.Adam(model.parameters(), lr=5e-5)
+    from mauv.optim import FusedAdam   # what mauv.loop_utils builds for GPU models
+    opt = FusedAdam(model.parameters(), lr=5e-5)
     crit = torch.nn.CrossEntropyLoss()
     x, b, s, y = synthetic_batch(args.batch, args.optical, args.sonar, dev, 1234 + rank)
     kl_w = 2.0 ** 1 / 2.0 ** 30   # epoch 0 of 30 (main.py:293)

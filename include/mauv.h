@@ -148,6 +148,20 @@ int mauv_kl_bwd(const MauvKlEntry* table, int n, const float* coef_dev, float sc
 int mauv_philox_raw(unsigned long long seed, unsigned long long sample, unsigned int layer,
                     int nq, unsigned int* out_u32x4, float* out_normal4, hipStream_t stream);
 
+/* ---- fused Adam (adam.hip) ------------------------------------------------------------------
+ * torch.optim.Adam as the reference builds it (train/loop_utils.py:45-61: amsgrad=False,
+ * maximize=False, L2 weight_decay) stepped for a whole table of fp32 tensors in one launch;
+ * step = the (shared) 1-based step count used for bias correction. */
+typedef struct MauvAdamEntry {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  long long numel;
+} MauvAdamEntry;
+int mauv_adam_step(const MauvAdamEntry* table, int n, float lr, float beta1, float beta2,
+                   float eps, float weight_decay, long long step, hipStream_t stream);
+
 /* ---- BatchNorm2d (training mode, per MC group) + residual + ReLU (bn.hip) ---------------
  * torchvision Bottleneck bn1..3 / downsample.1 / stem bn1 in .train() for every MC pass
  * (train/multimodal.py:60,232; inference/predictors.py:27).  y/out [G][M][C], M = B*H*W. */

@@ -75,7 +75,7 @@ __device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int
 constexpr int BK = 16;  // host-side alignment granule (both tile depths are multiples)
 constexpr int PAD = 4;
 
-template <int MODE, int BM, int BN, int BKT, bool VA, bool VB>
+template <int MODE, int BM, int BN, int BKT, bool VA, bool VB, bool MID>
 __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
   constexpr int KQ = BKT / 4;  // float4 per k-row of a k-contiguous tile row
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 32, NI = WN / 32;
@@ -409,8 +409,14 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+      // MID: write the next tile's staged registers into the other LDS buffer halfway through
+      // this tile's MFMAs (that buffer was last read before the previous barrier), so the
+      // ds_writes overlap this wave's own MFMA execution instead of forming a separate phase
+      if constexpr (MID)
+        if (kk == BKT / 4 - 1 && more) store_tiles(cur ^ 1);
     }
-    if (more) store_tiles(cur ^ 1);
+    if constexpr (!MID)
+      if (more) store_tiles(cur ^ 1);
     __syncthreads();
     cur ^= 1;
   }
@@ -540,6 +546,7 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
 }
 
 static int g_bk = 0;  // tile depth: 16 or 32 (MAUV_CONV_BK; default 16)
+static int g_mid = -1;  // MAUV_CONV_MIDSTORE: LDS writes of the next tile mid-loop
 
 template <int MODE, int BM, int BN, bool VA, bool VB>
 static void launch(const ConvArgs& a, hipStream_t st) {
@@ -547,11 +554,19 @@ static void launch(const ConvArgs& a, hipStream_t st) {
     const char* e = getenv("MAUV_CONV_BK");
     g_bk = (e && atoi(e) == 32) ? 32 : 16;  // measured: 16 wins (3 vs 2 blocks/CU)
   }
+  if (g_mid < 0) {
+    const char* e = getenv("MAUV_CONV_MIDSTORE");
+    g_mid = e ? atoi(e) : 0;
+  }
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
-  if (g_bk == 16)
-    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 32, VA, VB>), grid, dim3(256), 0, st, a);
+  if (g_bk == 16) {
+    if (g_mid)
+      hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, true>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, false>), grid, dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 32, VA, VB, false>), grid, dim3(256), 0, st, a);
+  }
 }
 
 template <int MODE, bool VA, bool VB>

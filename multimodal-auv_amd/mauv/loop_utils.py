@@ -1,6 +1,8 @@
 """Epoch drivers and optimiser factory with the reference's signatures (train/loop_utils.py).
 
-* ``define_optimizers_and_schedulers``      loop_utils.py:13-63 (CE + 4 Adam + 4 StepLR)
+* ``define_optimizers_and_schedulers``      loop_utils.py:13-63 (CE + 4 Adam + 4 StepLR; Adam
+                                            is mauv.optim.FusedAdam — one HIP launch per step —
+                                            for models on a ROCm device, torch's otherwise)
 * ``train_and_evaluate_unimodal_model``     loop_utils.py:65-159 (epochs ``range(1, n)``)
 * ``train_and_evaluate_multimodal_model``   loop_utils.py:162-250 (scheduler stepped after
                                             training AND after evaluation, as the reference)
@@ -11,6 +13,7 @@ import os
 import torch.nn as nn
 import torch.optim as optim
 
+from .optim import FusedAdam
 from .train import (train_unimodal_model, evaluate_unimodal_model, train_multimodal_model,
                     evaluate_multimodal_model)
 
@@ -23,8 +26,11 @@ def define_optimizers_and_schedulers(models_dict, optimizer_params=None, schedul
         logging.error(f"Unsupported criterion type provided: {criterion_type}")
         raise ValueError(f"Unsupported criterion: {criterion_type}")
     criterion = nn.CrossEntropyLoss()
-    optimizers = {k: optim.Adam(models_dict[k].parameters(), **optimizer_params[k])
-                  for k in _MODEL_KEYS}
+    def adam(model, kw):
+        params = list(model.parameters())
+        on_gpu = all(p.is_cuda for p in params)
+        return (FusedAdam if on_gpu else optim.Adam)(params, **kw)
+    optimizers = {k: adam(models_dict[k], optimizer_params[k]) for k in _MODEL_KEYS}
     schedulers = {k: optim.lr_scheduler.StepLR(optimizers[k], **scheduler_params[k])
                   for k in optimizers}
     return criterion, optimizers, schedulers
