@@ -91,8 +91,10 @@ def pmc_traffic():
     return d["bytes_per_launch"], os.path.relpath(files[-1], REPO)
 
 
-def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic=True,
+def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic=True, suffix="",
                   kernel="conv_gemm_f32 (implicit-GEMM fwd+dgrad+wgrad, all launches of one step)"):
+    """Roofline of one step's implicit-GEMM launches of one precision (suffix "" = fp32,
+    "_bfloat16" = the 16-bit trunks; the fp32 fusion-head GEMMs are then excluded)."""
     from mauv import ops
     ops.PROFILE = []
     torch.cuda.synchronize()
@@ -102,6 +104,8 @@ def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic=True,
     by = {}
     nbytes = 0.0
     for kind, fl, nb, nl, e0, e1 in rows:
+        if (suffix and not kind.endswith(suffix)) or (not suffix and "_" in kind):
+            continue
         ms = e0.elapsed_time(e1)
         d = by.setdefault(kind, [0, 0.0, 0.0])
         d[0] += nl
@@ -228,7 +232,7 @@ def main():
                           f"statistics, master weights, head), num_mc={args.num_mc}"}
         if not args.no_roofline:
             bf16["roofline"] = roofline_step(
-                step, peak=BF16_MFMA_PEAK_TF, traffic=False,
+                step, peak=BF16_MFMA_PEAK_TF, traffic=False, suffix="_bfloat16",
                 kernel="conv_gemm_h16<bf16> (implicit-GEMM fwd+dgrad+wgrad, one step)")
         set_precision(model.module if world > 1 else model, None)
 

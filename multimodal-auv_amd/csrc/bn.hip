@@ -186,29 +186,26 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const typename S::T* __re
                                                        const float* __restrict__ res_shift,
                                                        int relu, typename S::T* __restrict__ out,
                                                        long long M, int C) {
-  const int c4n = C / 4;
-  const long long per_g = M * c4n;
+  const int c8n = C / 8;  // 8 channels per thread-iteration: 16-B (16-bit) / 2x16-B (fp32)
+  const long long per_g = M * c8n;
   const int g = blockIdx.y;
   const typename S::T* yg = y + (long long)g * M * C;
   typename S::T* og = out + (long long)g * M * C;
   const typename S::T* rg = res ? res + (long long)g * M * C : nullptr;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < per_g; i += (long long)gridDim.x * 256) {
-    const int c = 4 * (int)(i % c4n);
-    floatx4 v = S::ld4(yg + 4 * i);
-    const floatx4 sc = *(const floatx4*)(scale + g * C + c);
-    const floatx4 sh = *(const floatx4*)(shift + g * C + c);
-    v = v * sc + sh;
+    const int c = 8 * (int)(i % c8n);
+    floatx8 v = S::ld8(yg + 8 * i);
+    v = v * ldf8(scale + g * C + c) + ldf8(shift + g * C + c);
     if (rg) {
-      floatx4 rv = S::ld4(rg + 4 * i);
-      if (res_scale)
-        rv = rv * *(const floatx4*)(res_scale + g * C + c) + *(const floatx4*)(res_shift + g * C + c);
+      floatx8 rv = S::ld8(rg + 8 * i);
+      if (res_scale) rv = rv * ldf8(res_scale + g * C + c) + ldf8(res_shift + g * C + c);
       v += rv;
     }
     if (relu) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+      for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
     }
-    S::st4(og + 4 * i, v);
+    S::st8(og + 8 * i, v);
   }
 }
 
@@ -240,52 +237,46 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const typename S::T* __res
                                                       long long M, int C, int rpb, RowMap rm,
                                                       float* __restrict__ p1,
                                                       float* __restrict__ p2) {
+  // one 8-channel group per thread (C % 8 == 0, C <= 2048): tpr threads span a row, rp rows
+  // are walked in parallel
+  const int tpr = C / 8, rp = 256 / tpr;
   const int g = blockIdx.y, blk = blockIdx.x, nblk = gridDim.x;
   const int tid = threadIdx.x;
-  const int t_c = tid % rm.tpr, t_r = tid / rm.tpr;
+  const int t_c = tid % tpr, t_r = tid / tpr;
   const long long r0 = (long long)blk * rpb;
   const long long r1 = min(M, r0 + rpb);
   const long long go = (long long)g * M * C;
-  float s1[MAXCPT][4], s2[MAXCPT][4], mu[MAXCPT][4], is[MAXCPT][4];
+  const int c0 = 8 * t_c, gc = g * C + c0;
+  floatx8 s1 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2 = s1;
+  if (t_r < rp) {
+    const floatx8 mu = ldf8(mean + gc), is = ldf8(invstd + gc);
+    floatx8 sc, sh;
+    if (relu && !out) { sc = ldf8(scale + gc); sh = ldf8(shift + gc); }
+    for (long long r = r0 + t_r; r < r1; r += rp) {
+      const long long o = go + r * C + c0;
+      const floatx8 yv = S::ld8(y + o);
+      floatx8 dz = S::ld8(dout + o);
+      if (relu) {
+        const floatx8 pre = out ? S::ld8(out + o) : yv * sc + sh;
 #pragma unroll
-  for (int j = 0; j < MAXCPT; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      s1[j][e] = 0.f; s2[j][e] = 0.f;
-      const int c = 4 * (t_c + j * rm.tpr) + e;
-      mu[j][e] = j < rm.cpt ? mean[g * C + c] : 0.f;
-      is[j][e] = j < rm.cpt ? invstd[g * C + c] : 0.f;
-    }
-  for (long long r = r0 + t_r; r < r1; r += rm.rp) {
-#pragma unroll
-    for (int j = 0; j < MAXCPT; ++j) {
-      if (j >= rm.cpt) break;
-      const long long o = go + r * C + 4 * (t_c + j * rm.tpr);
-      const floatx4 yv = S::ld4(y + o);
-      floatx4 dz = S::ld4(dout + o);
-      if (relu) dz = relu_mask<S>(dz, out, o, yv, scale, shift, g * C + 4 * (t_c + j * rm.tpr));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s1[j][e] += dz[e];
-        s2[j][e] += dz[e] * (yv[e] - mu[j][e]) * is[j][e];
+        for (int e = 0; e < 8; ++e) dz[e] = pre[e] > 0.f ? dz[e] : 0.f;
       }
+      s1 += dz;
+      s2 += dz * (yv - mu) * is;
     }
   }
-  __shared__ float sh1[4096], sh2[4096];
+  __shared__ float sh1[2048], sh2[2048];  // [rp][C], rp * C = 8 * 256
+  if (t_r < rp) {
 #pragma unroll
-  for (int j = 0; j < MAXCPT; ++j) {
-    if (j >= rm.cpt) break;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = 4 * (t_c + j * rm.tpr) + e;
-      sh1[t_r * C + c] = s1[j][e];
-      sh2[t_r * C + c] = s2[j][e];
+    for (int e = 0; e < 8; ++e) {
+      sh1[t_r * C + c0 + e] = s1[e];
+      sh2[t_r * C + c0 + e] = s2[e];
     }
   }
   __syncthreads();
   for (int c = tid; c < C; c += 256) {
     float a = 0.f, b = 0.f;
-    for (int r = 0; r < rm.rp; ++r) { a += sh1[r * C + c]; b += sh2[r * C + c]; }
+    for (int r = 0; r < rp; ++r) { a += sh1[r * C + c]; b += sh2[r * C + c]; }
     const long long o = ((long long)g * nblk + blk) * C + c;
     p1[o] = a;
     p2[o] = b;
@@ -329,7 +320,7 @@ __global__ void bn_bwd_param_kernel(int G, int C, long long M, const float* __re
   if (dbeta) dbeta[c] += (float)(tb * (double)M);
 }
 
-// dy = gamma*invstd * (dz - k1 - xhat*k2); dres = dz (optional)
+// dy = gamma*invstd * (dz - k1 - xhat*k2); dres = dz (optional).  8 channels per iteration.
 template <class S>
 __global__ __launch_bounds__(256) void bn_bwd_apply(const typename S::T* __restrict__ y,
                                                     const typename S::T* __restrict__ out,
@@ -344,24 +335,24 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const typename S::T* __restr
                                                     typename S::T* __restrict__ dy,
                                                     typename S::T* __restrict__ dres, long long M,
                                                     int C) {
-  const int c4n = C / 4;
-  const long long per_g = M * c4n;
+  const int c8n = C / 8;
+  const long long per_g = M * c8n;
   const int g = blockIdx.y;
   const long long go = (long long)g * M * C;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < per_g; i += (long long)gridDim.x * 256) {
-    const int c = 4 * (int)(i % c4n);
-    const long long o = go + 4 * i;
-    floatx4 dz = S::ld4(dout + o);
-    const floatx4 yv = S::ld4(y + o);
-    if (relu) dz = relu_mask<S>(dz, out, o, yv, scale, shift, g * C + c);
-    const floatx4 mu = *(const floatx4*)(mean + g * C + c);
-    const floatx4 is = *(const floatx4*)(invstd + g * C + c);
-    const floatx4 sc = *(const floatx4*)(scale + g * C + c);
-    const floatx4 a = *(const floatx4*)(k1 + g * C + c);
-    const floatx4 b = *(const floatx4*)(k2 + g * C + c);
-    const floatx4 xh = (yv - mu) * is;
-    S::st4(dy + o, sc * (dz - a - xh * b));
-    if (dres) S::st4(dres + o, dz);
+    const int c = 8 * (int)(i % c8n);
+    const long long o = go + 8 * i;
+    floatx8 dz = S::ld8(dout + o);
+    const floatx8 yv = S::ld8(y + o);
+    const int gc = g * C + c;
+    if (relu) {
+      const floatx8 pre = out ? S::ld8(out + o) : yv * ldf8(scale + gc) + ldf8(shift + gc);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dz[e] = pre[e] > 0.f ? dz[e] : 0.f;
+    }
+    const floatx8 xh = (yv - ldf8(mean + gc)) * ldf8(invstd + gc);
+    S::st8(dy + o, ldf8(scale + gc) * (dz - ldf8(k1 + gc) - xh * ldf8(k2 + gc)));
+    if (dres) S::st8(dres + o, dz);
   }
 }
 
@@ -419,7 +410,7 @@ MAUV_API int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const 
                                float momentum, float eps, float* workspace, float* mean,
                                float* invstd, float* scale, float* shift, const float* res,
                                int relu, float* out, hipStream_t stream) {
-  if (C % 4 != 0 || C > 2048 || G <= 0 || M <= 0) { set_error("bn_fwd: unsupported C/G/M"); return kErrArg; }
+  if (C % 8 != 0 || C > 2048 || G <= 0 || M <= 0) { set_error("bn_fwd: unsupported C/G/M"); return kErrArg; }
   int nblk, rpb;
   reduce_geometry(M, C, nblk, rpb);
   const RowMap rm = row_map(C);
@@ -435,7 +426,7 @@ MAUV_API int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const 
     hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
                        mean, uvar, run_mean, run_var, momentum);
   if (out) {
-    hipLaunchKernelGGL(bn_apply_kernel<SF32>, dim3(ew_grid(M * C / 4 / 1), G), dim3(256), 0, stream,
+    hipLaunchKernelGGL(bn_apply_kernel<SF32>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, stream,
                        y, scale, shift, res, nullptr, nullptr, relu, out, M, C);
   }
   return check_launch("bn_fwd_train");
@@ -461,7 +452,8 @@ MAUV_API int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, 
 MAUV_API int mauv_bn_apply(const float* y, const float* scale, const float* shift,
                            const float* res, const float* res_scale, const float* res_shift,
                            int relu, float* out, int G, long long M, int C, hipStream_t stream) {
-  hipLaunchKernelGGL(bn_apply_kernel<SF32>, dim3(ew_grid(M * C / 4), G), dim3(256), 0, stream, y,
+  if (C % 8 != 0) { set_error("bn_apply: C % 8 != 0"); return kErrArg; }
+  hipLaunchKernelGGL(bn_apply_kernel<SF32>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, stream, y,
                      scale, shift, res, res_scale, res_shift, relu, out, M, C);
   return check_launch("bn_apply");
 }
@@ -473,7 +465,7 @@ static int bn_bwd_impl(const typename S::T* y, const typename S::T* out,
                        long long M, int C, float* workspace, typename S::T* dy,
                        typename S::T* dres, float* dgamma, float* dbeta, const float* pre_p1,
                        const float* pre_p2, int pre_nblk, hipStream_t stream) {
-  if (C % 4 != 0 || C > 2048) { set_error("bn_bwd: unsupported C"); return kErrArg; }
+  if (C % 8 != 0 || C > 2048) { set_error("bn_bwd: unsupported C (C % 8 != 0 or > 2048)"); return kErrArg; }
   if (relu && !out && !shift) { set_error("bn_bwd: relu mask needs out or scale/shift"); return kErrArg; }
   int nblk, rpb;
   reduce_geometry(M, C, nblk, rpb);
@@ -494,7 +486,7 @@ static int bn_bwd_impl(const typename S::T* y, const typename S::T* out,
   if (dgamma || dbeta)
     hipLaunchKernelGGL(bn_bwd_param_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C, M,
                        k1, k2, dgamma, dbeta);
-  hipLaunchKernelGGL(bn_bwd_apply<S>, dim3(ew_grid(M * C / 4), G), dim3(256), 0, stream, y, out,
+  hipLaunchKernelGGL(bn_bwd_apply<S>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, stream, y, out,
                      dout, relu, mean, invstd, scale, shift, k1, k2, dy, dres, M, C);
   return check_launch("bn_bwd");
 }
@@ -518,7 +510,8 @@ MAUV_API int mauv_bn_apply_h16(int dtype, const void* y, const float* scale, con
                                const void* res, const float* res_scale, const float* res_shift,
                                int relu, void* out, int G, long long M, int C,
                                hipStream_t stream) {
-#define L(D) hipLaunchKernelGGL(bn_apply_kernel<S16<D>>, dim3(ew_grid(M * C / 4), G), dim3(256), 0, \
+  if (C % 8 != 0) { set_error("bn_apply_h16: C % 8 != 0"); return kErrArg; }
+#define L(D) hipLaunchKernelGGL(bn_apply_kernel<S16<D>>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, \
                                 stream, (const u16*)y, scale, shift, (const u16*)res, res_scale,    \
                                 res_shift, relu, (u16*)out, M, C);
   MAUV_DT_DISPATCH(dtype, "bn_apply_h16", L)

@@ -77,6 +77,20 @@ struct SF32 {
   static __device__ __forceinline__ void st(T* p, float v) { *p = v; }
   static __device__ __forceinline__ floatx4 ld4(const T* p) { return *(const floatx4*)p; }
   static __device__ __forceinline__ void st4(T* p, floatx4 v) { *(floatx4*)p = v; }
+  static __device__ __forceinline__ floatx8 ld8(const T* p) {
+    const floatx4 a = *(const floatx4*)p, b = *(const floatx4*)(p + 4);
+    floatx8 f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { f[e] = a[e]; f[4 + e] = b[e]; }
+    return f;
+  }
+  static __device__ __forceinline__ void st8(T* p, floatx8 v) {
+    floatx4 a, b;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { a[e] = v[e]; b[e] = v[4 + e]; }
+    *(floatx4*)p = a;
+    *(floatx4*)(p + 4) = b;
+  }
 };
 
 template <int DT>
@@ -99,8 +113,14 @@ struct S16 {
     u.y = (unsigned)H16<DT>::from_f(v[2]) | ((unsigned)H16<DT>::from_f(v[3]) << 16);
     *(uint2*)p = u;
   }
+  static __device__ __forceinline__ floatx8 ld8(const T* p) { return unpack8<DT>(*(const u32x4*)p); }
+  static __device__ __forceinline__ void st8(T* p, floatx8 v) { *(u32x4*)p = pack8<DT>(v); }
 };
 
+}  // namespace mauv
+
+namespace mauv {
+__device__ __forceinline__ floatx8 ldf8(const float* p) { return SF32::ld8(p); }
 }  // namespace mauv
 
 // Dispatch a C-ABI dtype code to a launch macro L(DT) (returns kErrArg on a bad code).

@@ -282,7 +282,7 @@ class TrunkRunner(_Runner):
             part = (buf[:G * nblk * Cout], buf[G * nblk * Cout:2 * G * nblk * Cout],
                     buf[2 * G * nblk * Cout:], nblk)
         ops.conv2d_fwd(x, w, y, G, B, H, W, cp, Cout, k, st, pd, x_strides=x_strides,
-                       x_bn=x_bn, stats=None if part is None else part[:3])
+                       x_bn=x_bn, stats=None if part is None else part[:3], alg_cin=Cin)
         rec = (conv, x, x_strides, x_bn, w, B, H, W) if self.save else None
         return y, rec, part
 
@@ -297,7 +297,7 @@ class TrunkRunner(_Runner):
             splits = ops.wgrad_splits(G, B, H, W, cp, Cout, k, st, pd)
             ws = torch.empty(splits, G, Cout, k * k * cp, device=dy.device)
             ops.conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, cp, Cout, k, st, pd,
-                                  x_strides=xs, x_bn=x_bn)
+                                  x_strides=xs, x_bn=x_bn, alg_cin=Cin)
             self._reparam_bwd(conv, conv.mu_kernel, conv.rho_kernel, ws, splits, Cout, Cin,
                               k * k, "kernel", dw_cin=cp)
             del ws

@@ -70,7 +70,7 @@ class _Prof:
 
 # ----------------------------------------------------------------------- convolutions
 def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_strides=None,
-               x_bn=None, stats=None):
+               x_bn=None, stats=None, alg_cin=None):
     """y[G][B*Ho*Wo][Cout] = conv(x'[g], w[g]) (+ bias[g]); w: [G][Cout][R][R][Cin].
     x_bn = (scale [G][Cin], shift [G][Cin], relu): x' = [relu](x*scale + shift) on load.
     stats = (mean, m2, cnt) partial buffers for the epilogue BN statistics (see
@@ -80,7 +80,9 @@ def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_stri
     sm, s2, sn = stats if stats is not None else (None, None, None)
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
     xg = 1 if (x_strides is not None and x_strides[0] == 0) else G
-    fl = 2.0 * G * B * Ho * Wo * Cout * R * R * Cin
+    # profiling counts ALGORITHMIC work: a zero-padded stem input (16-bit path) counts its
+    # real channels (alg_cin)
+    fl = 2.0 * G * B * Ho * Wo * Cout * R * R * (alg_cin or Cin)
     esz = w.element_size()
     nb = esz * (xg * B * H * W * Cin + G * Cout * R * R * Cin + G * B * Ho * Wo * Cout)
     if w.dtype in H16:
@@ -141,13 +143,13 @@ def wgrad_splits(G, B, H, W, Cin, Cout, R, stride, pad):
 
 
 def conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, R, stride, pad,
-                      x_strides=None, x_bn=None):
+                      x_strides=None, x_bn=None, alg_cin=None):
     """ws[splits][G][Cout][R*R*Cin] partial slabs (x' as in conv2d_fwd)."""
     xs = None if x_strides is None else _LL5(*x_strides)
     sc, sh, rl = x_bn if x_bn is not None else (None, None, 0)
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
     xg = 1 if (x_strides is not None and x_strides[0] == 0) else G
-    fl = 2.0 * G * B * Ho * Wo * Cout * R * R * Cin
+    fl = 2.0 * G * B * Ho * Wo * Cout * R * R * (alg_cin or Cin)
     nb = dy.element_size() * (xg * B * H * W * Cin + G * B * Ho * Wo * Cout) + 4.0 * ws.numel()
     if dy.dtype in H16:
         _h16(dy.dtype, dy)
