@@ -147,6 +147,9 @@ def main():
     ap.add_argument("--no-infer", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="trunk precision of the headline measurement (default fp32 = "
+                         "configs[1]); bf16 = configs[2]'s per-GPU slice (profiling)")
     ap.add_argument("--no-bf16", action="store_true",
                     help="skip the bf16 training measurement (configs[2] per-GPU slice)")
     ap.add_argument("--bf16-steps", type=int, default=5)
@@ -175,6 +178,9 @@ def main():
     opt = FusedAdam(model.parameters(), lr=5e-5)
     crit = torch.nn.CrossEntropyLoss()
     x, b, s, y = synthetic_batch(args.batch, args.optical, args.sonar, dev, 1234 + rank)
+    if args.dtype == "bf16":
+        from mauv.engine import set_precision
+        set_precision(model.module if world > 1 else model, torch.bfloat16)
     kl_w = 2.0 ** 1 / 2.0 ** 30   # epoch 0 of 30 (main.py:293)
 
     def step():
@@ -234,7 +240,8 @@ def main():
             bf16["roofline"] = roofline_step(
                 step, peak=BF16_MFMA_PEAK_TF, traffic=False, suffix="_bfloat16",
                 kernel="conv_gemm_h16<bf16> (implicit-GEMM fwd+dgrad+wgrad, one step)")
-        set_precision(model.module if world > 1 else model, None)
+        set_precision(model.module if world > 1 else model,
+                      torch.bfloat16 if args.dtype == "bf16" else None)
 
     infer = None
     if not args.no_infer:
@@ -265,10 +272,11 @@ def main():
             "metric": METRIC, "value": round(triplets_s, 3), "unit": "triplets/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (random-init weights, MOPED rho; inputs resident in HBM)",
-            "config": {"workload": "configs[1]: tri-modal BNN training step, 7 classes, "
-                                   f"B={args.batch}/GPU fp32, num_mc={args.num_mc}, optical "
+            "config": {"workload": ("configs[1]" if args.dtype == "fp32" else "configs[2] slice")
+                                   + ": tri-modal BNN training step, 7 classes, "
+                                   f"B={args.batch}/GPU {args.dtype}, num_mc={args.num_mc}, optical "
                                    f"{args.optical}px + bathy/SSS {args.sonar}px",
                        "global_batch": args.batch * world, "num_mc": args.num_mc,
                        "parallelism": f"dp{world}"},

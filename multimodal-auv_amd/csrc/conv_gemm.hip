@@ -75,13 +75,21 @@ __device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int
 constexpr int BK = 16;  // host-side alignment granule (both tile depths are multiples)
 constexpr int PAD = 4;
 
-template <int MODE, int BM, int BN, int BKT, bool VA, bool VB, bool MID>
+// ROW: operands that are k-contiguous in HBM (FWD A and B, DGRAD A) are staged as row images
+// [rows][BKT+4] with one ds_write_b128 per float4, and each lane reads its whole k-slice of a
+// tile with ds_read_b128s up front (k order permuted: instruction kk of lane half lh takes
+// k = (BKT/2)*lh + kk, the same for A and B); k-strided operands keep the k-major image
+// [BKT][rows+4] read with one ds_read_b32 per MFMA.
+template <int MODE, int BM, int BN, int BKT, bool VA, bool VB, bool ROW>
 __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
   constexpr int KQ = BKT / 4;  // float4 per k-row of a k-contiguous tile row
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 32, NI = WN / 32;
   constexpr int NVA = BM * BKT / 4 / 256, NVB = BN * BKT / 4 / 256;
-  __shared__ float As[2][BKT][BM + PAD];
-  __shared__ float Bs[2][BKT][BN + PAD];
+  constexpr bool RA = ROW && (MODE != WGRAD), RB = ROW && (MODE == FWD);
+  constexpr int RLDF = BKT + 4;
+  constexpr int A_SZ = RA ? BM * RLDF : BKT * (BM + PAD);
+  constexpr int B_SZ = RB ? BN * RLDF : BKT * (BN + PAD);
+  __shared__ __attribute__((aligned(16))) float smem[2 * (A_SZ + B_SZ)];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -349,16 +357,21 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
   };
 
   auto store_tiles = [&](int buf) {
+    float* Ab = smem + buf * (A_SZ + B_SZ);
+    float* Bb = Ab + A_SZ;
 #pragma unroll
     for (int j = 0; j < NVA; ++j) {
       const int idx = tid + 256 * j;
       if constexpr (MODE == WGRAD) {
         const int kr = idx / (BM / 4), r4 = idx % (BM / 4);
-        *(floatx4*)&As[buf][kr][4 * r4] = ra[j];
+        *(floatx4*)(Ab + kr * (BM + PAD) + 4 * r4) = ra[j];
+      } else if constexpr (RA) {
+        const int row = idx / KQ, kq = idx % KQ;
+        *(floatx4*)(Ab + row * RLDF + 4 * kq) = ra[j];
       } else {
         const int row = idx / KQ, kq = idx % KQ;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) As[buf][4 * kq + e][row] = ra[j][e];
+        for (int e = 0; e < 4; ++e) Ab[(4 * kq + e) * (BM + PAD) + row] = ra[j][e];
       }
     }
 #pragma unroll
@@ -366,11 +379,15 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
       const int idx = tid + 256 * j;
       if constexpr (MODE == FWD) {
         const int row = idx / KQ, kq = idx % KQ;
+        if constexpr (RB) {
+          *(floatx4*)(Bb + row * RLDF + 4 * kq) = rb[j];
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Bs[buf][4 * kq + e][row] = rb[j][e];
+          for (int e = 0; e < 4; ++e) Bb[(4 * kq + e) * (BN + PAD) + row] = rb[j][e];
+        }
       } else {
         const int kr = idx / (BN / 4), r4 = idx % (BN / 4);
-        *(floatx4*)&Bs[buf][kr][4 * r4] = rb[j];
+        *(floatx4*)(Bb + kr * (BN + PAD) + 4 * r4) = rb[j];
       }
     }
   };
@@ -397,26 +414,64 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
       load_a(kbeg + (t + 1) * BKT);
       load_b(kbeg + (t + 1) * BKT);
     }
+    const float* Ab = smem + cur * (A_SZ + B_SZ);
+    const float* Bb = Ab + A_SZ;
+    if constexpr (RA || RB) {
+      constexpr int KH = BKT / 2;
+      float a8[MI][KH], b8[NI][KH];
 #pragma unroll
-    for (int kk = 0; kk < BKT / 2; ++kk) {
-      float av[MI], bv[NI];
+      for (int mi = 0; mi < MI; ++mi) {
+        if constexpr (RA) {
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) av[mi] = As[cur][2 * kk + lh][wm * WM + mi * 32 + li];
+          for (int q = 0; q < KH / 4; ++q) {
+            const floatx4 v = *(const floatx4*)(Ab + (wm * WM + mi * 32 + li) * RLDF + KH * lh + 4 * q);
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) bv[ni] = Bs[cur][2 * kk + lh][wn * WN + ni * 32 + li];
+            for (int e = 0; e < 4; ++e) a8[mi][4 * q + e] = v[e];
+          }
+        } else {
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
+          for (int kk = 0; kk < KH; ++kk)
+            a8[mi][kk] = Ab[(KH * lh + kk) * (BM + PAD) + wm * WM + mi * 32 + li];
+        }
+      }
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
-      // MID: write the next tile's staged registers into the other LDS buffer halfway through
-      // this tile's MFMAs (that buffer was last read before the previous barrier), so the
-      // ds_writes overlap this wave's own MFMA execution instead of forming a separate phase
-      if constexpr (MID)
-        if (kk == BKT / 4 - 1 && more) store_tiles(cur ^ 1);
+      for (int ni = 0; ni < NI; ++ni) {
+        if constexpr (RB) {
+#pragma unroll
+          for (int q = 0; q < KH / 4; ++q) {
+            const floatx4 v = *(const floatx4*)(Bb + (wn * WN + ni * 32 + li) * RLDF + KH * lh + 4 * q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) b8[ni][4 * q + e] = v[e];
+          }
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < KH; ++kk)
+            b8[ni][kk] = Bb[(KH * lh + kk) * (BN + PAD) + wn * WN + ni * 32 + li];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < KH; ++kk)
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a8[mi][kk], b8[ni][kk], acc[mi][ni], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BKT / 2; ++kk) {
+        float av[MI], bv[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) av[mi] = Ab[(2 * kk + lh) * (BM + PAD) + wm * WM + mi * 32 + li];
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) bv[ni] = Bb[(2 * kk + lh) * (BN + PAD) + wn * WN + ni * 32 + li];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+      }
     }
-    if constexpr (!MID)
-      if (more) store_tiles(cur ^ 1);
+    if (more) store_tiles(cur ^ 1);
     __syncthreads();
     cur ^= 1;
   }
@@ -487,7 +542,7 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
       }
     }
   if (fst || bst) {
-    float* red = &As[0][0][0];  // LDS is free: the main loop ended with a barrier
+    float* red = smem;  // LDS is free: the main loop ended with a barrier
     const int tcol = wn * WN + li;  // + ni*32
     // column totals of s1 over the block tile: lane halves, then the two wm waves
 #pragma unroll
@@ -546,7 +601,9 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
 }
 
 static int g_bk = 0;  // tile depth: 16 or 32 (MAUV_CONV_BK; default 16)
-static int g_mid = -1;  // MAUV_CONV_MIDSTORE: LDS writes of the next tile mid-loop
+// MAUV_CONV_ROW: row images + b128 operand reads for FWD (bit 0) / DGRAD (bit 1); measured
+// on the bench workload: DGRAD +3.5 %, FWD -2 % -> default DGRAD only (2)
+static int g_row = -1;
 
 template <int MODE, int BM, int BN, bool VA, bool VB>
 static void launch(const ConvArgs& a, hipStream_t st) {
@@ -554,13 +611,13 @@ static void launch(const ConvArgs& a, hipStream_t st) {
     const char* e = getenv("MAUV_CONV_BK");
     g_bk = (e && atoi(e) == 32) ? 32 : 16;  // measured: 16 wins (3 vs 2 blocks/CU)
   }
-  if (g_mid < 0) {
-    const char* e = getenv("MAUV_CONV_MIDSTORE");
-    g_mid = e ? atoi(e) : 0;
+  if (g_row < 0) {
+    const char* e = getenv("MAUV_CONV_ROW");
+    g_row = e ? atoi(e) : 2;
   }
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
   if (g_bk == 16) {
-    if (g_mid)
+    if ((MODE == FWD && (g_row & 1)) || (MODE == DGRAD && (g_row & 2)))
       hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, true>), grid, dim3(256), 0, st, a);
     else
       hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, false>), grid, dim3(256), 0, st, a);

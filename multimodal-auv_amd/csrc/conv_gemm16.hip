@@ -92,7 +92,7 @@ __device__ __forceinline__ u32x4 col_frag(const u16* img, int LD, int R0, int s,
   return r;
 }
 
-template <int MODE, int DT, int BM, int BN, bool TAPU, bool MID>
+template <int MODE, int DT, int BM, int BN, bool TAPU>
 __global__ __launch_bounds__(256) void conv_gemm_h16(const ConvArgs16 a) {
   constexpr bool A_COL = (MODE == H_WGRAD);
   constexpr bool B_COL = (MODE != H_FWD);
@@ -341,11 +341,8 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(const ConvArgs16 a) {
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = H16<DT>::mfma(af[mi], bfr[ni], acc[mi][ni]);
-      if constexpr (MID)  // next tile's LDS writes behind the first k-step's MFMAs
-        if (s == 0 && more) store(cur ^ 1);
     }
-    if constexpr (!MID)
-      if (more) store(cur ^ 1);
+    if (more) store(cur ^ 1);
     __syncthreads();
     cur ^= 1;
   }
@@ -473,19 +470,10 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(const ConvArgs16 a) {
   }
 }
 
-static int g_mid16 = -1;  // MAUV_CONV_MIDSTORE (as conv_gemm.hip)
-
 template <int MODE, int DT, int BM, int BN, bool TAPU>
 static void launch16(const ConvArgs16& a, hipStream_t st) {
-  if (g_mid16 < 0) {
-    const char* e = getenv("MAUV_CONV_MIDSTORE");
-    g_mid16 = e ? atoi(e) : 0;
-  }
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == H_WGRAD ? a.G * a.splits : a.G);
-  if (g_mid16)
-    hipLaunchKernelGGL((conv_gemm_h16<MODE, DT, BM, BN, TAPU, true>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_gemm_h16<MODE, DT, BM, BN, TAPU, false>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv_gemm_h16<MODE, DT, BM, BN, TAPU>), grid, dim3(256), 0, st, a);
 }
 
 template <int MODE, int DT, bool TAPU>

@@ -59,35 +59,62 @@ __global__ __launch_bounds__(256) void reparam_sample_kernel(
   }
 }
 
-// One block per output channel o: its P = Cin*RS parameters are the same index set in the
-// KRSC slab layout and in the OIHW parameter layout, so the block
-//   (A) streams the slab rows coalesced in KRSC order, summing split-K partials (and, in
-//       reference mode, the G samples) into an LDS image stored in OIHW order, then
-//   (B) walks OIHW quads (the Philox counter unit) and applies the chain rule:
+// One block per (output channel o, range of CB input channels): that range's parameters are
+// ONE contiguous OIHW interval [(o*Cin + c0)*RS, (o*Cin + c0 + cb)*RS) and, per tap rs, a
+// contiguous KRSC run of cb channels — so the block
+//   (A) streams the slab runs coalesced (KRSC order), summing split-K partials (and, in
+//       reference mode, the G samples) with 4 independent accumulators, into an LDS image in
+//       OIHW order, then
+//   (B) walks the interval's OIHW quads (the Philox counter unit) and applies the chain rule:
 //       dmu += sum,  drho += sum_g d_g * eps_g' * sigmoid(rho).
 // Reference mode (fixed >= 0): one epsilon for every g, so drho += (sum_g d_g) * eps * sig —
-// one LDS pass.  Exact mode: one pass per g.
+// one pass.  Exact mode: one pass per g.
+// input channels per block: 64 for 1x1 (RS = 1), 16 otherwise (<= 16*49 parameters)
+__host__ __device__ inline int rb_cb(int RS) { return RS == 1 ? 64 : 16; }
+
 __global__ __launch_bounds__(256) void reparam_bwd_kernel(
     const float* __restrict__ dw, int splits, long long dw_gs, long long dw_ss,
     const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
     uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS, int cin_pad,
     float* __restrict__ dmu, float* __restrict__ drho, long long fixed) {
-  extern __shared__ float sd[];  // [P] in OIHW-local order (c*RS + rs)
+  __shared__ float sd[16 * 49];   // [cb][RS]
+  __shared__ float red[4][64];
   const int o = blockIdx.x, tid = threadIdx.x;
-  const int P = Cin * RS;
-  const long long numel = (long long)Cout * P;
-  const long long i0 = (long long)o * P;
-  const long long q0 = i0 >> 2, q1 = (i0 + P - 1) >> 2;  // quads touching this channel
+  const int CB = rb_cb(RS);
+  const int c0 = blockIdx.y * CB, cb = min(CB, Cin - c0);
+  const int len = cb * RS;
+  const long long numel = (long long)Cout * Cin * RS;
+  const long long i0 = ((long long)o * Cin + c0) * RS;
+  const long long q0 = i0 >> 2, q1 = (i0 + len - 1) >> 2;  // quads touching the interval
   const int npass = fixed >= 0 ? 1 : G;
+  const int lane = tid & 63, tg = tid >> 6;  // 64 elements x 4 term groups per round
   for (int pass = 0; pass < npass; ++pass) {
-    const int g0 = fixed >= 0 ? 0 : pass, g1 = fixed >= 0 ? G : pass + 1;
-    for (int k = tid; k < P; k += 256) {  // k = rs*Cin + c (KRSC-local, coalesced in c)
-      const int rs = k / Cin, c = k - rs * Cin;
-      const long long src = ((long long)o * RS + rs) * cin_pad + c;
-      float d = 0.f;
-      for (int g = g0; g < g1; ++g)
-        for (int s = 0; s < splits; ++s) d += dw[s * dw_ss + g * dw_gs + src];
-      sd[c * RS + rs] = d;
+    const int g0 = fixed >= 0 ? 0 : pass, ng = fixed >= 0 ? G : 1;
+    const int nt = ng * splits;  // terms per element: t -> (g = g0 + t / splits, s = t % splits)
+    for (int kb = 0; kb < len; kb += 64) {
+      const int k = kb + lane;  // k = rs*cb + cc (coalesced in cc)
+      float d0 = 0.f, d1 = 0.f;
+      if (k < len) {
+        const int rs = k / cb, cc = k - rs * cb;
+        const float* src = dw + ((long long)o * RS + rs) * cin_pad + c0 + cc + g0 * dw_gs;
+        int t = tg;
+        for (; t + 4 < nt; t += 8) {
+          const int ga = t / splits, gb = (t + 4) / splits;
+          d0 += src[(t - ga * splits) * dw_ss + ga * dw_gs];
+          d1 += src[(t + 4 - gb * splits) * dw_ss + gb * dw_gs];
+        }
+        if (t < nt) {
+          const int ga = t / splits;
+          d0 += src[(t - ga * splits) * dw_ss + ga * dw_gs];
+        }
+      }
+      red[tg][lane] = d0 + d1;
+      __syncthreads();
+      if (tg == 0 && k < len) {
+        const int rs = k / cb, cc = k - rs * cb;
+        sd[cc * RS + rs] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+      }
+      __syncthreads();
     }
     __syncthreads();
     const long long esample = fixed >= 0 ? fixed : pass;
@@ -105,7 +132,7 @@ __global__ __launch_bounds__(256) void reparam_bwd_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const long long i = 4 * q + e;
-        if (i < i0 || i >= i0 + P) continue;
+        if (i < i0 || i >= i0 + len) continue;
         const float d = sd[(int)(i - i0)];
         dmu[i] += d;
         drho[i] += d * ep[e] * sigmoidf_(rho[i]);
@@ -236,9 +263,9 @@ MAUV_API int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride,
   const long long nq = (numel + 3) / 4;
   const long long gs = dw_gstride ? dw_gstride : (long long)Cout * RS * dw_cin;
   const long long ss = dw_sstride ? dw_sstride : gs * G;
-  if ((long long)Cin * RS > 16384) { set_error("reparam_bwd: Cin*R*S > 16384"); return kErrArg; }
+  if (RS > 49) { set_error("reparam_bwd: R*S > 49"); return kErrArg; }
   (void)nq;
-  hipLaunchKernelGGL(reparam_bwd_kernel, dim3(Cout), dim3(256), (size_t)Cin * RS * 4, stream, dw, splits,
+  hipLaunchKernelGGL(reparam_bwd_kernel, dim3(Cout, ceil_div(Cin, rb_cb(RS))), dim3(256), 0, stream, dw, splits,
                      gs, ss, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS, dw_cin, dmu, drho,
                      fixed_sample >= 0 ? (long long)(fixed_sample - (long long)sample0) : -1LL);
   return check_launch("reparam_bwd");
