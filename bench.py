@@ -35,6 +35,10 @@ for _p in (REPO, os.path.join(REPO, "multimodal-auv_amd")):
 METRIC = "triplets/sec training + MC-samples/sec inference, 7-class BNN, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md: f32-in MFMA = vector peak (spec)
 BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: dense bf16/f16 MFMA (no sparsity)
+# fp32 GEMM arithmetic of the convs (include/mauv.h mauv_set_f32_math): "split" issues six
+# bf16 MFMA plane products per fp32 product, "exact" one f32 MFMA
+F32_PEAK_TF = {"split": BF16_MFMA_PEAK_TF / 6, "split1": BF16_MFMA_PEAK_TF / 6,
+               "split3": BF16_MFMA_PEAK_TF / 3, "exact": FP32_MFMA_PEAK_TF}
 
 
 def synthetic_batch(B, S_opt, S_son, device, seed):
@@ -155,6 +159,8 @@ def main():
     ap.add_argument("--bf16-steps", type=int, default=5)
     ap.add_argument("--infer-fp32", action="store_true",
                     help="also time MC inference with fp32 trunks (default: autocast f16 only)")
+    ap.add_argument("--exact-steps", type=int, default=2,
+                    help="also time the fp32 step with exact f32 MFMA products (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -207,7 +213,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     triplets_s = args.batch * world * args.steps / dt
-    roof = None if args.no_roofline else roofline_step(step)
+    from mauv import ops
+    f32_math = ops.f32_math()
+    roof = None
+    if not args.no_roofline and args.dtype == "fp32":
+        roof = roofline_step(step, peak=round(F32_PEAK_TF[f32_math], 1),
+                             kernel=f"conv_gemm_f32 [{f32_math}] (implicit-GEMM fwd+dgrad+wgrad, "
+                                    "all launches of one step)")
+        roof["f32_math"] = f32_math
+        roof["frac_of_f32_mfma_peak"] = round(roof["achieved"] / FP32_MFMA_PEAK_TF, 4)
 
     def timed(fn, steps):
         barrier()
@@ -223,6 +237,17 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             t = tt.item()
         return t
+
+    exact = None
+    if args.dtype == "fp32" and args.exact_steps > 0 and f32_math != "exact":
+        # the same step with every fp32 product on v_mfma_f32_32x32x2_f32 (reference point)
+        ops.set_f32_math("exact")
+        step()
+        te = timed(step, args.exact_steps)
+        exact = {"value": round(args.batch * world * args.exact_steps / te, 3),
+                 "unit": "triplets/s", "ms_per_step": round(te / args.exact_steps * 1e3, 2),
+                 "steps": args.exact_steps, "f32_math": "exact (v_mfma_f32_32x32x2_f32)"}
+        ops.set_f32_math(f32_math)
 
     bf16 = None
     if not args.no_bf16:
@@ -280,6 +305,8 @@ def main():
                                    f"{args.optical}px + bathy/SSS {args.sonar}px",
                        "global_batch": args.batch * world, "num_mc": args.num_mc,
                        "parallelism": f"dp{world}"},
+            "f32_math": f32_math if args.dtype == "fp32" else None,
+            "fp32_exact_mfma": exact,
             "inference": infer, "bf16_train": bf16, "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -75,6 +75,16 @@ int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strides, const
                                const float* x_shift, int x_relu, const float* dy, float* ws,
                                int splits, int G, int B, int H, int W, int Cin, int Cout, int R,
                                int S, int stride, int pad, hipStream_t stream);
+/* Arithmetic of the three fp32 conv entry points above (process-wide; initial value from
+ * MAUV_F32_MATH=split|split3|exact):
+ *   6 split (default): every fp32 operand is split exactly into three bf16 planes
+ *     x = h + m + l and the six plane products h*h, h*m, m*h, h*l, l*h, m*m run on
+ *     v_mfma_f32_32x32x16_bf16 with fp32 accumulation (h*h in its own accumulator); the
+ *     dropped terms are <= 2^-24 |a*b| — fp32-grade results at 2.67x the f32-MFMA rate;
+ *   3 split3: planes (h, m), products h*h, h*m, m*h (~2^-16 |a*b|; opt-in);
+ *   0 exact: v_mfma_f32_32x32x2_f32 (an fmaf chain).
+ * mode -1 queries.  Returns the previous mode, or < 0 for an invalid mode. */
+int mauv_set_f32_math(int mode);
 
 /* ---- 16-bit implicit-GEMM convs (conv_gemm16.hip) -----------------------------------------
  * Same three GEMM views on v_mfma_f32_32x32x16_{bf16,f16}: dtype 0 = bf16 (BASELINE configs[2]

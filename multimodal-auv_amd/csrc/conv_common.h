@@ -1,0 +1,209 @@
+// Shared pieces of the fp32 implicit-GEMM convs (conv_gemm.hip: exact f32 MFMA and the
+// register-staged split path; conv_split.hip: the pipelined split-fp32 kernels): the argument
+// block, the BN-on-load transform and the fused epilogue (bias, residual addend / accumulate,
+// BN statistics partials of the forward, BN-backward partials of the data gradient).
+#pragma once
+#include "h16.h"
+
+namespace mauv {
+
+enum { FWD = 0, DGRAD = 1, WGRAD = 2 };
+
+struct ConvArgs {
+  int B, H, W, Cin, Ho, Wo, Cout, R, S, stride, pad;
+  long long xs_g, xs_b, xs_h, xs_w, xs_c;  // x element strides
+  const float* x;
+  const float* w;
+  long long ws_g;
+  const float* dy;  // [G][B*Ho*Wo][Cout]
+  float* out;
+  long long out_sg;
+  const float* bias;
+  long long bias_sg;
+  const float* addend;
+  int accumulate;
+  int G, splits, kchunk;
+  int M, N, K;  // GEMM dims (per group)
+  // DGRAD output-parity class (sub-pixel decomposition): this launch computes dx for the
+  // input pixels (stride*i + ph, stride*j + pw) only, whose contributing taps are
+  // r = r0 + stride*tr (tr < nr), s = s0 + stride*ts (ts < ns) — no structurally-zero MACs.
+  int ph, pw, Hc, Wc, r0, s0, nr, ns;
+  // optional per-(group, channel) transform of x on load: x' = [relu](x*xsc + xsh) — the
+  // pending BatchNorm(+ReLU) of the producing layer, applied lazily so that layer's
+  // normalised activation is never written to HBM (FWD A-loader, WGRAD B-loader)
+  const float* xsc;
+  const float* xsh;
+  int xrelu;
+  // FWD epilogue BN statistics partials [G][st_nblk][N] (+ counts [G][st_nblk])
+  float *st_mean, *st_m2, *st_cnt;
+  int st_nblk, st_base;
+  // DGRAD epilogue BN-backward partials [G][bp_nblk][N]: sum dz, sum dz*xhat
+  const float *bp_y, *bp_out, *bp_sc, *bp_sh, *bp_mean, *bp_invstd;
+  int bp_relu;
+  float *bp_p1, *bp_p2;
+  int bp_nblk, bp_base;
+  // WGRAD pixel -> (b, oh, ow) by multiply-shift division (conv_split.hip): n / d =
+  // (n * mg) >> sh for n < 2^31 (mauv::magic_div)
+  unsigned long long mg_hw, mg_w;
+  int sh_hw, sh_w;
+};
+
+// q = n / d as (n * m) >> s for every n < 2^31: s = 31 + ceil(log2 d), m = floor(2^s / d) + 1
+// (m*d - 2^s lies in (0, d], so the error term n*(m*d - 2^s)/(d*2^s) < 1/d never crosses an
+// integer).
+inline void magic_div(unsigned d, unsigned long long& m, int& s) {
+  int l = 0;
+  while ((1ull << l) < d) ++l;
+  s = 31 + l;
+  m = (unsigned long long)(((unsigned __int128)1 << s) / d) + 1;
+}
+
+// Launch the pipelined split-fp32 kernel (conv_split.hip) for an fp32 conv; false when the
+// problem is outside its vector paths (the caller then runs conv_gemm.hip's kernels).
+bool conv_split_launch(int mode, const ConvArgs& a, int oneacc, hipStream_t st);
+
+__device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int relu) {
+  v = v * sc + sh;
+  if (relu) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+  }
+  return v;
+}
+
+
+// Epilogue of one BM x BN block tile: acc[mi][ni] holds the fp32 32x32 accumulator tiles of
+// this wave (the C/D layout of both v_mfma_f32_32x32x2_f32 and v_mfma_f32_32x32x16_bf16:
+// lane l = column l&31, register r = row (r&3) + 8(r>>2) + 4(l>>5)).
+template <int MODE, int BM, int BN, int MI, int NI>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx16 (&acc)[MI][NI],
+                                              float* smem, int tid, int m0, int n0, int g,
+                                              int sp) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  float* outg;
+  if constexpr (MODE == WGRAD)
+    outg = a.out + ((long long)sp * a.G + g) * ((long long)a.M * a.N);
+  else
+    outg = a.out + (long long)g * a.out_sg;
+  // Fused BatchNorm reductions (per block tile, per column = channel), written as per-m-tile
+  // partials that bn.hip's finalize kernels merge — the standalone statistics passes over y
+  // (forward) and over dx (backward) disappear:
+  //   FWD   + st_mean: tile-local (count, mean, M2) of y (two register passes, Welford-exact)
+  //   DGRAD + bp_p1  : sum dz and sum dz*xhat of the BN whose output gradient this dx is
+  //                    (dz = dx * relu-mask; mask/xhat from that BN's y and statistics)
+  const bool fst = (MODE == FWD) && a.st_mean;
+  const bool bst = (MODE == DGRAD) && a.bp_p1;
+  float s1[NI], s2[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) { s1[ni] = 0.f; s2[ni] = 0.f; }
+  const int nvalid = min(BM, a.M - m0);
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int col = n0 + wn * WN + ni * 32 + li;
+      if (col >= a.N) continue;
+      float bias = 0.f;
+      if constexpr (MODE == FWD)
+        if (a.bias) bias = a.bias[(long long)g * a.bias_sg + col];
+      float bmu = 0.f, bis = 0.f, bsc = 0.f, bsh = 0.f;
+      if constexpr (MODE == DGRAD) {
+        if (bst) {
+          bmu = a.bp_mean[g * a.N + col];
+          bis = a.bp_invstd[g * a.N + col];
+          if (!a.bp_out) { bsc = a.bp_sc[g * a.N + col]; bsh = a.bp_sh[g * a.N + col]; }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row >= a.M) continue;
+        long long orow = row;
+        if constexpr (MODE == DGRAD) {  // class-local row -> input pixel
+          if (a.stride != 1) {
+            const int HW = a.Hc * a.Wc, b = row / HW, rem = row - b * HW;
+            const int i = rem / a.Wc, jj = rem - i * a.Wc;
+            orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
+          }
+        }
+        const long long o = orow * a.N + col;
+        float v = acc[mi][ni][r] + bias;
+        if constexpr (MODE == DGRAD) {
+          if (a.addend) v += a.addend[(long long)g * a.out_sg + o];
+          if (a.accumulate) v += outg[o];
+          if (bst) {
+            const long long go = (long long)g * a.out_sg + o;
+            const float yv = a.bp_y[go];
+            const float pre = a.bp_out ? a.bp_out[go] : yv * bsc + bsh;
+            const float dz = (!a.bp_relu || pre > 0.f) ? v : 0.f;
+            s1[ni] += dz;
+            s2[ni] += dz * (yv - bmu) * bis;
+          }
+        }
+        if constexpr (MODE == FWD) s1[ni] += v;
+        outg[o] = v;
+      }
+    }
+  if (fst || bst) {
+    float* red = smem;  // LDS is free: the main loop ended with a barrier
+    const int tcol = wn * WN + li;  // + ni*32
+    // column totals of s1 over the block tile: lane halves, then the two wm waves
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) s1[ni] += __shfl_xor(s1[ni], 32, 64);
+    if (lh == 0) {
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) red[wm * BN + tcol + ni * 32] = s1[ni];
+    }
+    __syncthreads();
+    if (fst) {
+      // pass 2: M2 around the tile mean
+      float mean[NI];
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+        mean[ni] = (red[tcol + ni * 32] + red[BN + tcol + ni * 32]) / (float)nvalid;
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) s2[ni] = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          const int col = n0 + wn * WN + ni * 32 + li;
+          const float bias = (a.bias && col < a.N) ? a.bias[(long long)g * a.bias_sg + col] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (row < a.M) {
+              const float d = acc[mi][ni][r] + bias - mean[ni];
+              s2[ni] += d * d;
+            }
+          }
+        }
+    }
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) s2[ni] += __shfl_xor(s2[ni], 32, 64);
+    if (lh == 0) {
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) red[2 * BN + wm * BN + tcol + ni * 32] = s2[ni];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N) {
+      const float t1 = red[tid] + red[BN + tid], t2 = red[2 * BN + tid] + red[3 * BN + tid];
+      const int mt = m0 / BM;
+      if (fst) {
+        const long long so = ((long long)g * a.st_nblk + a.st_base + mt) * a.N + n0 + tid;
+        a.st_mean[so] = t1 / (float)nvalid;
+        a.st_m2[so] = t2;
+        if (n0 + tid == 0) a.st_cnt[(long long)g * a.st_nblk + a.st_base + mt] = (float)nvalid;
+      } else {
+        const long long so = ((long long)g * a.bp_nblk + a.bp_base + mt) * a.N + n0 + tid;
+        a.bp_p1[so] = t1;
+        a.bp_p2[so] = t2;
+      }
+    }
+  }
+}
+
+}  // namespace mauv

@@ -20,57 +20,29 @@
 // Tiles: 256 threads = 4 waves (2x2), block tile BM x BN x 16, double-buffered LDS stored
 // k-major ([k][row], rows contiguous) so each MFMA operand is one conflict-free ds_read_b32;
 // MFMA v_mfma_f32_32x32x2_f32 (exact fp32, fmaf-chain numerics).
+//
+// Arithmetic of the fp32 products (mauv_set_f32_math; template parameter SPL):
+//   SPL = 0  exact  — v_mfma_f32_32x32x2_f32 (f32 MFMA = the f32 vector rate, 157 TF/s);
+//   SPL = 6  split  (default) — every staged fp32 operand element is written to LDS as three
+//            bf16 planes, x = h + m + l exactly (h16.h split_bf16), and each 32x32x16 k-step
+//            issues the six plane products h.h | h.m, m.h, h.l, l.h, m.m on
+//            v_mfma_f32_32x32x16_bf16 (products exact in fp32, fp32 accumulation).  The
+//            dropped m.l, l.m, l.l total <= 2^-24 |a.b| (one fp32 rounding), and h.h
+//            accumulates in its own register tile so the large terms see one rounding per
+//            k as in an fmaf chain: fp32-grade results at 16/6 = 2.67x the f32 MFMA rate;
+//   SPL = 3  split3 (opt-in) — planes (h, m), products h.h | h.m, m.h: |error| <= ~2^-16
+//            |a.b| (finer than TF32's 2^-11), 5.3x the f32 MFMA rate.
+// Split tiles use the 16-bit kernel's LDS images (conv_gemm16.hip): k-contiguous operands
+// (FWD A/B, DGRAD A) as row images [rows][BKT+8] read with one ds_read_b128 per fragment,
+// k-strided operands (DGRAD B, WGRAD A/B) as col images [BKT][rows+32] read with two
+// ds_read_b64_tr_b16.  The accumulator layout of the two MFMA shapes is the same, so the
+// epilogues are shared.
 #include <stdlib.h>
+#include <string.h>
 
-#include "mauv_common.h"
+#include "conv_common.h"
 
 namespace mauv {
-
-enum { FWD = 0, DGRAD = 1, WGRAD = 2 };
-
-struct ConvArgs {
-  int B, H, W, Cin, Ho, Wo, Cout, R, S, stride, pad;
-  long long xs_g, xs_b, xs_h, xs_w, xs_c;  // x element strides
-  const float* x;
-  const float* w;
-  long long ws_g;
-  const float* dy;  // [G][B*Ho*Wo][Cout]
-  float* out;
-  long long out_sg;
-  const float* bias;
-  long long bias_sg;
-  const float* addend;
-  int accumulate;
-  int G, splits, kchunk;
-  int M, N, K;  // GEMM dims (per group)
-  // DGRAD output-parity class (sub-pixel decomposition): this launch computes dx for the
-  // input pixels (stride*i + ph, stride*j + pw) only, whose contributing taps are
-  // r = r0 + stride*tr (tr < nr), s = s0 + stride*ts (ts < ns) — no structurally-zero MACs.
-  int ph, pw, Hc, Wc, r0, s0, nr, ns;
-  // optional per-(group, channel) transform of x on load: x' = [relu](x*xsc + xsh) — the
-  // pending BatchNorm(+ReLU) of the producing layer, applied lazily so that layer's
-  // normalised activation is never written to HBM (FWD A-loader, WGRAD B-loader)
-  const float* xsc;
-  const float* xsh;
-  int xrelu;
-  // FWD epilogue BN statistics partials [G][st_nblk][N] (+ counts [G][st_nblk])
-  float *st_mean, *st_m2, *st_cnt;
-  int st_nblk, st_base;
-  // DGRAD epilogue BN-backward partials [G][bp_nblk][N]: sum dz, sum dz*xhat
-  const float *bp_y, *bp_out, *bp_sc, *bp_sh, *bp_mean, *bp_invstd;
-  int bp_relu;
-  float *bp_p1, *bp_p2;
-  int bp_nblk, bp_base;
-};
-
-__device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int relu) {
-  v = v * sc + sh;
-  if (relu) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
-  }
-  return v;
-}
 
 constexpr int BK = 16;  // host-side alignment granule (both tile depths are multiples)
 constexpr int PAD = 4;
@@ -80,8 +52,11 @@ constexpr int PAD = 4;
 // tile with ds_read_b128s up front (k order permuted: instruction kk of lane half lh takes
 // k = (BKT/2)*lh + kk, the same for A and B); k-strided operands keep the k-major image
 // [BKT][rows+4] read with one ds_read_b32 per MFMA.
-template <int MODE, int BM, int BN, int BKT, bool VA, bool VB, bool ROW>
-__global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
+// split tiles: 2 accumulator sets (128 AGPRs at 128x128) — held to <= 256 registers so two
+// blocks (2 waves per SIMD) share a CU, as their LDS (<= 72 KB per block) allows
+template <int MODE, int BM, int BN, int BKT, bool VA, bool VB, bool ROW, int SPL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SPL == 6 || SPL == 3 ? 2 : 1)))
+void conv_gemm_f32(const ConvArgs a) {
   constexpr int KQ = BKT / 4;  // float4 per k-row of a k-contiguous tile row
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 32, NI = WN / 32;
   constexpr int NVA = BM * BKT / 4 / 256, NVB = BN * BKT / 4 / 256;
@@ -89,7 +64,16 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
   constexpr int RLDF = BKT + 4;
   constexpr int A_SZ = RA ? BM * RLDF : BKT * (BM + PAD);
   constexpr int B_SZ = RB ? BN * RLDF : BKT * (BN + PAD);
-  __shared__ __attribute__((aligned(16))) float smem[2 * (A_SZ + B_SZ)];
+  // SPL > 0: NPL bf16 planes per operand (sizes in 16-bit words)
+  constexpr int NPL = SPL == 3 ? 2 : 3;
+  constexpr bool SA_COL = (MODE == WGRAD), SB_COL = (MODE != FWD);
+  constexpr int SRLD = BKT + 8;
+  constexpr int SA_PL = SA_COL ? BKT * (BM + 32) : BM * SRLD;
+  constexpr int SB_PL = SB_COL ? BKT * (BN + 32) : BN * SRLD;
+  constexpr int S_STG = NPL * (SA_PL + SB_PL);
+  constexpr int STG_F = SPL ? S_STG / 2 : A_SZ + B_SZ;  // floats per pipeline stage
+  static_assert(2 * STG_F >= 4 * BN, "epilogue reduction scratch exceeds LDS");
+  __shared__ __attribute__((aligned(16))) float smem[2 * STG_F];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -357,6 +341,31 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
   };
 
   auto store_tiles = [&](int buf) {
+    if constexpr (SPL != 0) {  // split planes (h16.h split_bf16) into the 16-bit images
+      u16* As = (u16*)smem + buf * S_STG;
+      u16* Bs = As + NPL * SA_PL;
+#pragma unroll
+      for (int j = 0; j < NVA; ++j) {
+        const int idx = tid + 256 * j;
+        const int off = SA_COL ? (idx / (BM / 4)) * (BM + 32) + 4 * (idx % (BM / 4))
+                               : (idx / KQ) * SRLD + 4 * (idx % KQ);
+        uint2 pl[3];
+        split_bf16<NPL>(ra[j], pl);
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) *(uint2*)(As + p * SA_PL + off) = pl[p];
+      }
+#pragma unroll
+      for (int j = 0; j < NVB; ++j) {
+        const int idx = tid + 256 * j;
+        const int off = SB_COL ? (idx / (BN / 4)) * (BN + 32) + 4 * (idx % (BN / 4))
+                               : (idx / KQ) * SRLD + 4 * (idx % KQ);
+        uint2 pl[3];
+        split_bf16<NPL>(rb[j], pl);
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) *(uint2*)(Bs + p * SB_PL + off) = pl[p];
+      }
+      return;
+    }
     float* Ab = smem + buf * (A_SZ + B_SZ);
     float* Bb = Ab + A_SZ;
 #pragma unroll
@@ -392,13 +401,13 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
     }
   };
 
-  floatx16 acc[MI][NI];
+  floatx16 acc[MI][NI], acl[MI][NI];  // acl: the split modes' small plane products
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+      for (int r = 0; r < 16; ++r) { acc[mi][ni][r] = 0.f; acl[mi][ni][r] = 0.f; }
 
   const int ntiles = (kend - kbeg + BKT - 1) / BKT;
   if (ntiles > 0) {
@@ -416,7 +425,55 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
     }
     const float* Ab = smem + cur * (A_SZ + B_SZ);
     const float* Bb = Ab + A_SZ;
-    if constexpr (RA || RB) {
+    if constexpr (SPL != 0) {
+      const u16* As = (const u16*)smem + cur * S_STG;
+      const u16* Bs = As + NPL * SA_PL;
+#pragma unroll
+      for (int s = 0; s < BKT / 16; ++s) {
+        u32x4 af[NPL][MI], bq[NPL][NI];
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) {
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi) {
+            if constexpr (SA_COL)
+              af[p][mi] = col_frag(As + p * SA_PL, BM + 32, wm * WM + mi * 32, s, lane);
+            else
+              af[p][mi] = row_frag_ld<SRLD>(As + p * SA_PL, wm * WM + mi * 32, s, li, lh);
+          }
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) {
+            if constexpr (SB_COL)
+              bq[p][ni] = col_frag(Bs + p * SB_PL, BN + 32, wn * WN + ni * 32, s, lane);
+            else
+              bq[p][ni] = row_frag_ld<SRLD>(Bs + p * SB_PL, wn * WN + ni * 32, s, li, lh);
+          }
+        }
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) {
+            if constexpr (SPL == 5) {  // one accumulator for all six products
+              floatx16 c = acc[mi][ni];
+              c = H16<DT_BF16>::mfma(af[0][mi], bq[2][ni], c);
+              c = H16<DT_BF16>::mfma(af[2][mi], bq[0][ni], c);
+              c = H16<DT_BF16>::mfma(af[1][mi], bq[1][ni], c);
+              c = H16<DT_BF16>::mfma(af[0][mi], bq[1][ni], c);
+              c = H16<DT_BF16>::mfma(af[1][mi], bq[0][ni], c);
+              acc[mi][ni] = H16<DT_BF16>::mfma(af[0][mi], bq[0][ni], c);
+              continue;
+            }
+            floatx16 c = acl[mi][ni];
+            if constexpr (SPL == 6) {
+              c = H16<DT_BF16>::mfma(af[0][mi], bq[2][ni], c);
+              c = H16<DT_BF16>::mfma(af[2][mi], bq[0][ni], c);
+              c = H16<DT_BF16>::mfma(af[1][mi], bq[1][ni], c);
+            }
+            c = H16<DT_BF16>::mfma(af[0][mi], bq[1][ni], c);
+            acl[mi][ni] = H16<DT_BF16>::mfma(af[1][mi], bq[0][ni], c);
+            acc[mi][ni] = H16<DT_BF16>::mfma(af[0][mi], bq[0][ni], acc[mi][ni]);
+          }
+      }
+    } else if constexpr (RA || RB) {
       constexpr int KH = BKT / 2;
       float a8[MI][KH], b8[NI][KH];
 #pragma unroll
@@ -477,133 +534,30 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(const ConvArgs a) {
   }
 
   // ---------------- epilogue ----------------
-  float* outg;
-  if constexpr (MODE == WGRAD)
-    outg = a.out + ((long long)sp * a.G + g) * ((long long)a.M * a.N);
-  else
-    outg = a.out + (long long)g * a.out_sg;
-  // Fused BatchNorm reductions (per block tile, per column = channel), written as per-m-tile
-  // partials that bn.hip's finalize kernels merge — the standalone statistics passes over y
-  // (forward) and over dx (backward) disappear:
-  //   FWD   + st_mean: tile-local (count, mean, M2) of y (two register passes, Welford-exact)
-  //   DGRAD + bp_p1  : sum dz and sum dz*xhat of the BN whose output gradient this dx is
-  //                    (dz = dx * relu-mask; mask/xhat from that BN's y and statistics)
-  const bool fst = (MODE == FWD) && a.st_mean;
-  const bool bst = (MODE == DGRAD) && a.bp_p1;
-  float s1[NI], s2[NI];
+  if constexpr (SPL == 6 || SPL == 3) {
 #pragma unroll
-  for (int ni = 0; ni < NI; ++ni) { s1[ni] = 0.f; s2[ni] = 0.f; }
-  const int nvalid = min(BM, a.M - m0);
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int col = n0 + wn * WN + ni * 32 + li;
-      if (col >= a.N) continue;
-      float bias = 0.f;
-      if constexpr (MODE == FWD)
-        if (a.bias) bias = a.bias[(long long)g * a.bias_sg + col];
-      float bmu = 0.f, bis = 0.f, bsc = 0.f, bsh = 0.f;
-      if constexpr (MODE == DGRAD) {
-        if (bst) {
-          bmu = a.bp_mean[g * a.N + col];
-          bis = a.bp_invstd[g * a.N + col];
-          if (!a.bp_out) { bsc = a.bp_sc[g * a.N + col]; bsh = a.bp_sh[g * a.N + col]; }
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row >= a.M) continue;
-        long long orow = row;
-        if constexpr (MODE == DGRAD) {  // class-local row -> input pixel
-          if (a.stride != 1) {
-            const int HW = a.Hc * a.Wc, b = row / HW, rem = row - b * HW;
-            const int i = rem / a.Wc, jj = rem - i * a.Wc;
-            orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
-          }
-        }
-        const long long o = orow * a.N + col;
-        float v = acc[mi][ni][r] + bias;
-        if constexpr (MODE == DGRAD) {
-          if (a.addend) v += a.addend[(long long)g * a.out_sg + o];
-          if (a.accumulate) v += outg[o];
-          if (bst) {
-            const long long go = (long long)g * a.out_sg + o;
-            const float yv = a.bp_y[go];
-            const float pre = a.bp_out ? a.bp_out[go] : yv * bsc + bsh;
-            const float dz = (!a.bp_relu || pre > 0.f) ? v : 0.f;
-            s1[ni] += dz;
-            s2[ni] += dz * (yv - bmu) * bis;
-          }
-        }
-        if constexpr (MODE == FWD) s1[ni] += v;
-        outg[o] = v;
-      }
-    }
-  if (fst || bst) {
-    float* red = smem;  // LDS is free: the main loop ended with a barrier
-    const int tcol = wn * WN + li;  // + ni*32
-    // column totals of s1 over the block tile: lane halves, then the two wm waves
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) s1[ni] += __shfl_xor(s1[ni], 32, 64);
-    if (lh == 0) {
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) red[wm * BN + tcol + ni * 32] = s1[ni];
-    }
-    __syncthreads();
-    if (fst) {
-      // pass 2: M2 around the tile mean
-      float mean[NI];
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
-        mean[ni] = (red[tcol + ni * 32] + red[BN + tcol + ni * 32]) / (float)nvalid;
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) s2[ni] = 0.f;
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-          const int col = n0 + wn * WN + ni * 32 + li;
-          const float bias = (a.bias && col < a.N) ? a.bias[(long long)g * a.bias_sg + col] : 0.f;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            if (row < a.M) {
-              const float d = acc[mi][ni][r] + bias - mean[ni];
-              s2[ni] += d * d;
-            }
-          }
-        }
-    }
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) s2[ni] += __shfl_xor(s2[ni], 32, 64);
-    if (lh == 0) {
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) red[2 * BN + wm * BN + tcol + ni * 32] = s2[ni];
-    }
-    __syncthreads();
-    if (tid < BN && n0 + tid < a.N) {
-      const float t1 = red[tid] + red[BN + tid], t2 = red[2 * BN + tid] + red[3 * BN + tid];
-      const int mt = m0 / BM;
-      if (fst) {
-        const long long so = ((long long)g * a.st_nblk + a.st_base + mt) * a.N + n0 + tid;
-        a.st_mean[so] = t1 / (float)nvalid;
-        a.st_m2[so] = t2;
-        if (n0 + tid == 0) a.st_cnt[(long long)g * a.st_nblk + a.st_base + mt] = (float)nvalid;
-      } else {
-        const long long so = ((long long)g * a.bp_nblk + a.bp_base + mt) * a.N + n0 + tid;
-        a.bp_p1[so] = t1;
-        a.bp_p2[so] = t2;
-      }
-    }
+      for (int ni = 0; ni < NI; ++ni) acc[mi][ni] += acl[mi][ni];
   }
+  conv_epilogue<MODE, BM, BN>(a, acc, smem, tid, m0, n0, g, sp);
 }
 
 static int g_bk = 0;  // tile depth: 16 or 32 (MAUV_CONV_BK; default 16)
 // MAUV_CONV_ROW: row images + b128 operand reads for FWD (bit 0) / DGRAD (bit 1); measured
 // on the bench workload: DGRAD +3.5 %, FWD -2 % -> default DGRAD only (2)
 static int g_row = -1;
+
+// fp32 product arithmetic (file header): 6 = split (default), 3 = split3, 0 = exact.
+// Initial value from MAUV_F32_MATH=split|split3|exact; mauv_set_f32_math changes it.
+static int g_f32_math = -1;
+static int f32_math() {
+  if (g_f32_math < 0) {
+    const char* e = getenv("MAUV_F32_MATH");
+    g_f32_math = !e ? 6 : !strcmp(e, "exact") ? 0 : !strcmp(e, "split3") ? 3 : !strcmp(e, "split1") ? 5 : 6;
+  }
+  return g_f32_math;
+}
 
 template <int MODE, int BM, int BN, bool VA, bool VB>
 static void launch(const ConvArgs& a, hipStream_t st) {
@@ -616,13 +570,20 @@ static void launch(const ConvArgs& a, hipStream_t st) {
     g_row = e ? atoi(e) : 2;
   }
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
-  if (g_bk == 16) {
+  const int fm = f32_math();
+  if (fm == 6) {
+    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, false, 6>), grid, dim3(256), 0, st, a);
+  } else if (fm == 5) {
+    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, false, 5>), grid, dim3(256), 0, st, a);
+  } else if (fm == 3) {
+    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, false, 3>), grid, dim3(256), 0, st, a);
+  } else if (g_bk == 16) {
     if ((MODE == FWD && (g_row & 1)) || (MODE == DGRAD && (g_row & 2)))
-      hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, true>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, true, 0>), grid, dim3(256), 0, st, a);
     else
-      hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, false>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, false, 0>), grid, dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 32, VA, VB, false>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 32, VA, VB, false, 0>), grid, dim3(256), 0, st, a);
   }
 }
 
@@ -692,6 +653,8 @@ MAUV_API int mauv_conv2d_fwd_f32(const float* x, const long long* x_strides,
                   (a.xs_b % 4 == 0) && (a.xs_g % 4 == 0);
   const bool vb = (a.K % 4 == 0);
   if (x_scale && !(va && vb)) { set_error("conv2d_fwd: x transform needs the vector path"); return kErrArg; }
+  const int fm = f32_math();
+  if ((fm == 6 || fm == 5) && conv_split_launch(FWD, a, fm == 5, stream)) return check_launch("conv2d_fwd");
   if (va && vb) launch_tiles<FWD, true, true>(a, stream);
   else if (vb) launch_tiles<FWD, false, true>(a, stream);
   else launch_tiles<FWD, false, false>(a, stream);
@@ -730,12 +693,26 @@ MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx
       a.M = B * a.Hc * a.Wc;
       a.K = a.nr * a.ns * Cout;  // 0 -> the class only receives the addend / zeros
       if (a.M <= 0) continue;
-      if (va && vb) launch_tiles<DGRAD, true, true>(a, stream);
+      const int fm = f32_math();
+      if ((fm == 6 || fm == 5) && conv_split_launch(DGRAD, a, fm == 5, stream)) {}
+      else if (va && vb) launch_tiles<DGRAD, true, true>(a, stream);
       else if (vb) launch_tiles<DGRAD, false, true>(a, stream);
       else launch_tiles<DGRAD, false, false>(a, stream);
       a.bp_base += stat_blocks(a.M, a.N, G);
     }
   return check_launch("conv2d_bwd_data");
+}
+
+// Arithmetic of the fp32 convs (file header): 0 exact, 6 split (default), 3 split3; -1 only
+// queries.  Returns the previous mode.
+MAUV_API int mauv_set_f32_math(int mode) {
+  const int prev = f32_math();
+  if (mode == 0 || mode == 3 || mode == 5 || mode == 6) g_f32_math = mode;
+  else if (mode != -1) {
+    set_error("set_f32_math: mode must be 0 (exact), 6 (split), 3 (split3) or -1 (query)");
+    return kErrArg;
+  }
+  return prev;
 }
 
 // Number of per-m-tile BN statistic partials the fused epilogues write (host sizing helpers).
@@ -783,6 +760,8 @@ MAUV_API int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strid
   const bool vb = (Cin % 4 == 0) && a.xs_c == 1 && (a.xs_w % 4 == 0) && (a.xs_h % 4 == 0) &&
                   (a.xs_b % 4 == 0) && (a.xs_g % 4 == 0);
   if (x_scale && !(va && vb)) { set_error("conv2d_bwd_weight: x transform needs the vector path"); return kErrArg; }
+  const int fm = f32_math();
+  if ((fm == 6 || fm == 5) && conv_split_launch(WGRAD, a, fm == 5, stream)) return check_launch("conv2d_bwd_weight");
   if (va && vb) launch_tiles<WGRAD, true, true>(a, stream);
   else if (va) launch_tiles<WGRAD, true, false>(a, stream);
   else launch_tiles<WGRAD, false, false>(a, stream);

@@ -78,19 +78,7 @@ __device__ __forceinline__ u32x4 bn_chunk(u32x4 v, const float* sc, const float*
 __device__ __forceinline__ u32x4 row_frag(const u16* img, int R0, int s, int li, int lh) {
   return *(const u32x4*)(img + (R0 + li) * RLD + 16 * s + 8 * lh);
 }
-// ... and from a col image with leading dimension LD (two transposed reads)
-__device__ __forceinline__ u32x4 col_frag(const u16* img, int LD, int R0, int s, int lane) {
-  const int gq = (lane >> 4) & 3, i = lane & 15, q = i >> 2, p = i & 3, h = lane >> 5;
-  const int col = R0 + 16 * (gq & 1) + 4 * p;
-  const int kr = 16 * s + 8 * h + q;
-  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + kr * LD + col));
-  const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (kr + 4) * LD + col));
-  const uint2 u0 = __builtin_bit_cast(uint2, t0), u1 = __builtin_bit_cast(uint2, t1);
-  u32x4 r;
-  r[0] = u0.x; r[1] = u0.y; r[2] = u1.x; r[3] = u1.y;
-  return r;
-}
+// ... and from a col image with leading dimension LD: col_frag (h16.h)
 
 template <int MODE, int DT, int BM, int BN, bool TAPU>
 __global__ __launch_bounds__(256) void conv_gemm_h16(const ConvArgs16 a) {

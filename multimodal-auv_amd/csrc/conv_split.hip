@@ -1,0 +1,376 @@
+// Pipelined split-fp32 implicit-GEMM convolution: the default arithmetic of every fp32 conv of
+// the three ResNet-50 trunks (models/base_models.py:15-18, models/model_utils.py:57-61) and of
+// the fusion head's linears, forward / data gradient / weight gradient, on the vector paths
+// (all convs but the 1- and 3-channel stems, which stay on conv_gemm.hip).
+//
+// Arithmetic (conv_gemm.hip header, include/mauv.h mauv_set_f32_math): each fp32 operand
+// element is split exactly into bf16 planes x = h + m + l and the product a.b is accumulated in
+// fp32 from h.h, h.m, m.h, h.l, l.h, m.m on v_mfma_f32_32x32x16_bf16 (dropped terms <= 2^-24
+// |a.b|).  With the MFMAs 2.67x cheaper than f32 MFMA, the staging becomes the bottleneck of a
+// load -> wait -> split -> LDS -> barrier loop; this kernel restructures it:
+//  * two tiles in flight: stage t issues the global loads of tile t+2, runs the MFMAs of tile t
+//    from one LDS buffer and splits + writes tile t+1 (loaded a stage earlier) into the other —
+//    one branch-free basic block per stage, so the split VALU and ds_writes interleave with the
+//    MFMAs and HBM latency hides behind a whole stage;
+//  * raw buffer loads: 32-bit offsets = per-thread constant + tile-uniform scalar; an offset past
+//    the descriptor's range returns 0, which implements spatial padding, ragged tiles and the
+//    tiles past the end of K without branches;
+//  * the producing layer's pending BatchNorm(+ReLU) is applied at split time (FWD: scale/shift
+//    of the input channels staged in LDS once per block; WGRAD: per-thread channel constants).
+// LDS images are conv_gemm16.hip's: k-contiguous operands (FWD A/B, DGRAD A) as row images
+// [rows][BK+8] (one ds_read_b128 per fragment), k-strided ones (DGRAD B, WGRAD A/B) as col images
+// [BK][rows+32] (two ds_read_b64_tr_b16).  Epilogue: conv_common.h (shared with conv_gemm.hip).
+#include "conv_common.h"
+
+namespace mauv {
+
+namespace {
+
+constexpr unsigned kOOB = 0x7ffffff0u;  // beyond every descriptor range: the load returns 0
+constexpr int kMaxXbn = 512;            // FWD pending-BN input channels staged in LDS
+
+__device__ __forceinline__ floatx4 bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, long long nfloats) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(nfloats * 4), 0x00020000);
+}
+__device__ __forceinline__ unsigned mdiv(unsigned n, unsigned long long m, int s) {
+  return (unsigned)(((unsigned long long)n * m) >> s);
+}
+__device__ __forceinline__ floatx4 bn_relu(floatx4 v, floatx4 sc, floatx4 sh, int relu, bool ok) {
+  v = v * sc + sh;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = (!ok || (relu && !(v[e] > 0.f))) ? 0.f : v[e];
+  return v;
+}
+
+template <int NVA, int NVB>
+struct Stage {
+  floatx4 a[NVA], b[NVB];
+  unsigned ok;  // validity bits (pending-BN operands): a j -> bit j, b j -> bit 8 + j
+  int tc;       // FWD: input-channel offset of this stage's k slice
+};
+
+}  // namespace
+
+template <int MODE, int BM, int BN, bool XBN, bool ONEACC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void conv_split_f32(const ConvArgs a) {
+  constexpr int BK = 16;
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 32, NI = WN / 32;
+  constexpr int NVA = BM / 64, NVB = BN / 64;  // float4 per thread per operand per stage
+  constexpr bool A_COL = (MODE == WGRAD), B_COL = (MODE != FWD);
+  constexpr int RLD = BK + 8;
+  constexpr int A_PL = A_COL ? BK * (BM + 32) : BM * RLD;  // 16-bit words per plane
+  constexpr int B_PL = B_COL ? BK * (BN + 32) : BN * RLD;
+  constexpr int STG = 3 * (A_PL + B_PL);
+  constexpr int XS = (XBN && MODE == FWD) ? 2 * kMaxXbn : 0;  // floats
+  static_assert(2 * STG >= 8 * BN, "epilogue scratch");
+  __shared__ __attribute__((aligned(16))) u16 smem[2 * STG + 2 * XS];
+  float* xbn = (float*)(smem + 2 * STG);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
+  int m0, n0;
+  {  // XCD-aware tile order (conv_gemm.hip)
+    const int nN = (a.N + BN - 1) / BN;
+    const int b = blockIdx.x, nwg = gridDim.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    m0 = (L / nN) * BM;
+    n0 = (L - (L / nN) * nN) * BN;
+  }
+  int g, sp = 0;
+  if constexpr (MODE == WGRAD) { g = blockIdx.y / a.splits; sp = blockIdx.y % a.splits; }
+  else g = blockIdx.y;
+  int kbeg = 0, kend = a.K;
+  if constexpr (MODE == WGRAD) { kbeg = sp * a.kchunk; kend = min(a.K, kbeg + a.kchunk); }
+  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const long long ny = (long long)a.B * a.Ho * a.Wo * a.Cout;  // dy floats per group
+  const float* xg = a.x + (long long)g * a.xs_g;
+  const float* wg = a.w + (long long)g * a.ws_g;
+  const float* dyg = a.dy + (long long)g * ny;
+  __amdgpu_buffer_rsrc_t ra, rb;
+  if constexpr (MODE == FWD) { ra = rsrc(xg, a.B * a.xs_b); rb = rsrc(wg, a.ws_g); }
+  else if constexpr (MODE == DGRAD) { ra = rsrc(dyg, ny); rb = rsrc(wg, a.ws_g); }
+  else { ra = rsrc(dyg, ny); rb = rsrc(xg, a.B * a.xs_b); }
+  const int xs_h = (int)a.xs_h, xs_w = (int)a.xs_w, xs_b = (int)a.xs_b;
+
+  // ---- per-thread loader constants ----
+  unsigned abase[NVA], bbase[NVB];
+  int aq0[NVA], aq1[NVA];
+  int bq0[NVB], bq1[NVB], bq2[NVB];
+  floatx4 wsc = {1.f, 1.f, 1.f, 1.f}, wsh = {0.f, 0.f, 0.f, 0.f};  // WGRAD pending BN of x
+  const int kq = tid & 3;
+#pragma unroll
+  for (int j = 0; j < NVA; ++j) {
+    const int idx = tid + 256 * j;
+    if constexpr (MODE == FWD || MODE == DGRAD) {
+      const int m = m0 + (idx >> 2);
+      const bool ok = m < a.M;
+      const int mm = ok ? m : 0;
+      if constexpr (MODE == FWD) {
+        const int HW = a.Ho * a.Wo, b = mm / HW, rem = mm - b * HW;
+        const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+        const int p0 = oh * a.stride - a.pad, p1 = ow * a.stride - a.pad;
+        abase[j] = (unsigned)((b * xs_b + p0 * xs_h + p1 * xs_w + 4 * kq) * 4);
+        aq0[j] = ok ? p0 : -(1 << 28);
+        aq1[j] = p1;
+      } else {
+        const int HW = a.Hc * a.Wc, b = mm / HW, rem = mm - b * HW;
+        const int i = rem / a.Wc, jj = rem - i * a.Wc;
+        const int q0 = i + (a.ph + a.pad - a.r0) / a.stride;
+        const int q1 = jj + (a.pw + a.pad - a.s0) / a.stride;
+        abase[j] = (unsigned)(((b * a.Ho * a.Wo + q0 * a.Wo + q1) * a.Cout + 4 * kq) * 4);
+        aq0[j] = ok ? q0 : (1 << 28);
+        aq1[j] = q1;
+      }
+    } else {  // WGRAD A: 4 consecutive couts at k row idx / (BM/4)
+      const int co = m0 + 4 * (idx % (BM / 4)), kr = idx / (BM / 4);
+      abase[j] = co < a.M ? (unsigned)((kr * a.Cout + co) * 4) : kOOB;
+      aq0[j] = kr;
+      aq1[j] = 0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NVB; ++j) {
+    const int idx = tid + 256 * j;
+    if constexpr (MODE == FWD) {
+      const int n = n0 + (idx >> 2);
+      bbase[j] = n < a.N ? (unsigned)((n * a.K + 4 * kq) * 4) : kOOB;
+    } else if constexpr (MODE == DGRAD) {
+      const int c = n0 + 4 * (idx % (BN / 4)), kr = idx / (BN / 4);
+      bbase[j] = c < a.N ? (unsigned)((kr * a.R * a.S * a.Cin + c) * 4) : kOOB;
+    } else {  // WGRAD B: fixed column quad (r, s, c..c+3), pixel row idx / (BN/4)
+      const int col = n0 + 4 * (idx % (BN / 4));
+      const bool ok = col < a.N;
+      const int cc = ok ? col : 0, rs = cc / a.Cin, c = cc - rs * a.Cin;
+      const int r = rs / a.S, s = rs - r * a.S;
+      bq0[j] = idx / (BN / 4);        // pixel row within the stage
+      bq1[j] = ok ? r - a.pad : -(1 << 28);
+      bq2[j] = s - a.pad;
+      bbase[j] = (unsigned)(c * 4);
+      if constexpr (XBN) {
+        if (j == 0) {
+          wsc = *(const floatx4*)(a.xsc + g * a.Cin + c);
+          wsh = *(const floatx4*)(a.xsh + g * a.Cin + c);
+        }
+      }
+    }
+  }
+  if constexpr (XBN && MODE == FWD) {
+    for (int i = tid; i < a.Cin; i += 256) {
+      xbn[i] = a.xsc[g * a.Cin + i];
+      xbn[kMaxXbn + i] = a.xsh[g * a.Cin + i];
+    }
+  }
+
+  // ---- tile-uniform k position (FWD: tap r, s + channel; DGRAD: tap tr, ts + cout) ----
+  int t_r = 0, t_s = 0, t_c = 0;
+  typedef Stage<NVA, NVB> St;
+
+  auto load = [&](St& S, int t) {
+    const int k0 = kbeg + t * BK;
+    const bool sok = k0 < kend;  // stage-uniform for FWD / DGRAD (K % 16 == 0)
+    if constexpr (MODE == FWD) {
+      const unsigned soff = (unsigned)((t_r * xs_h + t_s * xs_w + t_c) * 4);
+      S.ok = 0;
+      S.tc = t_c;
+#pragma unroll
+      for (int j = 0; j < NVA; ++j) {
+        const bool ok = sok && (unsigned)(aq0[j] + t_r) < (unsigned)a.H &&
+                        (unsigned)(aq1[j] + t_s) < (unsigned)a.W;
+        S.a[j] = bload(ra, ok ? abase[j] + soff : kOOB);
+        S.ok |= (unsigned)ok << j;
+      }
+#pragma unroll
+      for (int j = 0; j < NVB; ++j) S.b[j] = bload(rb, sok ? bbase[j] + (unsigned)(k0 * 4) : kOOB);
+      t_c += BK;
+      if (t_c >= a.Cin) { t_c = 0; if (++t_s == a.S) { t_s = 0; ++t_r; } }
+    } else if constexpr (MODE == DGRAD) {
+      const unsigned soff = (unsigned)((t_c - (t_r * a.Wo + t_s) * a.Cout) * 4);
+#pragma unroll
+      for (int j = 0; j < NVA; ++j) {
+        const bool ok = sok && (unsigned)(aq0[j] - t_r) < (unsigned)a.Ho &&
+                        (unsigned)(aq1[j] - t_s) < (unsigned)a.Wo;
+        S.a[j] = bload(ra, ok ? abase[j] + soff : kOOB);
+      }
+      const int r = a.r0 + a.stride * t_r, s = a.s0 + a.stride * t_s;
+      const unsigned woff = (unsigned)(((t_c * a.R + r) * a.S + s) * a.Cin * 4);
+#pragma unroll
+      for (int j = 0; j < NVB; ++j) S.b[j] = bload(rb, sok ? bbase[j] + woff : kOOB);
+      t_c += BK;
+      if (t_c >= a.Cout) { t_c = 0; if (++t_s == a.ns) { t_s = 0; ++t_r; } }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NVA; ++j) {
+        const bool ok = k0 + aq0[j] < kend;
+        S.a[j] = bload(ra, ok ? abase[j] + (unsigned)(k0 * a.Cout * 4) : kOOB);
+      }
+      const unsigned HW = (unsigned)(a.Ho * a.Wo);
+      S.ok = 0;
+#pragma unroll
+      for (int j = 0; j < NVB; ++j) {
+        const unsigned p = (unsigned)(k0 + bq0[j]);
+        const unsigned b = mdiv(p, a.mg_hw, a.sh_hw), rem = p - b * HW;
+        const unsigned oh = mdiv(rem, a.mg_w, a.sh_w), ow = rem - oh * (unsigned)a.Wo;
+        const int ih = (int)oh * a.stride + bq1[j], iw = (int)ow * a.stride + bq2[j];
+        const bool ok = (int)p < kend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        S.b[j] = bload(rb, ok ? bbase[j] + (unsigned)(((int)b * xs_b + ih * xs_h + iw * xs_w) * 4)
+                              : kOOB);
+        S.ok |= (unsigned)ok << (8 + j);
+      }
+    }
+  };
+
+  auto split_store = [&](const St& S, int buf) {
+    u16* As = smem + buf * STG;
+    u16* Bs = As + 3 * A_PL;
+#pragma unroll
+    for (int j = 0; j < NVA; ++j) {
+      const int idx = tid + 256 * j;
+      floatx4 v = S.a[j];
+      if constexpr (XBN && MODE == FWD) {
+        const int c = S.tc + 4 * kq;
+        v = bn_relu(v, *(const floatx4*)(xbn + c), *(const floatx4*)(xbn + kMaxXbn + c), a.xrelu,
+                    (S.ok >> j) & 1);
+      }
+      const int off = A_COL ? (idx / (BM / 4)) * (BM + 32) + 4 * (idx % (BM / 4))
+                            : (idx >> 2) * RLD + 4 * (idx & 3);
+      uint2 pl[3];
+      split_bf16<3>(v, pl);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *(uint2*)(As + p * A_PL + off) = pl[p];
+    }
+#pragma unroll
+    for (int j = 0; j < NVB; ++j) {
+      const int idx = tid + 256 * j;
+      floatx4 v = S.b[j];
+      if constexpr (XBN && MODE == WGRAD) v = bn_relu(v, wsc, wsh, a.xrelu, (S.ok >> (8 + j)) & 1);
+      const int off = B_COL ? (idx / (BN / 4)) * (BN + 32) + 4 * (idx % (BN / 4))
+                            : (idx >> 2) * RLD + 4 * (idx & 3);
+      uint2 pl[3];
+      split_bf16<3>(v, pl);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *(uint2*)(Bs + p * B_PL + off) = pl[p];
+    }
+  };
+
+  floatx16 acc[MI][NI], acl[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { acc[mi][ni][r] = 0.f; acl[mi][ni][r] = 0.f; }
+
+  auto compute = [&](int buf) {
+    const u16* As = smem + buf * STG;
+    const u16* Bs = As + 3 * A_PL;
+    u32x4 af[3][MI], bq[3][NI];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        if constexpr (A_COL) af[p][mi] = col_frag(As + p * A_PL, BM + 32, wm * WM + mi * 32, 0, lane);
+        else af[p][mi] = row_frag_ld<RLD>(As + p * A_PL, wm * WM + mi * 32, 0, li, lh);
+      }
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        if constexpr (B_COL) bq[p][ni] = col_frag(Bs + p * B_PL, BN + 32, wn * WN + ni * 32, 0, lane);
+        else bq[p][ni] = row_frag_ld<RLD>(Bs + p * B_PL, wn * WN + ni * 32, 0, li, lh);
+      }
+    }
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        floatx16 c = ONEACC ? acc[mi][ni] : acl[mi][ni];
+        c = H16<DT_BF16>::mfma(af[0][mi], bq[2][ni], c);
+        c = H16<DT_BF16>::mfma(af[2][mi], bq[0][ni], c);
+        c = H16<DT_BF16>::mfma(af[1][mi], bq[1][ni], c);
+        c = H16<DT_BF16>::mfma(af[0][mi], bq[1][ni], c);
+        c = H16<DT_BF16>::mfma(af[1][mi], bq[0][ni], c);
+        if constexpr (ONEACC) {
+          acc[mi][ni] = H16<DT_BF16>::mfma(af[0][mi], bq[0][ni], c);
+        } else {
+          acl[mi][ni] = c;
+          acc[mi][ni] = H16<DT_BF16>::mfma(af[0][mi], bq[0][ni], acc[mi][ni]);
+        }
+      }
+  };
+
+  // ---- pipeline: buffer 0 <- tile 0, registers S1 <- tile 1 ----
+  St S0, S1;
+  load(S0, 0);
+  load(S1, 1);
+  if constexpr (XBN && MODE == FWD) __syncthreads();  // xbn staged
+  split_store(S0, 0);
+  __syncthreads();
+  for (int t = 0; t < nt; t += 2) {
+    load(S0, t + 2);
+    compute(0);
+    split_store(S1, 1);
+    __syncthreads();
+    if (t + 1 >= nt) break;
+    load(S1, t + 3);
+    compute(1);
+    split_store(S0, 0);
+    __syncthreads();
+  }
+
+  if constexpr (!ONEACC) {
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) acc[mi][ni] += acl[mi][ni];
+  }
+  conv_epilogue<MODE, BM, BN>(a, acc, (float*)smem, tid, m0, n0, g, sp);
+}
+
+template <int MODE, int BM, int BN, bool XBN>
+static void launch_split(const ConvArgs& a, int oneacc, hipStream_t st) {
+  dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
+  if (oneacc)
+    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, false>), grid, dim3(256), 0, st, a);
+}
+
+template <int MODE, bool XBN>
+static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
+  const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
+  if (bm == 64 && bn == 64) launch_split<MODE, 64, 64, XBN>(a, oneacc, st);
+  else if (bm == 64) launch_split<MODE, 64, 128, XBN>(a, oneacc, st);
+  else if (bn == 64) launch_split<MODE, 128, 64, XBN>(a, oneacc, st);
+  else launch_split<MODE, 128, 128, XBN>(a, oneacc, st);
+}
+
+bool conv_split_launch(int mode, const ConvArgs& a0, int oneacc, hipStream_t st) {
+  const long long lim = 0x7fff0000LL / 4;  // floats addressable by a 31-bit byte offset
+  const long long nx = (long long)a0.B * a0.xs_b, ny = (long long)a0.B * a0.Ho * a0.Wo * a0.Cout;
+  if (nx > lim || ny > lim || a0.ws_g > lim) return false;
+  ConvArgs a = a0;
+  if (mode == FWD) {
+    const bool va = (a.Cin % 32 == 0) && a.xs_c == 1 && a.xs_w % 4 == 0 && a.xs_h % 4 == 0 &&
+                    a.xs_b % 4 == 0 && a.xs_g % 4 == 0 && a.xs_g != 0;
+    if (!va || (a.xsc && a.Cin > kMaxXbn)) return false;
+    if (a.xsc) split_tiles<FWD, true>(a, oneacc, st);
+    else split_tiles<FWD, false>(a, oneacc, st);
+  } else if (mode == DGRAD) {
+    if (a.Cout % 32 || a.Cin % 4) return false;
+    split_tiles<DGRAD, false>(a, oneacc, st);
+  } else {
+    const bool vb = (a.Cin % 4 == 0) && a.xs_c == 1 && a.xs_w % 4 == 0 && a.xs_h % 4 == 0 &&
+                    a.xs_b % 4 == 0 && a.xs_g % 4 == 0;
+    if (a.Cout % 4 || !vb) return false;
+    magic_div((unsigned)(a.Ho * a.Wo), a.mg_hw, a.sh_hw);
+    magic_div((unsigned)a.Wo, a.mg_w, a.sh_w);
+    if (a.xsc) split_tiles<WGRAD, true>(a, oneacc, st);
+    else split_tiles<WGRAD, false>(a, oneacc, st);
+  }
+  return true;
+}
+
+}  // namespace mauv

@@ -65,6 +65,54 @@ __device__ __forceinline__ u32x4 pack8(floatx8 f) {
   return v;
 }
 
+// ---- MFMA operand fragments (v_mfma_f32_32x32x16_{bf16,f16}: lane l holds row l&31,
+// k = 8(l>>5) + j, j = 0..7) from the two LDS operand images of the implicit-GEMM convs ----
+// row image [rows][LD] (k-contiguous rows): one ds_read_b128 for k-step s
+template <int LD>
+__device__ __forceinline__ u32x4 row_frag_ld(const u16* img, int R0, int s, int li, int lh) {
+  return *(const u32x4*)(img + (R0 + li) * LD + 16 * s + 8 * lh);
+}
+// col image [k][LD] (rows-contiguous, k-strided operand): two hardware-transposed
+// ds_read_b64_tr_b16 reads; LD = rows + 32 makes a 32-lane half cover the 64 banks once
+__device__ __forceinline__ u32x4 col_frag(const u16* img, int LD, int R0, int s, int lane) {
+  const int gq = (lane >> 4) & 3, i = lane & 15, q = i >> 2, p = i & 3, h = lane >> 5;
+  const int col = R0 + 16 * (gq & 1) + 4 * p;
+  const int kr = 16 * s + 8 * h + q;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + kr * LD + col));
+  const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (kr + 4) * LD + col));
+  const uint2 u0 = __builtin_bit_cast(uint2, t0), u1 = __builtin_bit_cast(uint2, t1);
+  u32x4 r;
+  r[0] = u0.x; r[1] = u0.y; r[2] = u1.x; r[3] = u1.y;
+  return r;
+}
+
+// ---- exact split of fp32 into bf16 planes (the split-fp32 conv arithmetic) ----
+// x = h + m + l exactly: h = RNE_bf16(x) keeps 8 significant bits, r = x - h is exact in
+// fp32 and spans at most x's low 16 bit positions, m = RNE_bf16(r), and r - m spans at most
+// 8 bit positions, so l = r - m is itself a bf16.  |m| <= 2^-8 |x|, |l| <= 2^-16 |x|.
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32 (round to nearest even)
+  return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+// NPL = 3: (h, m, l) exact; NPL = 2: (h, m), x - h - m <= 2^-16 |x| dropped
+template <int NPL>
+__device__ __forceinline__ void split_bf16(floatx4 v, uint2* pl) {
+  pl[0].x = pk_bf16(v[0], v[1]);
+  pl[0].y = pk_bf16(v[2], v[3]);
+  const float r0 = v[0] - bf_lo(pl[0].x), r1 = v[1] - bf_hi(pl[0].x);
+  const float r2 = v[2] - bf_lo(pl[0].y), r3 = v[3] - bf_hi(pl[0].y);
+  pl[1].x = pk_bf16(r0, r1);
+  pl[1].y = pk_bf16(r2, r3);
+  if constexpr (NPL == 3) {
+    pl[2].x = pk_bf16(r0 - bf_lo(pl[1].x), r1 - bf_hi(pl[1].x));
+    pl[2].y = pk_bf16(r2 - bf_lo(pl[1].y), r3 - bf_hi(pl[1].y));
+  }
+}
+
 }  // namespace mauv
 
 namespace mauv {

@@ -69,6 +69,24 @@ class _Prof:
 
 
 # ----------------------------------------------------------------------- convolutions
+F32_MATH = {"exact": 0, "split3": 3, "split1": 5, "split": 6}
+_F32_NAMES = {v: k for k, v in F32_MATH.items()}
+
+
+def f32_math():
+    """Arithmetic of the fp32 convs: "split" (default; exact three-way bf16 split of every
+    operand, six plane products on bf16 MFMA, fp32 accumulation), "split3" or "exact"
+    (v_mfma_f32_32x32x2_f32) — include/mauv.h mauv_set_f32_math."""
+    return _F32_NAMES[lib.mauv_set_f32_math(-1)]
+
+
+def set_f32_math(mode):
+    """Select the fp32 conv arithmetic (process-wide); returns the previous mode."""
+    rc = lib.mauv_set_f32_math(F32_MATH[mode])
+    check(0 if rc >= 0 else rc, "set_f32_math")
+    return _F32_NAMES[rc]
+
+
 def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_strides=None,
                x_bn=None, stats=None, alg_cin=None):
     """y[G][B*Ho*Wo][Cout] = conv(x'[g], w[g]) (+ bias[g]); w: [G][Cout][R][R][Cin].

@@ -53,6 +53,21 @@ def test_abi_version_and_error_string():
     assert isinstance(lib.mauv_last_error(), bytes)
 
 
+def test_f32_math_mode_host_switch():
+    """mauv_set_f32_math is host-only state: default split (6), settable, bad modes rejected."""
+    from mauv._lib import lib
+    if "MAUV_F32_MATH" not in os.environ:
+        assert lib.mauv_set_f32_math(-1) == 6
+    prev = lib.mauv_set_f32_math(0)
+    try:
+        assert lib.mauv_set_f32_math(-1) == 0
+        assert lib.mauv_set_f32_math(3) == 0
+        assert lib.mauv_set_f32_math(7) < 0 and b"mode" in lib.mauv_last_error()
+        assert lib.mauv_set_f32_math(-1) == 3
+    finally:
+        lib.mauv_set_f32_math(prev)
+
+
 def test_state_dict_compatible_with_reference_layout():
     from mauv.models import define_models, DEFAULT_PRIOR
     from oracle.model_ref import define_models as oracle_define

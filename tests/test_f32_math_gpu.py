@@ -1,0 +1,124 @@
+"""The fp32 conv arithmetics (include/mauv.h mauv_set_f32_math) against float64.
+
+"split" (the default) stages every fp32 operand as three bf16 planes, x = h + m + l exactly,
+and accumulates the six plane products h*h, h*m, m*h, h*l, l*h, m*m from bf16 MFMA in fp32
+(h*h in its own accumulator).  Requirement: as accurate as "exact" (v_mfma_f32_32x32x2_f32,
+an fmaf chain) — per output (fwd y, dgrad dx, wgrad dW) the max error vs float64 is within
+2x the exact mode's plus 2^-24 of the output scale — at the ResNet-50 shapes, the head's
+linears, and with operands spanning fp32's range (1e-30 .. 1e30, which bf16's 8-bit
+exponent keeps).  "split3" (h, m planes only; opt-in) is held to 1e-4 relative.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+ULP32 = 2.0 ** -24
+
+
+@pytest.fixture
+def f32_math():
+    from mauv import ops
+    prev = ops.f32_math()
+    yield ops.set_f32_math
+    ops.set_f32_math(prev)
+
+
+def _ref_all(x, w, dy, st, pad):
+    """float64 (y, dx, dW) per MC group; x [G,B,H,W,Cin], w [G,Cout,R,R,Cin] (KRSC)."""
+    ys, dxs, dws = [], [], []
+    for g in range(w.shape[0]):
+        xg = x[g].permute(0, 3, 1, 2).double().requires_grad_(True)
+        wg = w[g].permute(0, 3, 1, 2).double().requires_grad_(True)
+        yg = F.conv2d(xg, wg, stride=st, padding=pad)
+        yg.backward(dy[g].permute(0, 3, 1, 2).double())
+        ys.append(yg.detach().permute(0, 2, 3, 1))
+        dxs.append(xg.grad.permute(0, 2, 3, 1))
+        dws.append(wg.grad.permute(0, 2, 3, 1))
+    return torch.stack(ys), torch.stack(dxs), torch.stack(dws)
+
+
+def _run_all(x, w, dy, G, B, H, Cin, Cout, R, st, pad):
+    from mauv import ops
+    Ho = ops.out_hw(H, R, st, pad)
+    x, w, dy = x.to(dev), w.to(dev), dy.to(dev)
+    y = torch.empty(G, B, Ho, Ho, Cout, device=dev)
+    ops.conv2d_fwd(x, w, y, G, B, H, H, Cin, Cout, R, st, pad)
+    dx = torch.empty(G, B, H, H, Cin, device=dev)
+    ops.conv2d_bwd_data(dy, w, dx, G, B, H, H, Cin, Cout, R, st, pad)
+    sp = ops.wgrad_splits(G, B, H, H, Cin, Cout, R, st, pad)
+    ws = torch.empty(sp, G, Cout, R * R * Cin, device=dev)
+    ops.conv2d_bwd_weight(x, dy, ws, sp, G, B, H, H, Cin, Cout, R, st, pad)
+    torch.cuda.synchronize()
+    return y.cpu(), dx.cpu(), ws.sum(0).view(G, Cout, R, R, Cin).cpu()
+
+
+def _errors(outs, refs):
+    return [((o.double() - r).abs().max().item(), r.abs().max().item())
+            for o, r in zip(outs, refs)]
+
+
+CASES = [
+    # G, B, H, Cin, Cout, R, stride, pad
+    (2, 2, 8, 64, 64, 1, 1, 0),
+    (2, 2, 8, 64, 64, 3, 1, 1),
+    (2, 3, 9, 128, 128, 3, 2, 1),
+    (1, 2, 8, 256, 512, 1, 2, 0),
+    (2, 2, 4, 512, 2048, 1, 1, 0),
+    (1, 4, 14, 256, 256, 3, 1, 1),     # K = 2304 (layer3 3x3)
+    (2, 1, 1, 2048, 384, 1, 1, 0),     # attention q|k|v linear
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_split_as_accurate_as_exact(case, f32_math):
+    G, B, H, Cin, Cout, R, st, pad = case
+    torch.manual_seed(0)
+    x = torch.randn(G, B, H, H, Cin)
+    w = torch.randn(G, Cout, R, R, Cin) / math.sqrt(Cin * R * R)
+    Ho = (H + 2 * pad - R) // st + 1
+    dy = torch.randn(G, B, Ho, Ho, Cout)
+    refs = _ref_all(x, w, dy, st, pad)
+    err = {}
+    for mode in ("exact", "split", "split3"):
+        f32_math(mode)
+        err[mode] = _errors(_run_all(x, w, dy, G, B, H, Cin, Cout, R, st, pad), refs)
+    for what, (e_x, scale), (e_s, _), (e_3, _) in zip(("y", "dx", "dW"), err["exact"],
+                                                    err["split"], err["split3"]):
+        assert e_s <= 2.0 * e_x + ULP32 * scale, (what, e_s, e_x, scale)
+        assert e_3 <= 1e-4 * scale, (what, e_3, scale)
+
+
+def test_split_keeps_fp32_range(f32_math):
+    """Per-channel scales 1e-30 .. 1e30 (products O(1)): bf16 planes share fp32's exponent."""
+    G, B, H, Cin, Cout, R = 1, 2, 6, 64, 64, 3
+    torch.manual_seed(3)
+    s = torch.logspace(-30, 30, Cin)
+    x = torch.randn(G, B, H, H, Cin) * s
+    w = torch.randn(G, Cout, R, R, Cin) / s / math.sqrt(Cin * R * R)
+    dy = torch.randn(G, B, H, H, Cout)
+    refs = _ref_all(x, w, dy, 1, 1)
+    f32_math("exact")
+    ex = _errors(_run_all(x, w, dy, G, B, H, Cin, Cout, R, 1, 1), refs)
+    f32_math("split")
+    sp = _errors(_run_all(x, w, dy, G, B, H, Cin, Cout, R, 1, 1), refs)
+    # y is O(1); dx and dW carry the per-channel scales, so compare them channel-relative
+    assert sp[0][0] <= 2.0 * ex[0][0] + ULP32 * sp[0][1], (sp[0], ex[0])
+    for i in (1, 2):
+        assert math.isfinite(sp[i][0])
+    outs = _run_all(x, w, dy, G, B, H, Cin, Cout, R, 1, 1)
+    dx_rel = ((outs[1].double() - refs[1]).abs() / refs[1].abs().amax(dim=(0, 1, 2, 3))).max()
+    dw_rel = ((outs[2].double() - refs[2]).abs() / refs[2].abs().amax(dim=(0, 1, 2, 3))).max()
+    assert dx_rel.item() <= 1e-5 and dw_rel.item() <= 1e-5, (dx_rel.item(), dw_rel.item())
+
+
+def test_mode_switch_roundtrip(f32_math):
+    from mauv import ops
+    assert f32_math("exact") in ops.F32_MATH
+    assert ops.f32_math() == "exact"
+    assert f32_math("split") == "exact"
+    assert ops.f32_math() == "split"
