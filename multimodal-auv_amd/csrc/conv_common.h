@@ -75,14 +75,18 @@ __device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int
 // Epilogue of one BM x BN block tile: acc[mi][ni] holds the fp32 32x32 accumulator tiles of
 // this wave (the C/D layout of both v_mfma_f32_32x32x2_f32 and v_mfma_f32_32x32x16_bf16:
 // lane l = column l&31, register r = row (r&3) + 8(r>>2) + 4(l>>5)).
-template <int MODE, int BM, int BN, int MI, int NI>
+// WGM x WGN waves (wave = wm * WGN + wn).  BN statistics partials are per SR = min(BM, 128)
+// rows (the conv_tile_rows granularity the host sizes them with), so a 256-row tile writes two.
+template <int MODE, int BM, int BN, int MI, int NI, int WGM = 2, int WGN = 2>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx16 (&acc)[MI][NI],
                                               float* smem, int tid, int m0, int n0, int g,
                                               int sp) {
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int SR = BM > 128 ? 128 : BM, SUB = BM / SR, WPS = WGM / SUB;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
   const int li = lane & 31, lh = lane >> 5;
+  const int sub = wm / WPS;
   float* outg;
   if constexpr (MODE == WGRAD)
     outg = a.out + ((long long)sp * a.G + g) * ((long long)a.M * a.N);
@@ -99,7 +103,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx16 (&acc)
   float s1[NI], s2[NI];
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) { s1[ni] = 0.f; s2[ni] = 0.f; }
-  const int nvalid = min(BM, a.M - m0);
+  const int nvalid = min(SR, a.M - (m0 + sub * SR));  // rows of this wave's partial
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -162,8 +166,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx16 (&acc)
       // pass 2: M2 around the tile mean
       float mean[NI];
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
-        mean[ni] = (red[tcol + ni * 32] + red[BN + tcol + ni * 32]) / (float)nvalid;
+      for (int ni = 0; ni < NI; ++ni) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WPS; ++w) t += red[(sub * WPS + w) * BN + tcol + ni * 32];
+        mean[ni] = t / (float)nvalid;
+      }
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) s2[ni] = 0.f;
 #pragma unroll
@@ -186,19 +194,25 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx16 (&acc)
     for (int ni = 0; ni < NI; ++ni) s2[ni] += __shfl_xor(s2[ni], 32, 64);
     if (lh == 0) {
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) red[2 * BN + wm * BN + tcol + ni * 32] = s2[ni];
+      for (int ni = 0; ni < NI; ++ni) red[WGM * BN + wm * BN + tcol + ni * 32] = s2[ni];
     }
     __syncthreads();
-    if (tid < BN && n0 + tid < a.N) {
-      const float t1 = red[tid] + red[BN + tid], t2 = red[2 * BN + tid] + red[3 * BN + tid];
-      const int mt = m0 / BM;
+    const int col = tid % BN, sb = tid / BN, nv = min(SR, a.M - (m0 + sb * SR));
+    if (tid < SUB * BN && n0 + col < a.N && nv > 0) {
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPS; ++w) {
+        t1 += red[(sb * WPS + w) * BN + col];
+        t2 += red[WGM * BN + (sb * WPS + w) * BN + col];
+      }
+      const int mt = m0 / SR + sb;
       if (fst) {
-        const long long so = ((long long)g * a.st_nblk + a.st_base + mt) * a.N + n0 + tid;
-        a.st_mean[so] = t1 / (float)nvalid;
+        const long long so = ((long long)g * a.st_nblk + a.st_base + mt) * a.N + n0 + col;
+        a.st_mean[so] = t1 / (float)nv;
         a.st_m2[so] = t2;
-        if (n0 + tid == 0) a.st_cnt[(long long)g * a.st_nblk + a.st_base + mt] = (float)nvalid;
+        if (n0 + col == 0) a.st_cnt[(long long)g * a.st_nblk + a.st_base + mt] = (float)nv;
       } else {
-        const long long so = ((long long)g * a.bp_nblk + a.bp_base + mt) * a.N + n0 + tid;
+        const long long so = ((long long)g * a.bp_nblk + a.bp_base + mt) * a.N + n0 + col;
         a.bp_p1[so] = t1;
         a.bp_p2[so] = t2;
       }

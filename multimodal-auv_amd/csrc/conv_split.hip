@@ -20,6 +20,8 @@
 // LDS images are conv_gemm16.hip's: k-contiguous operands (FWD A/B, DGRAD A) as row images
 // [rows][BK+8] (one ds_read_b128 per fragment), k-strided ones (DGRAD B, WGRAD A/B) as col images
 // [BK][rows+32] (two ds_read_b64_tr_b16).  Epilogue: conv_common.h (shared with conv_gemm.hip).
+#include <stdlib.h>
+
 #include "conv_common.h"
 
 namespace mauv {
@@ -54,12 +56,29 @@ struct Stage {
 
 }  // namespace
 
+// Waves: 2 x 2 for tiles up to 128 x 128 (256 threads, two blocks per CU), 4 x 2 / 2 x 4 for
+// 256 x 128 / 128 x 256 (512 threads, one block per CU) — the 256-wide tiles halve the L2
+// re-reads of the other operand per MFMA, which the fp32 operand traffic makes the limit.
+template <int BM, int BN>
+struct SplitWaves {
+  static constexpr int M = BM == 256 ? 4 : 2, N = BN == 256 ? 4 : 2, T = 64 * M * N;
+};
+// loader row of index idx for the row images: wave-local permutation so that each 16-lane
+// ds_write_b64 group stores rows r, r+2, r+4, r+6 (row stride 12 dwords: conflict-free)
+__device__ __forceinline__ int row_of(int idx) {
+  const int l = idx & 63;
+  return (idx >> 6) * 16 + 8 * (l >> 5) + 2 * ((l >> 2) & 3) + ((l >> 4) & 1);
+}
+
 template <int MODE, int BM, int BN, bool XBN, bool ONEACC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__((SplitWaves<BM, BN>::T)) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_split_f32(const ConvArgs a) {
   constexpr int BK = 16;
-  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 32, NI = WN / 32;
-  constexpr int NVA = BM / 64, NVB = BN / 64;  // float4 per thread per operand per stage
+  constexpr int WGM = SplitWaves<BM, BN>::M, WGN = SplitWaves<BM, BN>::N;
+  constexpr int NT = SplitWaves<BM, BN>::T;
+  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
+  constexpr int NVA = 4 * BM / NT, NVB = 4 * BN / NT;  // float4 per thread per operand per stage
+  static_assert(NVA >= 1 && NVB >= 1, "tile too narrow for the thread count");
   constexpr bool A_COL = (MODE == WGRAD), B_COL = (MODE != FWD);
   constexpr int RLD = BK + 8;
   constexpr int A_PL = A_COL ? BK * (BM + 32) : BM * RLD;  // 16-bit words per plane
@@ -71,7 +90,7 @@ void conv_split_f32(const ConvArgs a) {
   float* xbn = (float*)(smem + 2 * STG);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, li = lane & 31, lh = lane >> 5;
+  const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
   int m0, n0;
   {  // XCD-aware tile order (conv_gemm.hip)
     const int nN = (a.N + BN - 1) / BN;
@@ -105,9 +124,9 @@ void conv_split_f32(const ConvArgs a) {
   const int kq = tid & 3;
 #pragma unroll
   for (int j = 0; j < NVA; ++j) {
-    const int idx = tid + 256 * j;
+    const int idx = tid + NT * j;
     if constexpr (MODE == FWD || MODE == DGRAD) {
-      const int m = m0 + (idx >> 2);
+      const int m = m0 + row_of(idx);
       const bool ok = m < a.M;
       const int mm = ok ? m : 0;
       if constexpr (MODE == FWD) {
@@ -135,9 +154,9 @@ void conv_split_f32(const ConvArgs a) {
   }
 #pragma unroll
   for (int j = 0; j < NVB; ++j) {
-    const int idx = tid + 256 * j;
+    const int idx = tid + NT * j;
     if constexpr (MODE == FWD) {
-      const int n = n0 + (idx >> 2);
+      const int n = n0 + row_of(idx);
       bbase[j] = n < a.N ? (unsigned)((n * a.K + 4 * kq) * 4) : kOOB;
     } else if constexpr (MODE == DGRAD) {
       const int c = n0 + 4 * (idx % (BN / 4)), kr = idx / (BN / 4);
@@ -160,7 +179,7 @@ void conv_split_f32(const ConvArgs a) {
     }
   }
   if constexpr (XBN && MODE == FWD) {
-    for (int i = tid; i < a.Cin; i += 256) {
+    for (int i = tid; i < a.Cin; i += NT) {
       xbn[i] = a.xsc[g * a.Cin + i];
       xbn[kMaxXbn + i] = a.xsh[g * a.Cin + i];
     }
@@ -229,7 +248,7 @@ void conv_split_f32(const ConvArgs a) {
     u16* Bs = As + 3 * A_PL;
 #pragma unroll
     for (int j = 0; j < NVA; ++j) {
-      const int idx = tid + 256 * j;
+      const int idx = tid + NT * j;
       floatx4 v = S.a[j];
       if constexpr (XBN && MODE == FWD) {
         const int c = S.tc + 4 * kq;
@@ -237,7 +256,7 @@ void conv_split_f32(const ConvArgs a) {
                     (S.ok >> j) & 1);
       }
       const int off = A_COL ? (idx / (BM / 4)) * (BM + 32) + 4 * (idx % (BM / 4))
-                            : (idx >> 2) * RLD + 4 * (idx & 3);
+                            : row_of(idx) * RLD + 4 * (idx & 3);
       uint2 pl[3];
       split_bf16<3>(v, pl);
 #pragma unroll
@@ -245,11 +264,11 @@ void conv_split_f32(const ConvArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < NVB; ++j) {
-      const int idx = tid + 256 * j;
+      const int idx = tid + NT * j;
       floatx4 v = S.b[j];
       if constexpr (XBN && MODE == WGRAD) v = bn_relu(v, wsc, wsh, a.xrelu, (S.ok >> (8 + j)) & 1);
       const int off = B_COL ? (idx / (BN / 4)) * (BN + 32) + 4 * (idx % (BN / 4))
-                            : (idx >> 2) * RLD + 4 * (idx & 3);
+                            : row_of(idx) * RLD + 4 * (idx & 3);
       uint2 pl[3];
       split_bf16<3>(v, pl);
 #pragma unroll
@@ -313,7 +332,8 @@ void conv_split_f32(const ConvArgs a) {
     compute(0);
     split_store(S1, 1);
     __syncthreads();
-    if (t + 1 >= nt) break;
+    // (an odd nt — only the ragged last split-K chunk of a WGRAD — computes one all-zero tile
+    // here rather than branching out of the stage pair)
     load(S1, t + 3);
     compute(1);
     split_store(S0, 0);
@@ -326,21 +346,40 @@ void conv_split_f32(const ConvArgs a) {
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) acc[mi][ni] += acl[mi][ni];
   }
-  conv_epilogue<MODE, BM, BN>(a, acc, (float*)smem, tid, m0, n0, g, sp);
+  conv_epilogue<MODE, BM, BN, MI, NI, WGM, WGN>(a, acc, (float*)smem, tid, m0, n0, g, sp);
 }
 
 template <int MODE, int BM, int BN, bool XBN>
 static void launch_split(const ConvArgs& a, int oneacc, hipStream_t st) {
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
+  const dim3 block(SplitWaves<BM, BN>::T);
   if (oneacc)
-    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true>), grid, block, 0, st, a);
   else
-    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, false>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, false>), grid, block, 0, st, a);
 }
 
 template <int MODE, bool XBN>
 static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
   const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
+  // MAUV_SPLIT_BIG: 1 = 256-wide tiles while they keep >= 2 blocks per CU-round, 2 = whenever
+  // both extents exceed 64 (tests); default 0 — measured on the bench workload, they do not beat
+  // two co-resident 128 x 128 blocks (225 vs 229 ms of convs per step)
+  const char* e = getenv("MAUV_SPLIT_BIG");
+  const int big = e ? atoi(e) : 0;
+  const long long minb = big == 2 ? 1 : 512;
+  if (big && bm == 128 && bn == 128) {
+    // a 256-wide side along the larger extent
+    const long long gz = (long long)a.G * (MODE == WGRAD ? a.splits : 1);
+    if (a.M >= a.N && (long long)ceil_div(a.M, 256) * ceil_div(a.N, 128) * gz >= minb) {
+      launch_split<MODE, 256, 128, XBN>(a, oneacc, st);
+      return;
+    }
+    if (a.N > a.M && a.N >= 256 && (long long)ceil_div(a.M, 128) * ceil_div(a.N, 256) * gz >= minb) {
+      launch_split<MODE, 128, 256, XBN>(a, oneacc, st);
+      return;
+    }
+  }
   if (bm == 64 && bn == 64) launch_split<MODE, 64, 64, XBN>(a, oneacc, st);
   else if (bm == 64) launch_split<MODE, 64, 128, XBN>(a, oneacc, st);
   else if (bn == 64) launch_split<MODE, 128, 64, XBN>(a, oneacc, st);

@@ -103,11 +103,15 @@ template <int NPL>
 __device__ __forceinline__ void split_bf16(floatx4 v, uint2* pl) {
   pl[0].x = pk_bf16(v[0], v[1]);
   pl[0].y = pk_bf16(v[2], v[3]);
+  // opaque to the optimiser: it would otherwise re-convert each element alone to extract the
+  // low half instead of shifting the packed word
+  asm("" : "+v"(pl[0].x), "+v"(pl[0].y));
   const float r0 = v[0] - bf_lo(pl[0].x), r1 = v[1] - bf_hi(pl[0].x);
   const float r2 = v[2] - bf_lo(pl[0].y), r3 = v[3] - bf_hi(pl[0].y);
   pl[1].x = pk_bf16(r0, r1);
   pl[1].y = pk_bf16(r2, r3);
   if constexpr (NPL == 3) {
+    asm("" : "+v"(pl[1].x), "+v"(pl[1].y));
     pl[2].x = pk_bf16(r0 - bf_lo(pl[1].x), r1 - bf_hi(pl[1].x));
     pl[2].y = pk_bf16(r2 - bf_lo(pl[1].y), r3 - bf_hi(pl[1].y));
   }

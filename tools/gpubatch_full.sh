@@ -1,0 +1,7 @@
+# round-end style check: every GPU test, smoke(), the default bench line
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/full_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/full_smoke.log 2>&1 || exit 1
+timeout -k 10 900 python -u bench.py > gpurun_out/full_bench.log 2>&1 || exit 1
+echo done

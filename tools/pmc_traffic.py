@@ -15,8 +15,10 @@ from collections import defaultdict
 
 
 def family(name):
-    if "conv_gemm" in name:
-        return "conv_gemm_f32"
+    if "conv_gemm_f32" in name or "conv_split_f32" in name:
+        return "conv_f32"        # the fp32 conv family: split kernels + stems on conv_gemm_f32
+    if "conv_gemm_h16" in name:
+        return "conv_h16"
     return name.split("(")[0].replace("void ", "")
 
 
@@ -42,8 +44,9 @@ def main(fetch_dir, write_dir, out_json):
         a[3] += v * 1024.0
     rows = {k: {"launches": v[0], "read_bytes": v[2], "write_bytes": v[3],
                 "bytes_per_launch": (v[2] + v[3]) / max(v[0], 1)} for k, v in agg.items()}
-    conv = rows["conv_gemm_f32"]
-    res = {"kernel": "conv_gemm_f32", "bytes_per_launch": round(conv["bytes_per_launch"]),
+    conv = rows["conv_f32"]
+    res = {"kernel": "conv_f32 (conv_split_f32 + stem conv_gemm_f32)",
+           "bytes_per_launch": round(conv["bytes_per_launch"]),
            "launches": conv["launches"], "per_family": rows,
            "method": "2*FETCH_SIZE + WRITE_SIZE (rocprofv3 PMC, separate passes, KiB units)"}
     with open(out_json, "w") as f:
