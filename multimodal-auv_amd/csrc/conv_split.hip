@@ -59,9 +59,13 @@ struct Stage {
 // Waves: 2 x 2 for tiles up to 128 x 128 (256 threads, two blocks per CU), 4 x 2 / 2 x 4 for
 // 256 x 128 / 128 x 256 (512 threads, one block per CU) — the 256-wide tiles halve the L2
 // re-reads of the other operand per MFMA, which the fp32 operand traffic makes the limit.
-template <int BM, int BN>
+// WV = 8 on a 128 x 128 tile: 4 x 2 waves of 32 x 64 (one accumulator set, <= 128 VGPRs, two
+// blocks = four waves per SIMD for latency hiding)
+template <int BM, int BN, int WV>
 struct SplitWaves {
-  static constexpr int M = BM == 256 ? 4 : 2, N = BN == 256 ? 4 : 2, T = 64 * M * N;
+  static constexpr bool W8 = (WV == 8 && BM == 128 && BN == 128);
+  static constexpr int M = W8 ? 4 : (BM == 256 ? 4 : 2), N = W8 ? 2 : (BN == 256 ? 4 : 2);
+  static constexpr int T = 64 * M * N, EU = W8 ? 4 : 2;
 };
 // loader row of index idx for the row images: wave-local permutation so that each 16-lane
 // ds_write_b64 group stores rows r, r+2, r+4, r+6 (row stride 12 dwords: conflict-free)
@@ -70,12 +74,13 @@ __device__ __forceinline__ int row_of(int idx) {
   return (idx >> 6) * 16 + 8 * (l >> 5) + 2 * ((l >> 2) & 3) + ((l >> 4) & 1);
 }
 
-template <int MODE, int BM, int BN, bool XBN, bool ONEACC>
-__global__ __launch_bounds__((SplitWaves<BM, BN>::T)) __attribute__((amdgpu_waves_per_eu(2)))
+template <int MODE, int BM, int BN, bool XBN, bool ONEACC, int WV>
+__global__ __launch_bounds__((SplitWaves<BM, BN, WV>::T))
+__attribute__((amdgpu_waves_per_eu(SplitWaves<BM, BN, WV>::EU)))
 void conv_split_f32(const ConvArgs a) {
   constexpr int BK = 16;
-  constexpr int WGM = SplitWaves<BM, BN>::M, WGN = SplitWaves<BM, BN>::N;
-  constexpr int NT = SplitWaves<BM, BN>::T;
+  constexpr int WGM = SplitWaves<BM, BN, WV>::M, WGN = SplitWaves<BM, BN, WV>::N;
+  constexpr int NT = SplitWaves<BM, BN, WV>::T;
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
   constexpr int NVA = 4 * BM / NT, NVB = 4 * BN / NT;  // float4 per thread per operand per stage
   static_assert(NVA >= 1 && NVB >= 1, "tile too narrow for the thread count");
@@ -349,14 +354,18 @@ void conv_split_f32(const ConvArgs a) {
   conv_epilogue<MODE, BM, BN, MI, NI, WGM, WGN>(a, acc, (float*)smem, tid, m0, n0, g, sp);
 }
 
-template <int MODE, int BM, int BN, bool XBN>
+template <int MODE, int BM, int BN, bool XBN, int WV = 4>
 static void launch_split(const ConvArgs& a, int oneacc, hipStream_t st) {
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
-  const dim3 block(SplitWaves<BM, BN>::T);
-  if (oneacc)
-    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true>), grid, block, 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, false>), grid, block, 0, st, a);
+  const dim3 block(SplitWaves<BM, BN, WV>::T);
+  if constexpr (WV == 8) {  // one accumulator set (128-VGPR budget)
+    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV>), grid, block, 0, st, a);
+  } else {
+    if (oneacc)
+      hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV>), grid, block, 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, false, WV>), grid, block, 0, st, a);
+  }
 }
 
 template <int MODE, bool XBN>
@@ -380,6 +389,11 @@ static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
       return;
     }
   }
+  // 128 x 128 tiles run as eight waves of 32 x 64 (four per SIMD): measured 206 vs 223 ms of
+  // convs per bench step over four waves of 64 x 64 (MAUV_SPLIT_W8=0 restores those)
+  static int w8 = -1;
+  if (w8 < 0) { const char* e8 = getenv("MAUV_SPLIT_W8"); w8 = e8 ? atoi(e8) : 1; }
+  if (w8 && bm == 128 && bn == 128) { launch_split<MODE, 128, 128, XBN, 8>(a, oneacc, st); return; }
   if (bm == 64 && bn == 64) launch_split<MODE, 64, 64, XBN>(a, oneacc, st);
   else if (bm == 64) launch_split<MODE, 64, 128, XBN>(a, oneacc, st);
   else if (bn == 64) launch_split<MODE, 128, 64, XBN>(a, oneacc, st);
