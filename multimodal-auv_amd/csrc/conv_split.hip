@@ -61,10 +61,13 @@ struct Stage {
 // re-reads of the other operand per MFMA, which the fp32 operand traffic makes the limit.
 // WV = 8 on a 128 x 128 tile: 4 x 2 waves of 32 x 64 (one accumulator set, <= 128 VGPRs, two
 // blocks = four waves per SIMD for latency hiding)
+// (128 x 64 / 64 x 128 with WV = 8: waves of 32 x 32; the 64-wide operand is then loaded by
+// half the threads)
 template <int BM, int BN, int WV>
 struct SplitWaves {
-  static constexpr bool W8 = (WV == 8 && BM == 128 && BN == 128);
-  static constexpr int M = W8 ? 4 : (BM == 256 ? 4 : 2), N = W8 ? 2 : (BN == 256 ? 4 : 2);
+  static constexpr bool W8 = (WV == 8 && BM <= 128 && BN <= 128 && BM + BN >= 192);
+  static constexpr int M = W8 ? (BM == 128 ? 4 : 2) : (BM == 256 ? 4 : 2);
+  static constexpr int N = W8 ? (BM == 128 ? 2 : 4) : (BN == 256 ? 4 : 2);
   static constexpr int T = 64 * M * N, EU = W8 ? 4 : 2;
 };
 // loader row of index idx for the row images: wave-local permutation so that each 16-lane
@@ -82,17 +85,23 @@ void conv_split_f32(const ConvArgs a) {
   constexpr int WGM = SplitWaves<BM, BN, WV>::M, WGN = SplitWaves<BM, BN, WV>::N;
   constexpr int NT = SplitWaves<BM, BN, WV>::T;
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
-  constexpr int NVA = 4 * BM / NT, NVB = 4 * BN / NT;  // float4 per thread per operand per stage
-  static_assert(NVA >= 1 && NVB >= 1, "tile too narrow for the thread count");
+  // float4 per stage per operand (LA, LB) and per thread (NVA, NVB); with LB < NT the threads
+  // tid >= LB load nothing (offset past the descriptor) and park their split planes in a dummy
+  // LDS slot, keeping the stage branch-free
+  constexpr int LA = 4 * BM, LB = 4 * BN;
+  constexpr int NVA = (LA + NT - 1) / NT, NVB = (LB + NT - 1) / NT;
+  constexpr bool PA = LA % NT != 0, PB = LB % NT != 0;
   constexpr bool A_COL = (MODE == WGRAD), B_COL = (MODE != FWD);
   constexpr int RLD = BK + 8;
   constexpr int A_PL = A_COL ? BK * (BM + 32) : BM * RLD;  // 16-bit words per plane
   constexpr int B_PL = B_COL ? BK * (BN + 32) : BN * RLD;
   constexpr int STG = 3 * (A_PL + B_PL);
   constexpr int XS = (XBN && MODE == FWD) ? 2 * kMaxXbn : 0;  // floats
+  constexpr int DUM = (PA || PB) ? 12 * NT : 0;                // dummy plane slots (16-bit)
   static_assert(2 * STG >= 8 * BN, "epilogue scratch");
-  __shared__ __attribute__((aligned(16))) u16 smem[2 * STG + 2 * XS];
+  __shared__ __attribute__((aligned(16))) u16 smem[2 * STG + 2 * XS + DUM];
   float* xbn = (float*)(smem + 2 * STG);
+  u16* dum = smem + 2 * STG + 2 * XS + 12 * threadIdx.x;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
@@ -205,11 +214,15 @@ void conv_split_f32(const ConvArgs a) {
       for (int j = 0; j < NVA; ++j) {
         const bool ok = sok && (unsigned)(aq0[j] + t_r) < (unsigned)a.H &&
                         (unsigned)(aq1[j] + t_s) < (unsigned)a.W;
-        S.a[j] = bload(ra, ok ? abase[j] + soff : kOOB);
+        const bool act = !PA || tid + NT * j < LA;
+        S.a[j] = bload(ra, ok && act ? abase[j] + soff : kOOB);
         S.ok |= (unsigned)ok << j;
       }
 #pragma unroll
-      for (int j = 0; j < NVB; ++j) S.b[j] = bload(rb, sok ? bbase[j] + (unsigned)(k0 * 4) : kOOB);
+      for (int j = 0; j < NVB; ++j) {
+        const bool act = !PB || tid + NT * j < LB;
+        S.b[j] = bload(rb, sok && act ? bbase[j] + (unsigned)(k0 * 4) : kOOB);
+      }
       t_c += BK;
       if (t_c >= a.Cin) { t_c = 0; if (++t_s == a.S) { t_s = 0; ++t_r; } }
     } else if constexpr (MODE == DGRAD) {
@@ -217,19 +230,20 @@ void conv_split_f32(const ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < NVA; ++j) {
         const bool ok = sok && (unsigned)(aq0[j] - t_r) < (unsigned)a.Ho &&
-                        (unsigned)(aq1[j] - t_s) < (unsigned)a.Wo;
+                        (unsigned)(aq1[j] - t_s) < (unsigned)a.Wo && (!PA || tid + NT * j < LA);
         S.a[j] = bload(ra, ok ? abase[j] + soff : kOOB);
       }
       const int r = a.r0 + a.stride * t_r, s = a.s0 + a.stride * t_s;
       const unsigned woff = (unsigned)(((t_c * a.R + r) * a.S + s) * a.Cin * 4);
 #pragma unroll
-      for (int j = 0; j < NVB; ++j) S.b[j] = bload(rb, sok ? bbase[j] + woff : kOOB);
+      for (int j = 0; j < NVB; ++j)
+        S.b[j] = bload(rb, sok && (!PB || tid + NT * j < LB) ? bbase[j] + woff : kOOB);
       t_c += BK;
       if (t_c >= a.Cout) { t_c = 0; if (++t_s == a.ns) { t_s = 0; ++t_r; } }
     } else {
 #pragma unroll
       for (int j = 0; j < NVA; ++j) {
-        const bool ok = k0 + aq0[j] < kend;
+        const bool ok = k0 + aq0[j] < kend && (!PA || tid + NT * j < LA);
         S.a[j] = bload(ra, ok ? abase[j] + (unsigned)(k0 * a.Cout * 4) : kOOB);
       }
       const unsigned HW = (unsigned)(a.Ho * a.Wo);
@@ -240,7 +254,8 @@ void conv_split_f32(const ConvArgs a) {
         const unsigned b = mdiv(p, a.mg_hw, a.sh_hw), rem = p - b * HW;
         const unsigned oh = mdiv(rem, a.mg_w, a.sh_w), ow = rem - oh * (unsigned)a.Wo;
         const int ih = (int)oh * a.stride + bq1[j], iw = (int)ow * a.stride + bq2[j];
-        const bool ok = (int)p < kend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const bool ok = (int)p < kend && (unsigned)ih < (unsigned)a.H &&
+                        (unsigned)iw < (unsigned)a.W && (!PB || tid + NT * j < LB);
         S.b[j] = bload(rb, ok ? bbase[j] + (unsigned)(((int)b * xs_b + ih * xs_h + iw * xs_w) * 4)
                               : kOOB);
         S.ok |= (unsigned)ok << (8 + j);
@@ -262,10 +277,13 @@ void conv_split_f32(const ConvArgs a) {
       }
       const int off = A_COL ? (idx / (BM / 4)) * (BM + 32) + 4 * (idx % (BM / 4))
                             : row_of(idx) * RLD + 4 * (idx & 3);
+      const bool act = !PA || idx < LA;
+      u16* dst = act ? As + off : dum;
+      const int pst = act ? A_PL : 4;
       uint2 pl[3];
       split_bf16<3>(v, pl);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) *(uint2*)(As + p * A_PL + off) = pl[p];
+      for (int p = 0; p < 3; ++p) *(uint2*)(dst + p * pst) = pl[p];
     }
 #pragma unroll
     for (int j = 0; j < NVB; ++j) {
@@ -274,10 +292,13 @@ void conv_split_f32(const ConvArgs a) {
       if constexpr (XBN && MODE == WGRAD) v = bn_relu(v, wsc, wsh, a.xrelu, (S.ok >> (8 + j)) & 1);
       const int off = B_COL ? (idx / (BN / 4)) * (BN + 32) + 4 * (idx % (BN / 4))
                             : row_of(idx) * RLD + 4 * (idx & 3);
+      const bool act = !PB || idx < LB;
+      u16* dst = act ? Bs + off : dum;
+      const int pst = act ? B_PL : 4;
       uint2 pl[3];
       split_bf16<3>(v, pl);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) *(uint2*)(Bs + p * B_PL + off) = pl[p];
+      for (int p = 0; p < 3; ++p) *(uint2*)(dst + p * pst) = pl[p];
     }
   };
 
@@ -389,11 +410,14 @@ static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
       return;
     }
   }
-  // 128 x 128 tiles run as eight waves of 32 x 64 (four per SIMD): measured 206 vs 223 ms of
-  // convs per bench step over four waves of 64 x 64 (MAUV_SPLIT_W8=0 restores those)
+  // eight-wave blocks (four waves per SIMD): 128 x 128 tiles as waves of 32 x 64, 128 x 64 and
+  // 64 x 128 as waves of 32 x 32 — measured 200 vs 235 ms of convs per bench step over four
+  // waves (MAUV_SPLIT_W8=0 restores those, 1 keeps four waves on the 64-wide tiles)
   static int w8 = -1;
-  if (w8 < 0) { const char* e8 = getenv("MAUV_SPLIT_W8"); w8 = e8 ? atoi(e8) : 1; }
+  if (w8 < 0) { const char* e8 = getenv("MAUV_SPLIT_W8"); w8 = e8 ? atoi(e8) : 2; }
   if (w8 && bm == 128 && bn == 128) { launch_split<MODE, 128, 128, XBN, 8>(a, oneacc, st); return; }
+  if (w8 == 2 && bm == 128 && bn == 64) { launch_split<MODE, 128, 64, XBN, 8>(a, oneacc, st); return; }
+  if (w8 == 2 && bm == 64 && bn == 128) { launch_split<MODE, 64, 128, XBN, 8>(a, oneacc, st); return; }
   if (bm == 64 && bn == 64) launch_split<MODE, 64, 64, XBN>(a, oneacc, st);
   else if (bm == 64) launch_split<MODE, 64, 128, XBN>(a, oneacc, st);
   else if (bn == 64) launch_split<MODE, 128, 64, XBN>(a, oneacc, st);
