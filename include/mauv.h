@@ -183,7 +183,9 @@ int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const float* ga
                       hipStream_t stream);
 /* statistics from per-m-tile partials written by mauv_conv2d_fwd_f32's epilogue: Chan merge,
  * mean/invstd/scale/shift [G][C], sequential running-stat update (run_* nullable);
- * workspace: G*C floats */
+ * workspace: mauv_bn_stats_workspace_floats(G, nblk, C) floats (G*C when nblk <= 512; larger
+ * partial counts are merged in segments) */
+long long mauv_bn_stats_workspace_floats(int G, int nblk, int C);
 int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, const float* pm2,
                            const float* pcnt, const float* gamma, const float* beta,
                            float* run_mean, float* run_var, float momentum, float eps,

@@ -159,6 +159,97 @@ __global__ __launch_bounds__(1024) void bn_stats_final(
   uvar_out[g * C + c] = (float)(nn > 1.0 ? mm / (nn - 1.0) : var);
 }
 
+// Large partial counts (an MC-batched inference chunk: tens of thousands of 128-row partials per
+// channel) are merged in two launches: stage 2a reduces segments of SEG partials per channel
+// exactly as above (two passes, double) into (count, mean, M2), stage 2b Chan-merges the
+// segments in order.  One segment (nblk <= SEG) keeps the single-launch path above.
+constexpr int SEG = 512;
+static inline int stat_segs(int nblk) { return (nblk + SEG - 1) / SEG; }
+
+__global__ __launch_bounds__(1024) void bn_stats_seg(int nblk, int C,
+                                                     const float* __restrict__ pmean,
+                                                     const float* __restrict__ pm2,
+                                                     const float* __restrict__ pcnt,
+                                                     double* __restrict__ seg) {
+  const int g = blockIdx.y, sg = blockIdx.z, S = gridDim.z;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int b0 = sg * SEG, b1 = min(nblk, b0 + SEG);
+  __shared__ double red[FIN_L][64];
+  double n = 0.0, s = 0.0;
+  if (c < C) {
+    for (int b = b0 + ty; b < b1; b += FIN_L) {
+      const double nb = pcnt[(long long)g * nblk + b];
+      n += nb;
+      s += nb * (double)pmean[((long long)g * nblk + b) * C + c];
+    }
+  }
+  const double nn = lane_sum16(n, red, tx, ty);
+  const double mu = nn > 0.0 ? lane_sum16(s, red, tx, ty) / nn : lane_sum16(s, red, tx, ty);
+  double q = 0.0;
+  if (c < C) {
+    for (int b = b0 + ty; b < b1; b += FIN_L) {
+      const long long o = ((long long)g * nblk + b) * C + c;
+      const double d = (double)pmean[o] - mu;
+      q += (double)pm2[o] + pcnt[(long long)g * nblk + b] * d * d;
+    }
+  }
+  const double mm = lane_sum16(q, red, tx, ty);
+  if (ty != 0 || c >= C) return;
+  double* o = seg + (((long long)g * S + sg) * C + c) * 3;
+  o[0] = nn;
+  o[1] = mu;
+  o[2] = mm;
+}
+
+__global__ __launch_bounds__(256) void bn_stats_merge(int G, int S, int C,
+                                                      const double* __restrict__ seg,
+                                                      const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, float eps,
+                                                      float* __restrict__ mean_out,
+                                                      float* __restrict__ invstd_out,
+                                                      float* __restrict__ scale_out,
+                                                      float* __restrict__ shift_out,
+                                                      float* __restrict__ uvar_out) {
+  const int g = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double nn = 0.0, mu = 0.0, mm = 0.0;
+  for (int s = 0; s < S; ++s) {
+    const double* o = seg + (((long long)g * S + s) * C + c) * 3;
+    chan_merge(nn, mu, mm, o[0], o[1], o[2]);
+  }
+  const double var = mm / nn;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * invstd;
+  mean_out[g * C + c] = (float)mu;
+  invstd_out[g * C + c] = invstd;
+  scale_out[g * C + c] = sc;
+  shift_out[g * C + c] = beta[c] - (float)mu * sc;
+  uvar_out[g * C + c] = (float)(nn > 1.0 ? mm / (nn - 1.0) : var);
+}
+
+// stage 2 dispatch: ws holds uvar [G][C] floats, then (segmented path) the segment triples
+static void stats_final(int G, int nblk, int C, const float* pmean, const float* pm2,
+                        const float* pcnt, const float* gamma, const float* beta, float eps,
+                        float* mean, float* invstd, float* scale, float* shift, float* ws,
+                        hipStream_t stream) {
+  const int S = stat_segs(nblk);
+  if (S == 1) {
+    hipLaunchKernelGGL(bn_stats_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, nblk, C,
+                       pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift, ws);
+    return;
+  }
+  double* seg = (double*)(((uintptr_t)(ws + (long long)G * C) + 7) & ~(uintptr_t)7);
+  hipLaunchKernelGGL(bn_stats_seg, dim3((C + 63) / 64, G, S), dim3(1024), 0, stream, nblk, C,
+                     pmean, pm2, pcnt, seg);
+  hipLaunchKernelGGL(bn_stats_merge, dim3((C + 255) / 256, G), dim3(256), 0, stream, G, S, C, seg,
+                     gamma, beta, eps, mean, invstd, scale, shift, ws);
+}
+static long long stats_ws_floats(int G, int nblk, int C) {
+  const int S = stat_segs(nblk);
+  return (long long)G * C + (S > 1 ? 6LL * G * S * C + 2 : 0);
+}
+
 // Stage 3: the G running-stat updates, in MC-sample order (= G sequential forward calls).
 __global__ void bn_running_kernel(int G, int C, const float* __restrict__ mean,
                                   const float* __restrict__ uvar, float* __restrict__ run_mean,
@@ -400,7 +491,12 @@ MAUV_API int mauv_bn_eval_params(int G, int C, const float* gamma, const float* 
 MAUV_API long long mauv_bn_workspace_floats(int G, long long M, int C) {
   int nblk, rpb;
   reduce_geometry(M, C, nblk, rpb);
-  return (long long)G * nblk * (2LL * C + 1) + 3LL * G * C;
+  return (long long)G * nblk * (2LL * C + 1) + 2LL * G * C + stats_ws_floats(G, nblk, C);
+}
+
+// Workspace floats of mauv_bn_stats_finalize for nblk partials per channel.
+MAUV_API long long mauv_bn_stats_workspace_floats(int G, int nblk, int C) {
+  return stats_ws_floats(G, nblk, C);
 }
 
 // Training-mode BN forward for G groups: statistics (mean/invstd/scale/shift out, [G][C]),
@@ -420,8 +516,8 @@ MAUV_API int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const 
   hipLaunchKernelGGL(bn_stats_partial, dim3(nblk, G), dim3(256), 0, stream, y, M, C, rpb, rm,
                      pmean, pm2, pcnt);
   float* uvar = pcnt + (long long)G * nblk;
-  hipLaunchKernelGGL(bn_stats_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, nblk, C,
-                     pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift, uvar);
+  stats_final(G, nblk, C, pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift, uvar,
+              stream);
   if (run_mean && run_var)
     hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
                        mean, uvar, run_mean, run_var, momentum);
@@ -439,8 +535,8 @@ MAUV_API int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, 
                                     float* workspace, float* mean, float* invstd, float* scale,
                                     float* shift, hipStream_t stream) {
   if (G <= 0 || nblk <= 0 || C <= 0) { set_error("bn_stats_finalize: bad shape"); return kErrArg; }
-  hipLaunchKernelGGL(bn_stats_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, nblk, C,
-                     pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift, workspace);
+  stats_final(G, nblk, C, pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift,
+              workspace, stream);
   if (run_mean && run_var)
     hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
                        mean, workspace, run_mean, run_var, momentum);

@@ -50,6 +50,7 @@ SIGNATURES = {
     "mauv_bn_workspace_floats": [I, LL, I],
     "mauv_bn_fwd_train": [P, I, LL, I, P, P, P, P, F, F, P, P, P, P, P, P, I, P, P],
     "mauv_bn_stats_finalize": [I, I, I, P, P, P, P, P, P, P, F, F, P, P, P, P, P, P],
+    "mauv_bn_stats_workspace_floats": [I, I, I],
     "mauv_bn_apply": [P, P, P, P, P, P, I, P, I, LL, I, P],
     "mauv_bn_eval_params": [I, I, P, P, P, P, F, P, P, P],
     "mauv_bn_bwd": [P, P, P, I, P, P, P, P, I, LL, I, P, P, P, P, P, P, P, I, P],
@@ -77,7 +78,8 @@ SIGNATURES = {
     "mauv_mc_finalize": [P, I, I, I, F, P, P, P, P, P, P],
     "mauv_nonfinite_count": [P, LL, P, P],
 }
-_RESTYPES = {"mauv_last_error": ctypes.c_char_p, "mauv_bn_workspace_floats": LL}
+_RESTYPES = {"mauv_last_error": ctypes.c_char_p, "mauv_bn_workspace_floats": LL,
+             "mauv_bn_stats_workspace_floats": LL}
 
 
 class MauvError(RuntimeError):

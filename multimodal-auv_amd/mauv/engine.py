@@ -325,7 +325,7 @@ class TrunkRunner(_Runner):
                 raise NotImplementedError("mauv: cumulative-average BN (momentum=None)")
             track = bn.training and bn.track_running_stats
             pm, pm2, pcnt, nblk = part
-            ws = torch.empty(G * C, device=y.device)
+            ws = torch.empty(ops.bn_stats_workspace_floats(G, nblk, C), device=y.device)
             ops.bn_stats_finalize(G, nblk, C, pm, pm2, pcnt, bn.weight, bn.bias,
                                   bn.running_mean if track else None,
                                   bn.running_var if track else None, bn.momentum, bn.eps, ws,

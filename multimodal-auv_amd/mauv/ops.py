@@ -263,6 +263,10 @@ def bn_eval_params(G, C, gamma, beta, run_mean, run_var, eps, scale, shift):
                                   _p(scale), _p(shift), stream()), "bn_eval_params")
 
 
+def bn_stats_workspace_floats(G, nblk, C):
+    return int(lib.mauv_bn_stats_workspace_floats(G, nblk, C))
+
+
 def bn_stats_finalize(G, nblk, C, pmean, pm2, pcnt, gamma, beta, run_mean, run_var, momentum,
                       eps, ws, mean, invstd, scale, shift):
     check(lib.mauv_bn_stats_finalize(G, nblk, C, _p(pmean), _p(pm2), _p(pcnt), _p(gamma),

@@ -360,3 +360,38 @@ def test_fused_adam_matches_torch_adam():
     ob2.load_state_dict(oa.state_dict())
     for p, q in zip(pa, pb):
         close(ob2.state[q]["exp_avg_sq"], oa.state[p]["exp_avg_sq"], rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.parametrize("nblk", [37, 1500])
+def test_bn_stats_finalize_segmented(nblk):
+    """Per-128-row partials (count, mean, M2) merged into batch statistics: one launch up to
+    512 partials per channel, segmented two-stage Chan merge beyond (MC-batched inference
+    chunks reach tens of thousands) — vs float64 statistics of the full data."""
+    from mauv import ops
+    G, C, rows = 2, 64, 128
+    torch.manual_seed(4)
+    M = nblk * rows - 57                                   # ragged last partial
+    y = torch.randn(G, M, C, dtype=torch.float64) * 3 + torch.linspace(-5, 5, C, dtype=torch.float64)
+    cnt = torch.full((nblk,), float(rows), dtype=torch.float64)
+    cnt[-1] = rows - 57
+    pm = torch.empty(G, nblk, C, dtype=torch.float64)
+    p2 = torch.empty(G, nblk, C, dtype=torch.float64)
+    for b in range(nblk):
+        blk = y[:, b * rows:min(M, (b + 1) * rows)]
+        pm[:, b] = blk.mean(1)
+        p2[:, b] = ((blk - blk.mean(1, keepdim=True)) ** 2).sum(1)
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    ws = torch.empty(ops.bn_stats_workspace_floats(G, nblk, C), device=dev)
+    st = torch.empty(4, G, C, device=dev)
+    ops.bn_stats_finalize(G, nblk, C, pm.float().to(dev), p2.float().to(dev),
+                          cnt.float().expand(G, nblk).contiguous().to(dev), gamma.to(dev),
+                          beta.to(dev), rm, rv, 0.1, 1e-5, ws, st[0], st[1], st[2], st[3])
+    mean, var = y.mean(1), y.var(1, unbiased=False)
+    close(st[0], mean, rtol=1e-6, atol=1e-6)
+    close(st[1], 1.0 / torch.sqrt(var + 1e-5), rtol=1e-6, atol=0)
+    uvar = y.var(1, unbiased=True)
+    ref_rv = torch.ones(C, dtype=torch.float64)
+    for g in range(G):
+        ref_rv = 0.9 * ref_rv + 0.1 * uvar[g]
+    close(rv, ref_rv, rtol=1e-6, atol=1e-6)
