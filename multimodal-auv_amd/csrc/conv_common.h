@@ -61,6 +61,9 @@ inline void magic_div(unsigned d, unsigned long long& m, int& s) {
 // Launch the pipelined split-fp32 kernel (conv_split.hip) for an fp32 conv; false when the
 // problem is outside its vector paths (the caller then runs conv_gemm.hip's kernels).
 bool conv_split_launch(int mode, const ConvArgs& a, int oneacc, hipStream_t st);
+// pipelined 16-bit kernels (conv_pipe16.hip); x/w/dy/out/addend hold 16-bit data of type dt
+// (DT_BF16 / DT_F16), WGRAD out stays fp32 slabs; false: shape not covered
+bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
 
 __device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int relu) {
   v = v * sc + sh;

@@ -26,7 +26,7 @@
 // 256 threads = 4 waves (2x2), wave tile (BM/2)x(BN/2) = 2x2 MFMA tiles of 32x32.
 #include <stdlib.h>
 
-#include "h16.h"
+#include "conv_common.h"
 
 namespace mauv {
 
@@ -498,6 +498,22 @@ static ConvArgs16 make_args16(int G, int B, int H, int W, int Cin, int Cout, int
   return a;
 }
 
+// the pipelined kernels (conv_pipe16.hip) take the fp32 argument block with 16-bit pointers
+static ConvArgs pipe_args(const ConvArgs16& h) {
+  ConvArgs a{};
+  a.B = h.B; a.H = h.H; a.W = h.W; a.Cin = h.Cin; a.Ho = h.Ho; a.Wo = h.Wo; a.Cout = h.Cout;
+  a.R = h.R; a.S = h.S; a.stride = h.stride; a.pad = h.pad;
+  a.xs_g = h.xs_g; a.xs_b = h.xs_b; a.xs_h = h.xs_h; a.xs_w = h.xs_w; a.xs_c = 1;
+  a.x = (const float*)h.x; a.w = (const float*)h.w; a.ws_g = h.ws_g; a.dy = (const float*)h.dy;
+  a.out = (float*)h.out; a.out_sg = h.out_sg; a.addend = (const float*)h.addend;
+  a.accumulate = h.accumulate; a.G = h.G; a.splits = h.splits; a.kchunk = h.kchunk;
+  a.M = h.M; a.N = h.N; a.K = h.K;
+  a.ph = h.ph; a.pw = h.pw; a.Hc = h.Hc; a.Wc = h.Wc; a.r0 = h.r0; a.s0 = h.s0; a.nr = h.nr;
+  a.ns = h.ns; a.xsc = h.xsc; a.xsh = h.xsh; a.xrelu = h.xrelu;
+  a.st_mean = h.st_mean; a.st_m2 = h.st_m2; a.st_cnt = h.st_cnt; a.st_nblk = h.st_nblk;
+  return a;
+}
+
 static int check_shape16(const char* what, int dt, int G, int B, int Cin, int Cout,
                          const long long* xs) {
   if (dt != DT_BF16 && dt != DT_F16) { set_error(std::string(what) + ": dtype must be 0 (bf16) or 1 (f16)"); return kErrArg; }
@@ -528,7 +544,8 @@ MAUV_API int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_st
   a.out_sg = (long long)a.M * a.N;
   a.st_mean = st_mean; a.st_m2 = st_m2; a.st_cnt = st_cnt;
   a.st_nblk = ceil_div(a.M, conv_tile_rows(a.M));
-  if (Cin % HBK == 0) dispatch16<H_FWD, true>(dtype, a, stream);
+  if (conv_pipe16_launch(FWD, dtype, pipe_args(a), stream)) {}
+  else if (Cin % HBK == 0) dispatch16<H_FWD, true>(dtype, a, stream);
   else dispatch16<H_FWD, false>(dtype, a, stream);
   return check_launch("conv2d_fwd_h16");
 }
@@ -556,7 +573,8 @@ MAUV_API int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, 
       a.M = B * a.Hc * a.Wc;
       a.K = a.nr * a.ns * Cout;
       if (a.M <= 0) continue;
-      dispatch16<H_DGRAD, true>(dtype, a, stream);
+      if (!conv_pipe16_launch(DGRAD, dtype, pipe_args(a), stream))
+        dispatch16<H_DGRAD, true>(dtype, a, stream);
     }
   return check_launch("conv2d_bwd_data_h16");
 }
@@ -572,7 +590,9 @@ MAUV_API int mauv_conv2d_bwd_weight_h16(int dtype, const void* x, const long lon
   a.xsc = x_scale; a.xsh = x_shift; a.xrelu = x_relu;
   a.M = Cout; a.N = R * S * Cin; a.K = B * a.Ho * a.Wo;
   a.splits = splits;
+  ConvArgs p = pipe_args(a);
+  p.kchunk = ((a.K + splits - 1) / splits + 63) / 64 * 64;  // the pipelined kernel's BK
   a.kchunk = ((a.K + splits - 1) / splits + HBK - 1) / HBK * HBK;
-  dispatch16<H_WGRAD, false>(dtype, a, stream);
+  if (!conv_pipe16_launch(WGRAD, dtype, p, stream)) dispatch16<H_WGRAD, false>(dtype, a, stream);
   return check_launch("conv2d_bwd_weight_h16");
 }

@@ -1,0 +1,482 @@
+// Pipelined 16-bit implicit-GEMM convolution (bf16 training, BASELINE configs[2]; f16 MC
+// inference under the reference predictor's torch.amp.autocast, inference/predictors.py:55):
+// the three GEMM views of conv_gemm16.hip with the staging structure of the split-fp32 kernel
+// (conv_split.hip):
+//  * tiles BM x BN x 64 (one (r, s) tap per stage), eight waves per 128-wide block;
+//  * two tiles in flight: stage t issues the 16-byte buffer loads of tile t+2, runs the MFMAs of
+//    tile t (four v_mfma_f32_32x32x16 k-steps) from one LDS buffer and writes tile t+1 into the
+//    other — one branch-free basic block per stage;
+//  * raw buffer loads with 32-bit offsets (an offset past the descriptor range returns 0:
+//    padding, ragged tiles and tiles past K need no branches);
+//  * the producing layer's pending BN(+ReLU) applied when the staged chunk is written to LDS
+//    (forward: scale/shift of the input channels staged in LDS once per block).
+// LDS images as conv_gemm16.hip: k-contiguous operands (FWD A/B, DGRAD A) as row images
+// [rows][72] (ds_read_b128 fragments, conflict-free 144-B rows), k-strided operands (DGRAD B,
+// WGRAD A/B) as col images [64][rows+32] (ds_read_b64_tr_b16).  Epilogues: FWD statistics from
+// the fp32 accumulators and 16-bit rows staged through LDS (DGRAD: + addend / accumulate, parity
+// class row remap); WGRAD fp32 split-K slabs (conv_common.h).
+#include <stdlib.h>
+
+#include "conv_common.h"
+
+namespace mauv {
+
+namespace {
+
+constexpr unsigned kOOB16 = 0x7ffffff0u;  // beyond every descriptor range: the load returns 0
+constexpr int kMaxXbn16 = 512;             // FWD pending-BN input channels staged in LDS
+
+__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc16(const void* p, long long nelem) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(nelem * 2), 0x00020000);
+}
+__device__ __forceinline__ unsigned mdiv16(unsigned n, unsigned long long m, int s) {
+  return (unsigned)(((unsigned long long)n * m) >> s);
+}
+template <int DT>
+__device__ __forceinline__ u32x4 bn_relu8(u32x4 v, floatx8 sc, floatx8 sh, int relu, bool ok) {
+  floatx8 f = unpack8<DT>(v);
+  f = f * sc + sh;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = (!ok || (relu && !(f[e] > 0.f))) ? 0.f : f[e];
+  return pack8<DT>(f);
+}
+
+template <int NVA, int NVB>
+struct Stage16 {
+  u32x4 a[NVA], b[NVB];
+  unsigned ok;  // validity bits of pending-BN chunks: a j -> bit j, b j -> bit 8 + j
+  int tc;       // FWD: input-channel offset of this stage's k slice
+};
+
+}  // namespace
+
+// 2 x 2 waves (64 x 64 each) for 64-wide tiles, 4 x 2 / 2 x 4 waves of 32 x 64 / 64 x 32 for
+// 128 x 128, 4 x 2 / 2 x 4 of 32 x 32 for 128 x 64 / 64 x 128 (eight waves: four per SIMD).
+template <int BM, int BN>
+struct Waves16 {
+  static constexpr bool W8 = BM + BN >= 192;
+  static constexpr int M = W8 ? (BM == 128 ? 4 : 2) : 2, N = W8 ? (BM == 128 ? 2 : 4) : 2;
+  static constexpr int T = 64 * M * N;
+};
+
+template <int MODE, int DT, int BM, int BN, bool XBN>
+__global__ __launch_bounds__((Waves16<BM, BN>::T)) __attribute__((amdgpu_waves_per_eu(4)))
+void conv_pipe16(const ConvArgs a) {
+  constexpr int BK = 64, EPC = 8, KQ = BK / EPC;
+  constexpr int WGM = Waves16<BM, BN>::M, WGN = Waves16<BM, BN>::N, NT = Waves16<BM, BN>::T;
+  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
+  // 16-byte chunks per stage per operand (LA, LB) and per thread; with LB < NT the threads
+  // tid >= LB load nothing and park their chunk in a dummy LDS slot (branch-free stage)
+  constexpr int LA = BM * KQ, LB = BN * KQ;
+  constexpr int NVA = (LA + NT - 1) / NT, NVB = (LB + NT - 1) / NT;
+  constexpr bool PA = LA % NT != 0, PB = LB % NT != 0;
+  constexpr bool A_COL = (MODE == WGRAD), B_COL = (MODE != FWD);
+  constexpr int RLD = BK + 8;
+  constexpr int A_SZ = A_COL ? BK * (BM + 32) : BM * RLD;  // 16-bit words
+  constexpr int B_SZ = B_COL ? BK * (BN + 32) : BN * RLD;
+  constexpr int STG = A_SZ + B_SZ;
+  constexpr int XS = (XBN && MODE == FWD) ? 2 * kMaxXbn16 : 0;  // floats
+  constexpr int DUM = (PA || PB) ? 8 * NT : 0;                 // dummy chunk slots (16-bit)
+  static_assert(2 * STG >= 2 * WM * (BN + 4) && 2 * STG >= 8 * WGM * BN, "epilogue scratch");
+  __shared__ __attribute__((aligned(16))) u16 smem[2 * STG + 2 * XS + DUM];
+  float* xbn = (float*)(smem + 2 * STG);
+  u16* dum = smem + 2 * STG + 2 * XS + 8 * threadIdx.x;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
+  int m0, n0;
+  {  // XCD-aware tile order (conv_gemm.hip)
+    const int nN = (a.N + BN - 1) / BN;
+    const int b = blockIdx.x, nwg = gridDim.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    m0 = (L / nN) * BM;
+    n0 = (L - (L / nN) * nN) * BN;
+  }
+  int g, sp = 0;
+  if constexpr (MODE == WGRAD) { g = blockIdx.y / a.splits; sp = blockIdx.y % a.splits; }
+  else g = blockIdx.y;
+  int kbeg = 0, kend = a.K;
+  if constexpr (MODE == WGRAD) { kbeg = sp * a.kchunk; kend = min(a.K, kbeg + a.kchunk); }
+  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const long long ny = (long long)a.B * a.Ho * a.Wo * a.Cout;  // dy elements per group
+  const u16* xg = (const u16*)a.x + (long long)g * a.xs_g;
+  const u16* wg = (const u16*)a.w + (long long)g * a.ws_g;
+  const u16* dyg = (const u16*)a.dy + (long long)g * ny;
+  __amdgpu_buffer_rsrc_t ra, rb;
+  if constexpr (MODE == FWD) { ra = rsrc16(xg, a.B * a.xs_b); rb = rsrc16(wg, a.ws_g); }
+  else if constexpr (MODE == DGRAD) { ra = rsrc16(dyg, ny); rb = rsrc16(wg, a.ws_g); }
+  else { ra = rsrc16(dyg, ny); rb = rsrc16(xg, a.B * a.xs_b); }
+  const int xs_h = (int)a.xs_h, xs_w = (int)a.xs_w, xs_b = (int)a.xs_b;
+
+  // ---- per-thread loader constants ----
+  unsigned abase[NVA], bbase[NVB];
+  int aq0[NVA], aq1[NVA];
+  int bq0[NVB], bq1[NVB], bq2[NVB];
+  floatx8 wsc, wsh;  // WGRAD pending BN of x (per-thread channel chunk)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { wsc[e] = 1.f; wsh[e] = 0.f; }
+  const int kq = tid % KQ;
+#pragma unroll
+  for (int j = 0; j < NVA; ++j) {
+    const int idx = tid + NT * j;
+    if constexpr (MODE == FWD || MODE == DGRAD) {
+      const int m = m0 + idx / KQ;
+      const bool ok = m < a.M && (!PA || idx < LA);
+      const int mm = m < a.M ? m : 0;
+      if constexpr (MODE == FWD) {
+        const int HW = a.Ho * a.Wo, b = mm / HW, rem = mm - b * HW;
+        const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+        const int p0 = oh * a.stride - a.pad, p1 = ow * a.stride - a.pad;
+        abase[j] = (unsigned)((b * xs_b + p0 * xs_h + p1 * xs_w + EPC * kq) * 2);
+        aq0[j] = ok ? p0 : -(1 << 28);
+        aq1[j] = p1;
+      } else {
+        const int HW = a.Hc * a.Wc, b = mm / HW, rem = mm - b * HW;
+        const int i = rem / a.Wc, jj = rem - i * a.Wc;
+        const int q0 = i + (a.ph + a.pad - a.r0) / a.stride;
+        const int q1 = jj + (a.pw + a.pad - a.s0) / a.stride;
+        abase[j] = (unsigned)(((b * a.Ho * a.Wo + q0 * a.Wo + q1) * a.Cout + EPC * kq) * 2);
+        aq0[j] = ok ? q0 : (1 << 28);
+        aq1[j] = q1;
+      }
+    } else {  // WGRAD A: 8 consecutive couts at k row idx / (BM/8)
+      const int co = m0 + EPC * (idx % (BM / EPC)), kr = idx / (BM / EPC);
+      abase[j] = (co < a.M && (!PA || idx < LA)) ? (unsigned)((kr * a.Cout + co) * 2) : kOOB16;
+      aq0[j] = kr;
+      aq1[j] = 0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NVB; ++j) {
+    const int idx = tid + NT * j;
+    if constexpr (MODE == FWD) {
+      const int n = n0 + idx / KQ;
+      bbase[j] = (n < a.N && (!PB || idx < LB)) ? (unsigned)((n * a.K + EPC * kq) * 2) : kOOB16;
+    } else if constexpr (MODE == DGRAD) {
+      const int c = n0 + EPC * (idx % (BN / EPC)), kr = idx / (BN / EPC);
+      bbase[j] = (c < a.N && (!PB || idx < LB)) ? (unsigned)((kr * a.R * a.S * a.Cin + c) * 2)
+                                                 : kOOB16;
+    } else {  // WGRAD B: fixed column chunk (r, s, c..c+7), pixel row idx / (BN/8)
+      const int col = n0 + EPC * (idx % (BN / EPC));
+      const bool ok = col < a.N && (!PB || idx < LB);
+      const int cc = ok ? col : 0, rs = cc / a.Cin, c = cc - rs * a.Cin;
+      const int r = rs / a.S, s = rs - r * a.S;
+      bq0[j] = idx / (BN / EPC);
+      bq1[j] = ok ? r - a.pad : -(1 << 28);
+      bq2[j] = s - a.pad;
+      bbase[j] = (unsigned)(c * 2);
+      if constexpr (XBN) {
+        if (j == 0) {
+          wsc = ldf8(a.xsc + g * a.Cin + c);
+          wsh = ldf8(a.xsh + g * a.Cin + c);
+        }
+      }
+    }
+  }
+  if constexpr (XBN && MODE == FWD) {
+    for (int i = tid; i < a.Cin; i += NT) {
+      xbn[i] = a.xsc[g * a.Cin + i];
+      xbn[kMaxXbn16 + i] = a.xsh[g * a.Cin + i];
+    }
+  }
+
+  int t_r = 0, t_s = 0, t_c = 0;  // tile-uniform k position (FWD: r, s, cin; DGRAD: tr, ts, cout)
+  typedef Stage16<NVA, NVB> St;
+
+  auto load = [&](St& S, int t) {
+    const int k0 = kbeg + t * BK;
+    const bool sok = k0 < kend;  // stage-uniform for FWD / DGRAD (K % 64 == 0)
+    if constexpr (MODE == FWD) {
+      const unsigned soff = (unsigned)((t_r * xs_h + t_s * xs_w + t_c) * 2);
+      S.ok = 0;
+      S.tc = t_c;
+#pragma unroll
+      for (int j = 0; j < NVA; ++j) {
+        const bool ok = sok && (unsigned)(aq0[j] + t_r) < (unsigned)a.H &&
+                        (unsigned)(aq1[j] + t_s) < (unsigned)a.W;
+        S.a[j] = bload16(ra, ok ? abase[j] + soff : kOOB16);
+        S.ok |= (unsigned)ok << j;
+      }
+#pragma unroll
+      for (int j = 0; j < NVB; ++j) S.b[j] = bload16(rb, sok ? bbase[j] + (unsigned)(k0 * 2) : kOOB16);
+      t_c += BK;
+      if (t_c >= a.Cin) { t_c = 0; if (++t_s == a.S) { t_s = 0; ++t_r; } }
+    } else if constexpr (MODE == DGRAD) {
+      const unsigned soff = (unsigned)((t_c - (t_r * a.Wo + t_s) * a.Cout) * 2);
+#pragma unroll
+      for (int j = 0; j < NVA; ++j) {
+        const bool ok = sok && (unsigned)(aq0[j] - t_r) < (unsigned)a.Ho &&
+                        (unsigned)(aq1[j] - t_s) < (unsigned)a.Wo;
+        S.a[j] = bload16(ra, ok ? abase[j] + soff : kOOB16);
+      }
+      const int r = a.r0 + a.stride * t_r, s = a.s0 + a.stride * t_s;
+      const unsigned woff = (unsigned)(((t_c * a.R + r) * a.S + s) * a.Cin * 2);
+#pragma unroll
+      for (int j = 0; j < NVB; ++j) S.b[j] = bload16(rb, sok ? bbase[j] + woff : kOOB16);
+      t_c += BK;
+      if (t_c >= a.Cout) { t_c = 0; if (++t_s == a.ns) { t_s = 0; ++t_r; } }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NVA; ++j) {
+        const bool ok = k0 + aq0[j] < kend;
+        S.a[j] = bload16(ra, ok ? abase[j] + (unsigned)(k0 * a.Cout * 2) : kOOB16);
+      }
+      const unsigned HW = (unsigned)(a.Ho * a.Wo);
+      S.ok = 0;
+#pragma unroll
+      for (int j = 0; j < NVB; ++j) {
+        const unsigned p = (unsigned)(k0 + bq0[j]);
+        const unsigned b = mdiv16(p, a.mg_hw, a.sh_hw), rem = p - b * HW;
+        const unsigned oh = mdiv16(rem, a.mg_w, a.sh_w), ow = rem - oh * (unsigned)a.Wo;
+        const int ih = (int)oh * a.stride + bq1[j], iw = (int)ow * a.stride + bq2[j];
+        const bool ok = (int)p < kend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        S.b[j] = bload16(rb, ok ? bbase[j] + (unsigned)(((int)b * xs_b + ih * xs_h + iw * xs_w) * 2)
+                                : kOOB16);
+        S.ok |= (unsigned)ok << (8 + j);
+      }
+    }
+  };
+
+  auto store = [&](const St& S, int buf) {
+    u16* As = smem + buf * STG;
+    u16* Bs = As + A_SZ;
+#pragma unroll
+    for (int j = 0; j < NVA; ++j) {
+      const int idx = tid + NT * j;
+      u32x4 v = S.a[j];
+      if constexpr (XBN && MODE == FWD) {
+        const int c = S.tc + EPC * kq;
+        v = bn_relu8<DT>(v, ldf8(xbn + c), ldf8(xbn + kMaxXbn16 + c), a.xrelu, (S.ok >> j) & 1);
+      }
+      const int off = A_COL ? (idx / (BM / EPC)) * (BM + 32) + EPC * (idx % (BM / EPC))
+                            : (idx / KQ) * RLD + EPC * (idx % KQ);
+      *(u32x4*)((!PA || idx < LA) ? As + off : dum) = v;
+    }
+#pragma unroll
+    for (int j = 0; j < NVB; ++j) {
+      const int idx = tid + NT * j;
+      u32x4 v = S.b[j];
+      if constexpr (XBN && MODE == WGRAD) v = bn_relu8<DT>(v, wsc, wsh, a.xrelu, (S.ok >> (8 + j)) & 1);
+      const int off = B_COL ? (idx / (BN / EPC)) * (BN + 32) + EPC * (idx % (BN / EPC))
+                            : (idx / KQ) * RLD + EPC * (idx % KQ);
+      *(u32x4*)((!PB || idx < LB) ? Bs + off : dum) = v;
+    }
+  };
+
+  floatx16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  auto compute = [&](int buf) {
+    const u16* As = smem + buf * STG;
+    const u16* Bs = As + A_SZ;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      u32x4 af[MI], bq[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        if constexpr (A_COL) af[mi] = col_frag(As, BM + 32, wm * WM + mi * 32, s, lane);
+        else af[mi] = row_frag_ld<RLD>(As, wm * WM + mi * 32, s, li, lh);
+      }
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        if constexpr (B_COL) bq[ni] = col_frag(Bs, BN + 32, wn * WN + ni * 32, s, lane);
+        else bq[ni] = row_frag_ld<RLD>(Bs, wn * WN + ni * 32, s, li, lh);
+      }
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = H16<DT>::mfma(af[mi], bq[ni], acc[mi][ni]);
+    }
+  };
+
+  // ---- pipeline: buffer 0 <- tile 0, registers S1 <- tile 1 ----
+  St S0, S1;
+  load(S0, 0);
+  load(S1, 1);
+  if constexpr (XBN && MODE == FWD) __syncthreads();  // xbn staged
+  store(S0, 0);
+  __syncthreads();
+  for (int t = 0; t < nt; t += 2) {
+    load(S0, t + 2);
+    compute(0);
+    store(S1, 1);
+    __syncthreads();
+    load(S1, t + 3);  // (odd nt: one all-zero tile rather than a branch out of the pair)
+    compute(1);
+    store(S0, 0);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  if constexpr (MODE == WGRAD) {
+    conv_epilogue<WGRAD, BM, BN, MI, NI, WGM, WGN>(a, acc, (float*)smem, tid, m0, n0, g, sp);
+    return;
+  }
+  float* red = (float*)smem;  // LDS is free: the main loop ended with a barrier
+  if (MODE == FWD && a.st_mean) {
+    // per-tile BN statistics of y from the fp32 accumulators (tile mean, then M2 around it)
+    const int nvalid = min(BM, a.M - m0);
+    const int tcol = wn * WN + li;
+    float s1[NI], s2[NI], mean[NI];
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) { s1[ni] = 0.f; s2[ni] = 0.f; }
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row < a.M) s1[ni] += acc[mi][ni][r];
+        }
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) s1[ni] += __shfl_xor(s1[ni], 32, 64);
+    if (lh == 0) {
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) red[wm * BN + tcol + ni * 32] = s1[ni];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WGM; ++w) t += red[w * BN + tcol + ni * 32];
+      mean[ni] = t / (float)nvalid;
+    }
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row < a.M) {
+            const float d = acc[mi][ni][r] - mean[ni];
+            s2[ni] += d * d;
+          }
+        }
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) s2[ni] += __shfl_xor(s2[ni], 32, 64);
+    if (lh == 0) {
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) red[WGM * BN + wm * BN + tcol + ni * 32] = s2[ni];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N) {
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WGM; ++w) { t1 += red[w * BN + tid]; t2 += red[WGM * BN + w * BN + tid]; }
+      const int mt = m0 / BM;
+      const long long so = ((long long)g * a.st_nblk + mt) * a.N + n0 + tid;
+      a.st_mean[so] = t1 / (float)nvalid;
+      a.st_m2[so] = t2;
+      if (n0 + tid == 0) a.st_cnt[(long long)g * a.st_nblk + mt] = (float)nvalid;
+    }
+    __syncthreads();  // red is overwritten by the staged store below
+  }
+  // 16-bit output through LDS: each wave row wm in turn parks its fp32 accumulators as a
+  // [WM][BN+4] tile, then all threads write 16-byte rows of 8 channels (residual addend /
+  // previous dx added in fp32, one rounding)
+  constexpr int SLD = BN + 4, CPR = BN / 8, NCH = WM * CPR;
+  float* stile = (float*)smem;
+  u16* outp = (u16*)a.out;
+  const u16* addp = (const u16*)a.addend;
+#pragma unroll
+  for (int pass = 0; pass < WGM; ++pass) {
+    if (wm == pass) {
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            stile[(mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SLD + wn * WN + ni * 32 + li] =
+                acc[mi][ni][r];
+    }
+    __syncthreads();
+    for (int c = tid; c < NCH; c += NT) {
+      const int rl = c / CPR, cc = c - rl * CPR;
+      const int row = m0 + pass * WM + rl, col = n0 + 8 * cc;
+      if (row >= a.M || col >= a.N) continue;
+      const floatx4 v0 = *(const floatx4*)(stile + rl * SLD + 8 * cc);
+      const floatx4 v1 = *(const floatx4*)(stile + rl * SLD + 8 * cc + 4);
+      floatx8 f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { f[e] = v0[e]; f[4 + e] = v1[e]; }
+      long long orow = row;
+      if constexpr (MODE == DGRAD) {
+        if (a.stride != 1) {
+          const int HW = a.Hc * a.Wc, b = row / HW, rem = row - b * HW;
+          const int i = rem / a.Wc, jj = rem - i * a.Wc;
+          orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
+        }
+      }
+      const long long o = (long long)g * a.out_sg + orow * a.N + col;
+      if constexpr (MODE == DGRAD) {
+        if (addp) f += unpack8<DT>(*(const u32x4*)(addp + o));
+        if (a.accumulate) f += unpack8<DT>(*(const u32x4*)(outp + o));
+      }
+      *(u32x4*)(outp + o) = pack8<DT>(f);
+    }
+    __syncthreads();
+  }
+}
+
+template <int MODE, int DT, int BM, int BN, bool XBN>
+static void launch_pipe16(const ConvArgs& a, hipStream_t st) {
+  dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
+  hipLaunchKernelGGL((conv_pipe16<MODE, DT, BM, BN, XBN>), grid, dim3(Waves16<BM, BN>::T), 0, st,
+                     a);
+}
+
+template <int MODE, int DT, bool XBN>
+static void pipe16_tiles(const ConvArgs& a, hipStream_t st) {
+  const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
+  if (bm == 64 && bn == 64) launch_pipe16<MODE, DT, 64, 64, XBN>(a, st);
+  else if (bm == 64) launch_pipe16<MODE, DT, 64, 128, XBN>(a, st);
+  else if (bn == 64) launch_pipe16<MODE, DT, 128, 64, XBN>(a, st);
+  else launch_pipe16<MODE, DT, 128, 128, XBN>(a, st);
+}
+
+template <int MODE, bool XBN>
+static void pipe16_dt(int dt, const ConvArgs& a, hipStream_t st) {
+  if (dt == DT_BF16) pipe16_tiles<MODE, DT_BF16, XBN>(a, st);
+  else pipe16_tiles<MODE, DT_F16, XBN>(a, st);
+}
+
+bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
+  static int on = -1;  // MAUV_PIPE16=0 keeps conv_gemm16.hip's kernels (A/B measurements)
+  if (on < 0) { const char* e = getenv("MAUV_PIPE16"); on = e ? atoi(e) : 1; }
+  if (!on) return false;
+  const long long lim = 0x7fff0000LL / 2;  // elements addressable by a 31-bit byte offset
+  const long long nx = (long long)a0.B * a0.xs_b, ny = (long long)a0.B * a0.Ho * a0.Wo * a0.Cout;
+  if (nx > lim || ny > lim || a0.ws_g > lim) return false;
+  const bool xs8 = a0.xs_w % 8 == 0 && a0.xs_h % 8 == 0 && a0.xs_b % 8 == 0 && a0.xs_g % 8 == 0;
+  ConvArgs a = a0;
+  if (mode == FWD) {
+    if (a.Cin % 64 || !xs8 || (a.xsc && a.Cin > kMaxXbn16)) return false;
+    if (a.xsc) pipe16_dt<FWD, true>(dt, a, st);
+    else pipe16_dt<FWD, false>(dt, a, st);
+  } else if (mode == DGRAD) {
+    if (a.Cout % 64 || a.Cin % 8) return false;
+    pipe16_dt<DGRAD, false>(dt, a, st);
+  } else {
+    if (a.Cout % 8 || a.Cin % 8 || !xs8 || a.kchunk % 64) return false;
+    magic_div((unsigned)(a.Ho * a.Wo), a.mg_hw, a.sh_hw);
+    magic_div((unsigned)a.Wo, a.mg_w, a.sh_w);
+    if (a.xsc) pipe16_dt<WGRAD, true>(dt, a, st);
+    else pipe16_dt<WGRAD, false>(dt, a, st);
+  }
+  return true;
+}
+
+}  // namespace mauv

@@ -41,6 +41,9 @@ CASES = [
     (2, 2, 4, 512, 2048, 1, 1, 0),
     (3, 2, 5, 64, 256, 1, 1, 0),
     (2, 2, 7, 8, 64, 3, 1, 1),      # Cin % 32 != 0: per-chunk tap decomposition, K tail
+    (1, 4, 20, 64, 128, 3, 1, 1),   # 128 x 128 eight-wave tiles, ragged last m tile
+    (2, 2, 15, 128, 64, 3, 2, 1),   # strided dgrad with Cout = 64, odd extents
+    (1, 2, 6, 96, 64, 3, 1, 1),     # Cin % 64 != 0: the pipelined FWD declines, DGRAD/WGRAD run
 ]
 
 
