@@ -36,12 +36,41 @@ __device__ __forceinline__ unsigned mdiv16(unsigned n, unsigned long long m, int
   return (unsigned)(((unsigned long long)n * m) >> s);
 }
 template <int DT>
-__device__ __forceinline__ u32x4 bn_relu8(u32x4 v, floatx8 sc, floatx8 sh, int relu, bool ok) {
-  floatx8 f = unpack8<DT>(v);
-  f = f * sc + sh;
+__device__ __forceinline__ unsigned pk2(float a, float b) {
+  if constexpr (DT == DT_BF16) {
+    return pk_bf16(a, b);
+  } else {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 v = {(_Float16)a, (_Float16)b};
+    return __builtin_bit_cast(unsigned, v);
+  }
+}
+// The producing layer's pending BN(+ReLU) on one 8-channel chunk: fp32 fma per element, one
+// round-to-nearest-even, then ReLU on the packed words as a signed-int16 max against `floor`
+// (0 with ReLU: both formats keep the sign in bit 15, so exactly the negative values and -0
+// become +0; 0x80008000 without).  Chunks outside the image (padding, ragged rows) become 0.
+template <int DT>
+__device__ __forceinline__ u32x4 bn_relu8(u32x4 v, const floatx8& sc, const floatx8& sh,
+                                          unsigned floor, bool ok) {
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  u32x4 o;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) f[e] = (!ok || (relu && !(f[e] > 0.f))) ? 0.f : f[e];
-  return pack8<DT>(f);
+  for (int i = 0; i < 4; ++i) {
+    float lo, hi;
+    if constexpr (DT == DT_BF16) {
+      lo = bf_lo(v[i]);
+      hi = bf_hi(v[i]);
+    } else {
+      lo = (float)__builtin_bit_cast(_Float16, (u16)(v[i] & 0xffffu));
+      hi = (float)__builtin_bit_cast(_Float16, (u16)(v[i] >> 16));
+    }
+    unsigned p = pk2<DT>(__builtin_fmaf(lo, sc[2 * i], sh[2 * i]),
+                         __builtin_fmaf(hi, sc[2 * i + 1], sh[2 * i + 1]));
+    asm("" : "+v"(p));  // keeps one v_cvt_pk per pair (else: two single conversions + v_perm)
+    const s2 m = __builtin_elementwise_max(__builtin_bit_cast(s2, p), __builtin_bit_cast(s2, floor));
+    o[i] = ok ? __builtin_bit_cast(unsigned, m) : 0u;
+  }
+  return o;
 }
 
 template <int NVA, int NVB>
@@ -241,17 +270,20 @@ void conv_pipe16(const ConvArgs a) {
     }
   };
 
+  const unsigned rfloor = a.xrelu ? 0u : 0x80008000u;
   auto store = [&](const St& S, int buf) {
     u16* As = smem + buf * STG;
     u16* Bs = As + A_SZ;
+    floatx8 fsc, fsh;  // FWD: every A chunk of this thread holds the same 8 input channels
+    if constexpr (XBN && MODE == FWD) {
+      fsc = ldf8(xbn + S.tc + EPC * kq);
+      fsh = ldf8(xbn + kMaxXbn16 + S.tc + EPC * kq);
+    }
 #pragma unroll
     for (int j = 0; j < NVA; ++j) {
       const int idx = tid + NT * j;
       u32x4 v = S.a[j];
-      if constexpr (XBN && MODE == FWD) {
-        const int c = S.tc + EPC * kq;
-        v = bn_relu8<DT>(v, ldf8(xbn + c), ldf8(xbn + kMaxXbn16 + c), a.xrelu, (S.ok >> j) & 1);
-      }
+      if constexpr (XBN && MODE == FWD) v = bn_relu8<DT>(v, fsc, fsh, rfloor, (S.ok >> j) & 1);
       const int off = A_COL ? (idx / (BM / EPC)) * (BM + 32) + EPC * (idx % (BM / EPC))
                             : (idx / KQ) * RLD + EPC * (idx % KQ);
       *(u32x4*)((!PA || idx < LA) ? As + off : dum) = v;
@@ -260,7 +292,7 @@ void conv_pipe16(const ConvArgs a) {
     for (int j = 0; j < NVB; ++j) {
       const int idx = tid + NT * j;
       u32x4 v = S.b[j];
-      if constexpr (XBN && MODE == WGRAD) v = bn_relu8<DT>(v, wsc, wsh, a.xrelu, (S.ok >> (8 + j)) & 1);
+      if constexpr (XBN && MODE == WGRAD) v = bn_relu8<DT>(v, wsc, wsh, rfloor, (S.ok >> (8 + j)) & 1);
       const int off = B_COL ? (idx / (BN / EPC)) * (BN + 32) + EPC * (idx % (BN / EPC))
                             : (idx / KQ) * RLD + EPC * (idx % KQ);
       *(u32x4*)((!PB || idx < LB) ? Bs + off : dum) = v;

@@ -1,0 +1,8 @@
+# HBM traffic per kernel family of one bf16 training step (two PMC passes)
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+B="bench.py --dtype bf16 --steps 1 --warmup 0 --no-cpu-baseline --no-infer --no-bf16 --exact-steps 0 --no-roofline"
+timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc16_fetch -o run -- python3 $B > gpurun_out/pmc16_fetch.log 2>&1 || exit 1
+timeout -s KILL 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc16_write -o run -- python3 $B > gpurun_out/pmc16_write.log 2>&1 || exit 1
+echo done
