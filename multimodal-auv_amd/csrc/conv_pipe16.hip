@@ -82,17 +82,22 @@ struct Stage16 {
 
 }  // namespace
 
-// 2 x 2 waves (64 x 64 each) for 64-wide tiles, 4 x 2 / 2 x 4 waves of 32 x 64 / 64 x 32 for
-// 128 x 128, 4 x 2 / 2 x 4 of 32 x 32 for 128 x 64 / 64 x 128 (eight waves: four per SIMD).
+// 2 x 2 waves (32 x 32 each) for 64 x 64 tiles; 4 x 2 / 2 x 4 waves of 32 x 64 / 64 x 32 for
+// 128 x 128, 4 x 2 / 2 x 4 of 32 x 32 for 128 x 64 / 64 x 128 (eight waves, four per SIMD:
+// two blocks per CU); 128 x 256 as 2 x 4 waves of 64 x 64 (one block per CU, two waves per
+// SIMD: half the loader / BN-on-load work and 2/3 of the LDS fragment reads per MAC).
 template <int BM, int BN>
 struct Waves16 {
-  static constexpr bool W8 = BM + BN >= 192;
-  static constexpr int M = W8 ? (BM == 128 ? 4 : 2) : 2, N = W8 ? (BM == 128 ? 2 : 4) : 2;
-  static constexpr int T = 64 * M * N;
+  static constexpr bool WIDE = BN == 256;
+  static constexpr bool W8 = WIDE || BM + BN >= 192;
+  static constexpr int M = WIDE ? 2 : W8 ? (BM == 128 ? 4 : 2) : 2;
+  static constexpr int N = WIDE ? 4 : W8 ? (BM == 128 ? 2 : 4) : 2;
+  static constexpr int T = 64 * M * N, EU = WIDE ? 2 : 4;
 };
 
 template <int MODE, int DT, int BM, int BN, bool XBN>
-__global__ __launch_bounds__((Waves16<BM, BN>::T)) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__((Waves16<BM, BN>::T))
+__attribute__((amdgpu_waves_per_eu(Waves16<BM, BN>::EU)))
 void conv_pipe16(const ConvArgs a) {
   constexpr int BK = 64, EPC = 8, KQ = BK / EPC;
   constexpr int WGM = Waves16<BM, BN>::M, WGN = Waves16<BM, BN>::N, NT = Waves16<BM, BN>::T;
@@ -415,29 +420,33 @@ void conv_pipe16(const ConvArgs a) {
     }
     __syncthreads();  // red is overwritten by the staged store below
   }
-  // 16-bit output through LDS: each wave row wm in turn parks its fp32 accumulators as a
-  // [WM][BN+4] tile, then all threads write 16-byte rows of 8 channels (residual addend /
-  // previous dx added in fp32, one rounding)
-  constexpr int SLD = BN + 4, CPR = BN / 8, NCH = WM * CPR;
+  // 16-bit output through LDS: the fp32 accumulators are parked as a row-major [rows][BN+4]
+  // tile — the whole block tile at once when it fits the operand buffers (one barrier), else
+  // one wave row wm per pass — then every thread writes 16-byte rows of 8 channels (residual
+  // addend / previous dx added in fp32, one rounding)
+  constexpr int SLD = BN + 4, CPR = BN / 8;
+  constexpr int PASSES = BM * SLD * 4 <= 2 * STG * 2 ? 1 : WGM, PR = BM / PASSES;
+  constexpr int NCH = PR * CPR;
   float* stile = (float*)smem;
   u16* outp = (u16*)a.out;
   const u16* addp = (const u16*)a.addend;
 #pragma unroll
-  for (int pass = 0; pass < WGM; ++pass) {
-    if (wm == pass) {
+  for (int pass = 0; pass < PASSES; ++pass) {
+    if (PASSES == 1 || wm == pass) {
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            stile[(mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SLD + wn * WN + ni * 32 + li] =
-                acc[mi][ni][r];
+            stile[(wm * WM - pass * PR + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SLD +
+                  wn * WN + ni * 32 + li] = acc[mi][ni][r];
     }
     __syncthreads();
+#pragma unroll
     for (int c = tid; c < NCH; c += NT) {
       const int rl = c / CPR, cc = c - rl * CPR;
-      const int row = m0 + pass * WM + rl, col = n0 + 8 * cc;
+      const int row = m0 + pass * PR + rl, col = n0 + 8 * cc;
       if (row >= a.M || col >= a.N) continue;
       const floatx4 v0 = *(const floatx4*)(stile + rl * SLD + 8 * cc);
       const floatx4 v1 = *(const floatx4*)(stile + rl * SLD + 8 * cc + 4);
@@ -457,9 +466,15 @@ void conv_pipe16(const ConvArgs a) {
         if (addp) f += unpack8<DT>(*(const u32x4*)(addp + o));
         if (a.accumulate) f += unpack8<DT>(*(const u32x4*)(outp + o));
       }
-      *(u32x4*)(outp + o) = pack8<DT>(f);
+      u32x4 pk;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pk[e] = pk2<DT>(f[2 * e], f[2 * e + 1]);
+        asm("" : "+v"(pk[e]));
+      }
+      *(u32x4*)(outp + o) = pk;
     }
-    __syncthreads();
+    if (pass + 1 < PASSES) __syncthreads();
   }
 }
 
@@ -470,10 +485,21 @@ static void launch_pipe16(const ConvArgs& a, hipStream_t st) {
                      a);
 }
 
+// MAUV_P16_WIDE: bit m set -> mode m (FWD 0, DGRAD 1, WGRAD 2) takes 128 x 256 tiles when
+// N >= 256 and M > 64 (default off: one block per CU measured 5-25 % slower per shape than
+// two 128 x 128 blocks, tools/gpubatch_wide.sh)
+static int wide_modes() {
+  static int w = -1;
+  if (w < 0) { const char* e = getenv("MAUV_P16_WIDE"); w = e ? atoi(e) : 0; }
+  return w;
+}
+
 template <int MODE, int DT, bool XBN>
 static void pipe16_tiles(const ConvArgs& a, hipStream_t st) {
   const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
-  if (bm == 64 && bn == 64) launch_pipe16<MODE, DT, 64, 64, XBN>(a, st);
+  if (bm == 128 && a.N >= 256 && ((wide_modes() >> MODE) & 1))
+    launch_pipe16<MODE, DT, 128, 256, XBN>(a, st);
+  else if (bm == 64 && bn == 64) launch_pipe16<MODE, DT, 64, 64, XBN>(a, st);
   else if (bm == 64) launch_pipe16<MODE, DT, 64, 128, XBN>(a, st);
   else if (bn == 64) launch_pipe16<MODE, DT, 128, 64, XBN>(a, st);
   else launch_pipe16<MODE, DT, 128, 128, XBN>(a, st);

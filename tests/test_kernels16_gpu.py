@@ -44,6 +44,8 @@ CASES = [
     (1, 4, 20, 64, 128, 3, 1, 1),   # 128 x 128 eight-wave tiles, ragged last m tile
     (2, 2, 15, 128, 64, 3, 2, 1),   # strided dgrad with Cout = 64, odd extents
     (1, 2, 6, 96, 64, 3, 1, 1),     # Cin % 64 != 0: the pipelined FWD declines, DGRAD/WGRAD run
+    (1, 2, 12, 256, 256, 3, 1, 1),  # N >= 256, M > 64: 128 x 256 tiles (fwd, dgrad)
+    (2, 3, 9, 64, 512, 1, 1, 0),    # 128 x 256 fwd tiles, ragged m, two n tiles
 ]
 
 
@@ -113,10 +115,11 @@ def test_conv16_stem_shared_padded_input(dt):
 
 
 @pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
-def test_conv16_lazy_bn_input_and_stats(dt):
+@pytest.mark.parametrize("Cout", [128, 256])
+def test_conv16_lazy_bn_input_and_stats(dt, Cout):
     """x' = relu(x*scale + shift) applied on load (FWD and WGRAD) + epilogue statistics."""
     from mauv import ops
-    G, B, H, Cin, Cout = 2, 3, 8, 64, 128
+    G, B, H, Cin = 2, 3, 8, 64
     torch.manual_seed(3)
     x = torch.randn(G, B, H, H, Cin).to(dt)
     sc = torch.rand(G, Cin) + 0.5
