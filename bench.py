@@ -264,7 +264,7 @@ def main():
         if not args.no_roofline:
             bf16["roofline"] = roofline_step(
                 step, peak=BF16_MFMA_PEAK_TF, traffic=False, suffix="_bfloat16",
-                kernel="conv_gemm_h16<bf16> (implicit-GEMM fwd+dgrad+wgrad, one step)")
+                kernel="conv_pipe16<bf16> (pipelined implicit-GEMM fwd+dgrad+wgrad; stems conv_gemm_h16), one step")
         set_precision(model.module if world > 1 else model,
                       torch.bfloat16 if args.dtype == "bf16" else None)
 

@@ -95,7 +95,7 @@ struct Waves16 {
   static constexpr int T = 64 * M * N, EU = WIDE ? 2 : 4;
 };
 
-template <int MODE, int DT, int BM, int BN, bool XBN>
+template <int MODE, int DT, int BM, int BN, bool XBN, bool STEM>
 __global__ __launch_bounds__((Waves16<BM, BN>::T))
 __attribute__((amdgpu_waves_per_eu(Waves16<BM, BN>::EU)))
 void conv_pipe16(const ConvArgs a) {
@@ -134,7 +134,8 @@ void conv_pipe16(const ConvArgs a) {
   else g = blockIdx.y;
   int kbeg = 0, kend = a.K;
   if constexpr (MODE == WGRAD) { kbeg = sp * a.kchunk; kend = min(a.K, kbeg + a.kchunk); }
-  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  // STEM (FWD, Cin = 8, S <= 8): stage r holds the S taps of filter row r as 8 pixel chunks
+  const int nt = STEM ? a.R : kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
   const long long ny = (long long)a.B * a.Ho * a.Wo * a.Cout;  // dy elements per group
   const u16* xg = (const u16*)a.x + (long long)g * a.xs_g;
@@ -167,7 +168,7 @@ void conv_pipe16(const ConvArgs a) {
         const int p0 = oh * a.stride - a.pad, p1 = ow * a.stride - a.pad;
         abase[j] = (unsigned)((b * xs_b + p0 * xs_h + p1 * xs_w + EPC * kq) * 2);
         aq0[j] = ok ? p0 : -(1 << 28);
-        aq1[j] = p1;
+        aq1[j] = STEM ? (kq < a.S ? p1 + kq : -(1 << 28)) : p1;  // STEM: chunk kq = tap s
       } else {
         const int HW = a.Hc * a.Wc, b = mm / HW, rem = mm - b * HW;
         const int i = rem / a.Wc, jj = rem - i * a.Wc;
@@ -189,7 +190,8 @@ void conv_pipe16(const ConvArgs a) {
     const int idx = tid + NT * j;
     if constexpr (MODE == FWD) {
       const int n = n0 + idx / KQ;
-      bbase[j] = (n < a.N && (!PB || idx < LB)) ? (unsigned)((n * a.K + EPC * kq) * 2) : kOOB16;
+      bbase[j] = (n < a.N && (!PB || idx < LB) && (!STEM || kq < a.S))
+                     ? (unsigned)((n * a.K + EPC * kq) * 2) : kOOB16;
     } else if constexpr (MODE == DGRAD) {
       const int c = n0 + EPC * (idx % (BN / EPC)), kr = idx / (BN / EPC);
       bbase[j] = (c < a.N && (!PB || idx < LB)) ? (unsigned)((kr * a.R * a.S * a.Cin + c) * 2)
@@ -223,7 +225,7 @@ void conv_pipe16(const ConvArgs a) {
 
   auto load = [&](St& S, int t) {
     const int k0 = kbeg + t * BK;
-    const bool sok = k0 < kend;  // stage-uniform for FWD / DGRAD (K % 64 == 0)
+    const bool sok = STEM ? t < a.R : k0 < kend;  // stage-uniform (FWD / DGRAD: K % 64 == 0)
     if constexpr (MODE == FWD) {
       const unsigned soff = (unsigned)((t_r * xs_h + t_s * xs_w + t_c) * 2);
       S.ok = 0;
@@ -236,9 +238,14 @@ void conv_pipe16(const ConvArgs a) {
         S.ok |= (unsigned)ok << j;
       }
 #pragma unroll
-      for (int j = 0; j < NVB; ++j) S.b[j] = bload16(rb, sok ? bbase[j] + (unsigned)(k0 * 2) : kOOB16);
-      t_c += BK;
-      if (t_c >= a.Cin) { t_c = 0; if (++t_s == a.S) { t_s = 0; ++t_r; } }
+      for (int j = 0; j < NVB; ++j)
+        S.b[j] = bload16(rb, sok ? bbase[j] + (unsigned)(STEM ? t_r * a.S * 16 : k0 * 2) : kOOB16);
+      if constexpr (STEM) {
+        ++t_r;
+      } else {
+        t_c += BK;
+        if (t_c >= a.Cin) { t_c = 0; if (++t_s == a.S) { t_s = 0; ++t_r; } }
+      }
     } else if constexpr (MODE == DGRAD) {
       const unsigned soff = (unsigned)((t_c - (t_r * a.Wo + t_s) * a.Cout) * 2);
 #pragma unroll
@@ -478,10 +485,10 @@ void conv_pipe16(const ConvArgs a) {
   }
 }
 
-template <int MODE, int DT, int BM, int BN, bool XBN>
+template <int MODE, int DT, int BM, int BN, bool XBN, bool STEM = false>
 static void launch_pipe16(const ConvArgs& a, hipStream_t st) {
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
-  hipLaunchKernelGGL((conv_pipe16<MODE, DT, BM, BN, XBN>), grid, dim3(Waves16<BM, BN>::T), 0, st,
+  hipLaunchKernelGGL((conv_pipe16<MODE, DT, BM, BN, XBN, STEM>), grid, dim3(Waves16<BM, BN>::T), 0, st,
                      a);
 }
 
@@ -494,21 +501,25 @@ static int wide_modes() {
   return w;
 }
 
-template <int MODE, int DT, bool XBN>
+template <int MODE, int DT, bool XBN, bool STEM>
 static void pipe16_tiles(const ConvArgs& a, hipStream_t st) {
   const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
-  if (bm == 128 && a.N >= 256 && ((wide_modes() >> MODE) & 1))
-    launch_pipe16<MODE, DT, 128, 256, XBN>(a, st);
-  else if (bm == 64 && bn == 64) launch_pipe16<MODE, DT, 64, 64, XBN>(a, st);
-  else if (bm == 64) launch_pipe16<MODE, DT, 64, 128, XBN>(a, st);
-  else if (bn == 64) launch_pipe16<MODE, DT, 128, 64, XBN>(a, st);
-  else launch_pipe16<MODE, DT, 128, 128, XBN>(a, st);
+  if constexpr (!STEM) {
+    if (bm == 128 && a.N >= 256 && ((wide_modes() >> MODE) & 1)) {
+      launch_pipe16<MODE, DT, 128, 256, XBN>(a, st);
+      return;
+    }
+  }
+  if (bm == 64 && bn == 64) launch_pipe16<MODE, DT, 64, 64, XBN, STEM>(a, st);
+  else if (bm == 64) launch_pipe16<MODE, DT, 64, 128, XBN, STEM>(a, st);
+  else if (bn == 64) launch_pipe16<MODE, DT, 128, 64, XBN, STEM>(a, st);
+  else launch_pipe16<MODE, DT, 128, 128, XBN, STEM>(a, st);
 }
 
-template <int MODE, bool XBN>
+template <int MODE, bool XBN, bool STEM = false>
 static void pipe16_dt(int dt, const ConvArgs& a, hipStream_t st) {
-  if (dt == DT_BF16) pipe16_tiles<MODE, DT_BF16, XBN>(a, st);
-  else pipe16_tiles<MODE, DT_F16, XBN>(a, st);
+  if (dt == DT_BF16) pipe16_tiles<MODE, DT_BF16, XBN, STEM>(a, st);
+  else pipe16_tiles<MODE, DT_F16, XBN, STEM>(a, st);
 }
 
 bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
@@ -521,6 +532,11 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
   const bool xs8 = a0.xs_w % 8 == 0 && a0.xs_h % 8 == 0 && a0.xs_b % 8 == 0 && a0.xs_g % 8 == 0;
   ConvArgs a = a0;
   if (mode == FWD) {
+    if (a.Cin == 8 && a.S <= 8 && a.xs_w == 8 && !a.xsc && a.xs_h % 8 == 0 && a.xs_b % 8 == 0 &&
+        a.xs_g % 8 == 0) {  // the stems: 7x7 taps over 8 zero-padded input channels
+      pipe16_dt<FWD, false, true>(dt, a, st);
+      return true;
+    }
     if (a.Cin % 64 || !xs8 || (a.xsc && a.Cin > kMaxXbn16)) return false;
     if (a.xsc) pipe16_dt<FWD, true>(dt, a, st);
     else pipe16_dt<FWD, false>(dt, a, st);
