@@ -134,6 +134,12 @@ int mauv_reparam_sample_h16(int dtype, const float* mu, const float* rho, const 
                             unsigned long long seed, unsigned long long sample0,
                             unsigned int layer, int G, int Cout, int Cin, int RS, int cin_pad,
                             void* out, long long out_gstride, hipStream_t stream);
+/* fp32 counterpart of mauv_reparam_sample_h16's padded layout (the fp32 stems' 4-channel KRSC
+ * weights); same sampling as mauv_reparam_sample, pad channels not written. */
+int mauv_reparam_sample_padded(const float* mu, const float* rho, const float* eps,
+                               unsigned long long seed, unsigned long long sample0,
+                               unsigned int layer, int G, int Cout, int Cin, int RS, int cin_pad,
+                               float* out, long long out_gstride, hipStream_t stream);
 
 /* get_kl_loss (bayesian-torch 0.5.0; called at train/multimodal.py:114,284 and
  * train/unimodal.py:130,262): sum over entries of mean(log s_p - log s + (s^2 + (mu-m_p)^2)
@@ -237,6 +243,10 @@ int mauv_avgpool_bwd_h16(int dtype, const float* dy, int N, int HW, int C, void*
 /* Stem input of the 16-bit path: fp32 NCHW [B][C][H][W] -> 16-bit NHWC [B][H][W][Cp], channels
  * C..Cp-1 zero (the caller's images are read once per trunk, shared by all MC samples). */
 int mauv_pack_nchw_h16(int dtype, const float* x, int B, int C, int H, int W, int Cp, void* y,
+                       hipStream_t stream);
+/* Stem input of the fp32 path: NCHW -> NHWC [B][H][W][Cp] fp32, channels C..Cp-1 zero (Cp = 4:
+ * the stem conv then runs the pipelined split kernel on 16-byte pixel quads). */
+int mauv_pack_nchw_f32(const float* x, int B, int C, int H, int W, int Cp, float* y,
                        hipStream_t stream);
 
 /* ---- fusion head + MC head (head.hip) ----------------------------------------------------

@@ -77,7 +77,7 @@ __device__ __forceinline__ int row_of(int idx) {
   return (idx >> 6) * 16 + 8 * (l >> 5) + 2 * ((l >> 2) & 3) + ((l >> 4) & 1);
 }
 
-template <int MODE, int BM, int BN, bool XBN, bool ONEACC, int WV>
+template <int MODE, int BM, int BN, bool XBN, bool ONEACC, int WV, bool STEM = false>
 __global__ __launch_bounds__((SplitWaves<BM, BN, WV>::T))
 __attribute__((amdgpu_waves_per_eu(SplitWaves<BM, BN, WV>::EU)))
 void conv_split_f32(const ConvArgs a) {
@@ -118,7 +118,9 @@ void conv_split_f32(const ConvArgs a) {
   else g = blockIdx.y;
   int kbeg = 0, kend = a.K;
   if constexpr (MODE == WGRAD) { kbeg = sp * a.kchunk; kend = min(a.K, kbeg + a.kchunk); }
-  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  // STEM (FWD, Cin = 4 zero-padded channels, xs_w = 4): the taps of one filter row as pixel
+  // quads, s = 4h .. 4h+3 in stage h of the row (S <= 8: two stages per row; S <= 4: one)
+  const int nt = STEM ? a.R * ((a.S + 3) / 4) : kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
   const long long ny = (long long)a.B * a.Ho * a.Wo * a.Cout;  // dy floats per group
   const float* xg = a.x + (long long)g * a.xs_g;
@@ -149,7 +151,7 @@ void conv_split_f32(const ConvArgs a) {
         const int p0 = oh * a.stride - a.pad, p1 = ow * a.stride - a.pad;
         abase[j] = (unsigned)((b * xs_b + p0 * xs_h + p1 * xs_w + 4 * kq) * 4);
         aq0[j] = ok ? p0 : -(1 << 28);
-        aq1[j] = p1;
+        aq1[j] = STEM ? p1 + kq : p1;  // STEM: quad kq is the pixel of tap t_s + kq
       } else {
         const int HW = a.Hc * a.Wc, b = mm / HW, rem = mm - b * HW;
         const int i = rem / a.Wc, jj = rem - i * a.Wc;
@@ -205,14 +207,15 @@ void conv_split_f32(const ConvArgs a) {
 
   auto load = [&](St& S, int t) {
     const int k0 = kbeg + t * BK;
-    const bool sok = k0 < kend;  // stage-uniform for FWD / DGRAD (K % 16 == 0)
+    const bool sok = STEM ? t < nt : k0 < kend;  // stage-uniform (FWD / DGRAD: K % 16 == 0)
     if constexpr (MODE == FWD) {
       const unsigned soff = (unsigned)((t_r * xs_h + t_s * xs_w + t_c) * 4);
+      const bool tap = !STEM || kq + t_s < a.S;  // STEM: quad kq is tap s = t_s + kq
       S.ok = 0;
       S.tc = t_c;
 #pragma unroll
       for (int j = 0; j < NVA; ++j) {
-        const bool ok = sok && (unsigned)(aq0[j] + t_r) < (unsigned)a.H &&
+        const bool ok = sok && tap && (unsigned)(aq0[j] + t_r) < (unsigned)a.H &&
                         (unsigned)(aq1[j] + t_s) < (unsigned)a.W;
         const bool act = !PA || tid + NT * j < LA;
         S.a[j] = bload(ra, ok && act ? abase[j] + soff : kOOB);
@@ -221,10 +224,17 @@ void conv_split_f32(const ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < NVB; ++j) {
         const bool act = !PB || tid + NT * j < LB;
-        S.b[j] = bload(rb, sok && act ? bbase[j] + (unsigned)(k0 * 4) : kOOB);
+        S.b[j] = bload(rb, sok && act && tap ? bbase[j] + (unsigned)(STEM ? (t_r * a.S + t_s) * 16
+                                                                         : k0 * 4)
+                                             : kOOB);
       }
-      t_c += BK;
-      if (t_c >= a.Cin) { t_c = 0; if (++t_s == a.S) { t_s = 0; ++t_r; } }
+      if constexpr (STEM) {
+        t_s += 4;
+        if (t_s >= a.S) { t_s = 0; ++t_r; }
+      } else {
+        t_c += BK;
+        if (t_c >= a.Cin) { t_c = 0; if (++t_s == a.S) { t_s = 0; ++t_r; } }
+      }
     } else if constexpr (MODE == DGRAD) {
       const unsigned soff = (unsigned)((t_c - (t_r * a.Wo + t_s) * a.Cout) * 4);
 #pragma unroll
@@ -375,17 +385,18 @@ void conv_split_f32(const ConvArgs a) {
   conv_epilogue<MODE, BM, BN, MI, NI, WGM, WGN>(a, acc, (float*)smem, tid, m0, n0, g, sp);
 }
 
-template <int MODE, int BM, int BN, bool XBN, int WV = 4>
+template <int MODE, int BM, int BN, bool XBN, int WV = 4, bool STEM = false>
 static void launch_split(const ConvArgs& a, int oneacc, hipStream_t st) {
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
   const dim3 block(SplitWaves<BM, BN, WV>::T);
   if constexpr (WV == 8) {  // one accumulator set (128-VGPR budget)
-    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV, STEM>), grid, block, 0, st, a);
   } else {
     if (oneacc)
-      hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV>), grid, block, 0, st, a);
+      hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV, STEM>), grid, block, 0, st, a);
     else
-      hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, false, WV>), grid, block, 0, st, a);
+      hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, false, WV, STEM>), grid, block, 0, st,
+                         a);
   }
 }
 
@@ -429,6 +440,13 @@ bool conv_split_launch(int mode, const ConvArgs& a0, int oneacc, hipStream_t st)
   const long long nx = (long long)a0.B * a0.xs_b, ny = (long long)a0.B * a0.Ho * a0.Wo * a0.Cout;
   if (nx > lim || ny > lim || a0.ws_g > lim) return false;
   ConvArgs a = a0;
+  if (mode == FWD && a.Cin == 4 && a.S <= 8 && a.xs_c == 1 && a.xs_w == 4 && !a.xsc &&
+      a.xs_h % 4 == 0 && a.xs_b % 4 == 0 && a.xs_g % 4 == 0 && a.N == 64) {
+    // the stems over 4 zero-padded input channels (mauv_pack_nchw_f32)
+    if (a.M > 64) launch_split<FWD, 128, 64, false, 8, true>(a, oneacc, st);
+    else launch_split<FWD, 64, 64, false, 4, true>(a, oneacc, st);
+    return true;
+  }
   if (mode == FWD) {
     const bool va = (a.Cin % 32 == 0) && a.xs_c == 1 && a.xs_w % 4 == 0 && a.xs_h % 4 == 0 &&
                     a.xs_b % 4 == 0 && a.xs_g % 4 == 0 && a.xs_g != 0;

@@ -108,17 +108,17 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restric
   }
 }
 
-// Stem input for the 16-bit path: the caller's fp32 NCHW images -> 16-bit NHWC with the
-// channels zero-padded to Cp (8), so the stem conv runs on 16-byte channel chunks.
-template <int DT>
+// Stem input: the caller's fp32 NCHW images -> NHWC with the channels zero-padded to Cp (8 for
+// the 16-bit path, 4 for fp32), so the stem conv runs on 16-byte channel chunks.
+template <class S>
 __global__ __launch_bounds__(256) void pack_nchw_kernel(const float* __restrict__ x, int B, int C,
-                                                        int HW, int Cp, u16* __restrict__ y) {
+                                                        int HW, int Cp, typename S::T* __restrict__ y) {
   const long long total = (long long)B * HW * Cp;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const int c = (int)(i % Cp);
     const long long p = i / Cp;
     const long long b = p / HW, hw = p - b * HW;
-    y[i] = c < C ? H16<DT>::from_f(x[(b * C + c) * HW + hw]) : (u16)0;
+    S::st(y + i, c < C ? x[(b * C + c) * HW + hw] : 0.f);
   }
 }
 
@@ -206,9 +206,17 @@ MAUV_API int mauv_avgpool_bwd_h16(int dtype, const float* dy, int N, int HW, int
 MAUV_API int mauv_pack_nchw_h16(int dtype, const float* x, int B, int C, int H, int W, int Cp,
                                 void* y, hipStream_t stream) {
   if (Cp < C) { set_error("pack_nchw_h16: Cp < C"); return kErrArg; }
-#define L(D) hipLaunchKernelGGL(pack_nchw_kernel<D>, dim3(grid1((long long)B * H * W * Cp)), dim3(256), \
-                                0, stream, x, B, C, H * W, Cp, (u16*)y);
+#define L(D) hipLaunchKernelGGL(pack_nchw_kernel<S16<D>>, dim3(grid1((long long)B * H * W * Cp)), \
+                                dim3(256), 0, stream, x, B, C, H * W, Cp, (u16*)y);
   MAUV_DT_DISPATCH(dtype, "pack_nchw_h16", L)
 #undef L
   return check_launch("pack_nchw_h16");
+}
+
+MAUV_API int mauv_pack_nchw_f32(const float* x, int B, int C, int H, int W, int Cp, float* y,
+                                hipStream_t stream) {
+  if (Cp < C) { set_error("pack_nchw_f32: Cp < C"); return kErrArg; }
+  hipLaunchKernelGGL(pack_nchw_kernel<SF32>, dim3(grid1((long long)B * H * W * Cp)), dim3(256), 0,
+                     stream, x, B, C, H * W, Cp, y);
+  return check_launch("pack_nchw_f32");
 }

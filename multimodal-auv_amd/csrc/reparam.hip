@@ -224,6 +224,22 @@ MAUV_API int mauv_reparam_sample(const float* mu, const float* rho, const float*
   return check_launch("reparam_sample");
 }
 
+// mauv_reparam_sample into a KRSC layout with the input channels padded to cin_pad (the fp32
+// stems' 4-channel layout; pad channels are left untouched: the caller zero-fills them once).
+MAUV_API int mauv_reparam_sample_padded(const float* mu, const float* rho, const float* eps,
+                                        unsigned long long seed, unsigned long long sample0,
+                                        unsigned int layer, int G, int Cout, int Cin, int RS,
+                                        int cin_pad, float* out, long long out_gstride,
+                                        hipStream_t stream) {
+  if (cin_pad < Cin) { set_error("reparam_sample_padded: cin_pad < Cin"); return kErrArg; }
+  const long long numel = (long long)Cout * Cin * RS;
+  const long long nq = (numel + 3) / 4;
+  hipLaunchKernelGGL(reparam_sample_kernel<SF32>, dim3(grid_for(nq)), dim3(256), 0, stream, mu,
+                     rho, eps, seed, sample0, layer, G, Cout, Cin, RS, cin_pad, out,
+                     out_gstride ? out_gstride : (long long)Cout * RS * cin_pad);
+  return check_launch("reparam_sample_padded");
+}
+
 // 16-bit sampled weights (dtype 0 = bf16, 1 = f16) for the 16-bit convs, KRSC with the input
 // channels padded to cin_pad (pad channels are left untouched: the caller zero-fills them
 // once).  Sampling arithmetic is fp32; only the stored weight is rounded.

@@ -40,6 +40,7 @@ SIGNATURES = {
     "mauv_reparam_sample": [P, P, P, U64, U64, U32, I, I, I, I, P, LL, P],
     "mauv_reparam_bwd": [P, I, LL, LL, P, P, P, U64, U64, U32, I, I, I, I, I, P, P, LL, P],
     "mauv_reparam_sample_h16": [I, P, P, P, U64, U64, U32, I, I, I, I, I, P, LL, P],
+    "mauv_reparam_sample_padded": [P, P, P, U64, U64, U32, I, I, I, I, I, P, LL, P],
     "mauv_kl_workspace_bytes": [I],
     "mauv_kl_fwd": [P, I, P, F, P, P],
     "mauv_kl_bwd": [P, I, P, F, P],
@@ -66,6 +67,7 @@ SIGNATURES = {
     "mauv_avgpool_fwd_h16": [I, P, I, I, I, P, P],
     "mauv_avgpool_bwd_h16": [I, P, I, I, I, P, P],
     "mauv_pack_nchw_h16": [I, P, I, I, I, I, I, P, P],
+    "mauv_pack_nchw_f32": [P, I, I, I, I, I, P, P],
     # head.hip
     "mauv_attn_t": [P, I, P, P],
     "mauv_attn_t_bwd": [P, P, I, P, P],

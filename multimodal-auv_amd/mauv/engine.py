@@ -13,8 +13,9 @@ stored), per-group BN statistics and sequential running-stat updates, and a hand
 backward that writes dmu/drho/dgamma/dbeta straight into a flat gradient arena (one buffer
 per model, so the data-parallel all-reduce is a single bucketed RCCL call).
 
-Activations are NHWC ``[G][B][H][W][C]`` fp32.  The stems read the caller's NCHW images in
-place (strided loads, group stride 0 = image shared by all MC samples).
+Activations are NHWC ``[G][B][H][W][C]`` fp32.  The stems read one NHWC copy of the caller's
+NCHW images with the channels zero-padded to 4 (16-bit path: 8), shared by all MC samples
+(group stride 0).
 """
 import os
 
@@ -28,6 +29,9 @@ from .layers import is_bayesian, LinearReparameterization
 # pass over (y, dout).  Measured slower on MI355X (the LDS reduction lengthens every dgrad
 # tile more than the standalone partial kernel costs), so it is opt-in.
 DGRAD_BN_EPILOGUE = os.environ.get("MAUV_DGRAD_BN_EPILOGUE", "0") == "1"
+# fp32 stems on an NHWC copy of the images with 4 zero-padded channels (the pipelined split
+# kernel's STEM mode) instead of strided NCHW loads on the generic kernel
+F32_STEM_PACK = os.environ.get("MAUV_F32_STEM_PACK", "1") == "1"
 
 
 # ----------------------------------------------------------------------------- root state
@@ -261,8 +265,12 @@ class TrunkRunner(_Runner):
         self.dt = dtype   # activation / sampled-weight storage (fp32, bf16 or f16)
 
     def _cin_pad(self, Cin):
-        """16-bit convs move 8-channel chunks: the stems' 1/3 input channels pad to 8."""
-        return Cin if self.dt == torch.float32 or Cin % 8 == 0 else (Cin + 7) // 8 * 8
+        """The convs move 16-byte channel chunks: the stems' 1/3 input channels pad to 8
+        (16-bit) or 4 (fp32; MAUV_F32_STEM_PACK=0 keeps the fp32 stems on strided NCHW loads)."""
+        q = 4 if self.dt == torch.float32 else 8
+        if self.dt == torch.float32 and not F32_STEM_PACK:
+            q = 1
+        return Cin if Cin % q == 0 else (Cin + q - 1) // q * q
 
     # ---- conv / bn units ----
     def _conv(self, conv, x, B, H, W, x_strides=None, x_bn=None, bn_stats=True):
@@ -370,10 +378,10 @@ class TrunkRunner(_Runner):
             raise ValueError(f"trunk expects {t.conv1.in_channels} input channels, got {Cin}")
         self.B = B
         recs = self.recs = []
-        if self.dt == torch.float32:   # the stem reads the caller's NCHW images in place
+        cp = self._cin_pad(Cin)
+        if self.dt == torch.float32 and cp == Cin:   # the stem reads the NCHW images in place
             xs = (0, Cin * H * W, W, 1, H * W)
-        else:                          # 16-bit NHWC copy, channels zero-padded to 8
-            cp = self._cin_pad(Cin)
+        else:           # NHWC copy, channels zero-padded to 8 (16-bit) / 4 (fp32)
             xh = torch.empty(B, H, W, cp, device=x.device, dtype=self.dt)
             ops.pack_nchw(x, B, Cin, H, W, cp, xh)
             x, xs = xh, (0, H * W * cp, W * cp, cp, 1)

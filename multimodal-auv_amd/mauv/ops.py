@@ -190,14 +190,19 @@ def conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, R, stride, pad,
 def reparam_sample(mu, rho, out, G, seed, sample0, layer, Cout, Cin, RS, eps=None,
                    out_gstride=0, cin_pad=None):
     """out[g] (KRSC, group stride out_gstride or numel) = mu + softplus(rho) * eps_g.
-    A bf16/f16 `out` gets 16-bit weights with cin_pad (>= Cin) channels (pad untouched)."""
+    A bf16/f16 `out` gets 16-bit weights; cin_pad (>= Cin) channels in the KRSC layout (pad
+    untouched) for the padded stems (8 channels 16-bit, 4 fp32)."""
     _f32(mu, rho, eps)
     if out.dtype in H16:
         check(lib.mauv_reparam_sample_h16(H16[out.dtype], _p(mu), _p(rho), _p(eps), seed, sample0,
                                           layer, G, Cout, Cin, RS, cin_pad or Cin, _p(out),
                                           out_gstride, stream()), "reparam_sample_h16")
         return
-    assert cin_pad in (None, Cin)
+    if cin_pad not in (None, Cin):
+        check(lib.mauv_reparam_sample_padded(_p(mu), _p(rho), _p(eps), seed, sample0, layer, G,
+                                             Cout, Cin, RS, cin_pad, _p(out), out_gstride,
+                                             stream()), "reparam_sample_padded")
+        return
     check(lib.mauv_reparam_sample(_p(mu), _p(rho), _p(eps), seed, sample0, layer, G, Cout, Cin,
                                   RS, _p(out), out_gstride, stream()), "reparam_sample")
 
@@ -335,8 +340,11 @@ def avgpool_bwd(dy, N, HW, C, dx):
 
 
 def pack_nchw(x, B, C, H, W, Cp, y):
-    """fp32 NCHW images -> 16-bit NHWC with Cp (zero-padded) channels (16-bit stems)."""
+    """fp32 NCHW images -> NHWC with Cp (zero-padded) channels: 16-bit (Cp 8) or fp32 (Cp 4)."""
     _f32(x)
+    if y.dtype == torch.float32:
+        check(lib.mauv_pack_nchw_f32(_p(x), B, C, H, W, Cp, _p(y), stream()), "pack_nchw_f32")
+        return
     check(lib.mauv_pack_nchw_h16(H16[y.dtype], _p(x), B, C, H, W, Cp, _p(y), stream()),
           "pack_nchw_h16")
 

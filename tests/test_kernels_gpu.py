@@ -103,6 +103,49 @@ def test_stem_nchw_shared_input(cin):
     close(ws.sum(0).view(G, 64, 7, 7, cin), torch.stack(ref))
 
 
+@pytest.mark.parametrize("cin,H,R", [(3, 20, 7), (1, 37, 7), (3, 9, 3)])
+def test_stem_packed_nhwc4(cin, H, R):
+    """Stems on the packed layout (mauv_pack_nchw_f32: NHWC, channels zero-padded to 4) with
+    4-channel padded weights (mauv_reparam_sample_padded): the split kernel's STEM mode."""
+    from mauv import ops
+    G, B, st, pd = 3, 2, 2, R // 2
+    torch.manual_seed(2)
+    x = torch.randn(B, cin, H, H)
+    mu = torch.randn(64, cin, R, R) * 0.1
+    rho = torch.full_like(mu, -4.0)
+    eps = torch.randn(G, 64 * cin * R * R)
+    xd = x.to(dev)
+    xp = torch.empty(B, H, H, 4, device=dev)
+    ops.pack_nchw(xd, B, cin, H, H, 4, xp)
+    ref_xp = torch.zeros(B, H, H, 4)
+    ref_xp[..., :cin] = x.permute(0, 2, 3, 1)
+    assert torch.equal(xp.cpu(), ref_xp)
+    w = torch.zeros(G, 64, R, R, 4, device=dev)
+    ops.reparam_sample(mu.to(dev), rho.to(dev), w, G, 0, 0, 0, 64, cin, R * R, eps=eps.to(dev),
+                       cin_pad=4)
+    wref = mu.unsqueeze(0) + F.softplus(rho).unsqueeze(0) * eps.view(G, 64, cin, R, R)
+    close(w[..., :cin], wref.permute(0, 1, 3, 4, 2), rtol=1e-6, atol=1e-7)
+    assert torch.count_nonzero(w[..., cin:]) == 0
+    Ho = ops.out_hw(H, R, st, pd)
+    strides = (0, H * H * 4, H * 4, 4, 1)
+    y = torch.empty(G, B, Ho, Ho, 64, device=dev)
+    ops.conv2d_fwd(xp, w, y, G, B, H, H, 4, 64, R, st, pd, x_strides=strides, alg_cin=cin)
+    wc = w.cpu()[..., :cin]
+    xs = x.permute(0, 2, 3, 1).unsqueeze(0).expand(G, -1, -1, -1, -1)
+    close(y, _ref_conv(xs, wc, st, pd))
+    dy = torch.randn(G, B, Ho, Ho, 64)
+    splits = ops.wgrad_splits(G, B, H, H, 4, 64, R, st, pd)
+    ws = torch.empty(splits, G, 64, R * R * 4, device=dev)
+    ops.conv2d_bwd_weight(xp, dy.to(dev), ws, splits, G, B, H, H, 4, 64, R, st, pd,
+                          x_strides=strides, alg_cin=cin)
+    ref = []
+    for g in range(G):
+        wg = wc[g].permute(0, 3, 1, 2).double().requires_grad_(True)
+        F.conv2d(x.double(), wg, stride=st, padding=pd).backward(dy[g].permute(0, 3, 1, 2).double())
+        ref.append(wg.grad.permute(0, 2, 3, 1))
+    close(ws.sum(0).view(G, 64, R, R, 4)[..., :cin], torch.stack(ref))
+
+
 @pytest.mark.parametrize("K,N", [(2048, 384), (384, 1284), (1284, 32), (32, 7), (128, 128)])
 def test_linear_as_1x1(K, N):
     from mauv import ops

@@ -12,6 +12,8 @@ Tolerances (stated per SURVEY.md §8c):
                        median / 90th-percentile / max per-tensor error vs fp64 are within
                        1.5x / 2x / 2x (+1e-4) of the CPU fp32 path's.
 """
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -46,6 +48,7 @@ def test_multimodal_train_step_parity(S, B, N):
     from mauv.kl import get_kl_loss
     from mauv import mchead
     o, m = build_pair()
+    o_pre = copy.deepcopy(o)   # fresh running statistics for the fp64 'truth' run
     batch = make_batches(SEED_DATA, 1, B=B, S_opt=S, S_son=S)[0]
     x, b, s, y = batch["main_image"], batch["bathy_image"], batch["sss_image"], batch["label"]
 
@@ -59,7 +62,7 @@ def test_multimodal_train_step_parity(S, B, N):
     with bridge:
         o_logits, loss_o = oracle_loss(o)
     bridge.collect()
-    o64, (l64, loss64) = oracle64(o, bridge.store, lambda mm: oracle_loss(mm, torch.float64))
+    o64, (l64, loss64) = oracle64(o_pre, bridge.store, lambda mm: oracle_loss(mm, torch.float64))
 
     root_state(m).eps_provider = bridge.provider
     logits = m.mc_forward(*_cuda(x, b, s), N)
@@ -74,11 +77,16 @@ def test_multimodal_train_step_parity(S, B, N):
     _assert_grads_as_accurate(list(m.parameters()), list(o.parameters()), list(o64.parameters()))
     # running statistics after N sequential train-mode passes
     obuf = dict(o.named_buffers())  # (the oracle also holds non-persistent eps/prior buffers)
+    tbuf = dict(o64.named_buffers())
     for n, bm in m.named_buffers():
         if "running_mean" in n:
             assert (bm.cpu() - obuf[n]).abs().max().item() <= 1e-5 + 1e-4 * obuf[n].abs().max(), n
         if "running_var" in n:
-            assert max_rel(bm, obuf[n]) <= 1e-4, n
+            # 1e-4 of the fp32 oracle, or — where the variance of a few layer-4 values is
+            # ill-conditioned at these shapes — as accurate vs the fp64 run as the fp32 oracle
+            ok = max_rel(bm, obuf[n]) <= 1e-4 or \
+                max_rel(bm, tbuf[n]) <= 2.0 * max_rel(obuf[n], tbuf[n]) + 1e-6
+            assert ok, (n, max_rel(bm, obuf[n]), max_rel(bm, tbuf[n]), max_rel(obuf[n], tbuf[n]))
         if "num_batches" in n:
             assert int(bm) == int(obuf[n]) == N
 
