@@ -98,12 +98,18 @@ def pmc_traffic():
 def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic=True, suffix="",
                   kernel="conv_gemm_f32 (implicit-GEMM fwd+dgrad+wgrad, all launches of one step)"):
     """Roofline of one step's implicit-GEMM launches of one precision (suffix "" = fp32,
-    "_bfloat16" = the 16-bit trunks; the fp32 fusion-head GEMMs are then excluded)."""
-    from mauv import ops
+    "_bfloat16" = the 16-bit trunks; the fp32 fusion-head GEMMs are then excluded).  The
+    three trunks run one after another in this step (no concurrent trunk streams), so each
+    launch's HIP-event duration is the kernel's own."""
+    from mauv import ops, engine
+    prev, engine.TRUNK_STREAMS = engine.TRUNK_STREAMS, False
     ops.PROFILE = []
-    torch.cuda.synchronize()
-    step_fn()
-    torch.cuda.synchronize()
+    try:
+        torch.cuda.synchronize()
+        step_fn()
+        torch.cuda.synchronize()
+    finally:
+        engine.TRUNK_STREAMS = prev
     rows, ops.PROFILE = ops.PROFILE, None
     by = {}
     nbytes = 0.0

@@ -32,6 +32,18 @@ DGRAD_BN_EPILOGUE = os.environ.get("MAUV_DGRAD_BN_EPILOGUE", "0") == "1"
 # fp32 stems on an NHWC copy of the images with 4 zero-padded channels (the pipelined split
 # kernel's STEM mode) instead of strided NCHW loads on the generic kernel
 F32_STEM_PACK = os.environ.get("MAUV_F32_STEM_PACK", "1") == "1"
+# The three trunks of MultiModalModel are independent until the fusion head: each runs its
+# forward and (autograd replays the forward's stream) its backward on a stream of its own, so
+# one trunk's memory-bound BN passes overlap another's MFMA-bound convs.
+TRUNK_STREAMS = os.environ.get("MAUV_TRUNK_STREAMS", "1") == "1"
+_STREAMS = {}
+
+
+def _trunk_streams(dev):
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _STREAMS:
+        _STREAMS[key] = [torch.cuda.Stream(device=dev) for _ in range(3)]
+    return _STREAMS[key]
 
 
 # ----------------------------------------------------------------------------- root state
@@ -259,9 +271,10 @@ class TrunkRunner(_Runner):
       its output gradient.
     """
 
-    def __init__(self, trunk, state, G, sample0, save, dtype=torch.float32):
+    def __init__(self, trunk, state, G, sample0, save, dtype=torch.float32, join=None):
         super().__init__(state, G, sample0, save)
         self.trunk = trunk
+        self.join = join  # caller's stream when this trunk runs on a stream of its own
         self.dt = dtype   # activation / sampled-weight storage (fp32, bf16 or f16)
 
     def _cin_pad(self, Cin):
@@ -431,6 +444,8 @@ class TrunkRunner(_Runner):
     def run_backward(self, dout):
         t, G, B = self.trunk, self.G, self.B
         self.st.grads(dout.device)
+        if self.join is not None:   # dout comes from the fusion head's stream
+            dout.record_stream(torch.cuda.current_stream())
         dout = dout.contiguous()
         if t.has_classifier():
             dfeat = self._linear_bwd(self.fc_rec, dout)
@@ -474,6 +489,10 @@ class TrunkRunner(_Runner):
         dy0, _ = self._bn_bwd(rb, da0)
         del da0
         self._conv_bwd(rc, dy0, need_dx=False)
+        if self.join is not None:   # the caller's stream (optimizer, all-reduce) waits for us
+            ev = torch.cuda.Event()
+            ev.record()
+            self.join.wait_event(ev)
         return (None,)
 
 
@@ -584,7 +603,7 @@ def _to_device(x, dev):
     return x if x.device == dev else x.to(dev, non_blocking=True)
 
 
-def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None):
+def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None, join=None):
     """[num_mc, B, 2048|C] for one ResNet trunk (root = the trunk unless ``state`` given)."""
     _check_trunk(trunk)
     st = state or root_state(trunk)
@@ -594,7 +613,7 @@ def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None):
     s0 = st.next_samples(num_mc) if sample0 is None else sample0
     params = list(trunk.parameters())
     save = needs_grad(params)
-    runner = TrunkRunner(trunk, st, num_mc, s0, save, st.trunk_dtype())
+    runner = TrunkRunner(trunk, st, num_mc, s0, save, st.trunk_dtype(), join)
     x = _to_device(x, dev)
     if x.dtype != torch.float32:   # autocast callers may hand 16-bit images; stems read fp32
         x = x.float()
@@ -608,10 +627,27 @@ def run_multimodal_mc(model, inputs, bathy, sss, num_mc):
         _check_trunk(trunk)
     dev = model.fc.mu_weight.device
     s0 = st.next_samples(num_mc)
-    f_img = run_trunk_mc(model.image_model_feat, inputs, num_mc, st, s0)
-    f_bathy = run_trunk_mc(model.bathy_model_feat, bathy, num_mc, st, s0)
-    f_sss = run_trunk_mc(model.sss_model_feat, sss, num_mc, st, s0)
     head_params = [p for n, p in model.named_parameters() if not n.split(".")[0].endswith("_feat")]
+    trunks = (model.image_model_feat, model.bathy_model_feat, model.sss_model_feat)
+    xs = (inputs, bathy, sss)
+    # concurrent trunks need the fusion head's backward to set up the gradient arena first
+    # (it runs on the caller's stream before any trunk backward)
+    if TRUNK_STREAMS and dev.type == "cuda" and (not torch.is_grad_enabled()
+                                                 or needs_grad(head_params)):
+        cur = torch.cuda.current_stream(dev)
+        feats = []
+        for trunk, x, ts in zip(trunks, xs, _trunk_streams(dev)):
+            ts.wait_stream(cur)
+            if x.is_cuda:
+                x.record_stream(ts)
+            with torch.cuda.stream(ts):
+                feats.append(run_trunk_mc(trunk, x, num_mc, st, s0, join=cur))
+        for f, ts in zip(feats, _trunk_streams(dev)):
+            cur.wait_stream(ts)
+            f.record_stream(cur)
+        f_img, f_bathy, f_sss = feats
+    else:
+        f_img, f_bathy, f_sss = (run_trunk_mc(t, x, num_mc, st, s0) for t, x in zip(trunks, xs))
     save = needs_grad(head_params) or any(f.requires_grad for f in (f_img, f_bathy, f_sss))
     runner = HeadRunner(model, st, num_mc, s0, save)
     return _run(runner, head_params, (f_img, f_bathy, f_sss), save)
