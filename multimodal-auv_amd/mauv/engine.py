@@ -17,6 +17,7 @@ Activations are NHWC ``[G][B][H][W][C]`` fp32.  The stems read one NHWC copy of 
 NCHW images with the channels zero-padded to 4 (16-bit path: 8), shared by all MC samples
 (group stride 0).
 """
+import contextlib
 import os
 
 import torch
@@ -36,13 +37,20 @@ F32_STEM_PACK = os.environ.get("MAUV_F32_STEM_PACK", "1") == "1"
 # forward and (autograd replays the forward's stream) its backward on a stream of its own, so
 # one trunk's memory-bound BN passes overlap another's MFMA-bound convs.
 TRUNK_STREAMS = os.environ.get("MAUV_TRUNK_STREAMS", "1") == "1"
+# Within a trunk's backward the weight gradient of each conv (+ its reparameterisation
+# backward) is off the critical dgrad -> BN-backward chain: MAUV_SIDE_WGRAD=1 runs it on a
+# side stream.  Off by default: with the three trunks already concurrent it measured neutral
+# (226-229 vs 228-230 triplets/s fp32, tools/gpubatch_streams.sh).
+SIDE_WGRAD = os.environ.get("MAUV_SIDE_WGRAD", "0") == "1"
 _STREAMS = {}
 
 
 def _trunk_streams(dev):
+    """(main, side) stream pairs of the three trunks."""
     key = dev.index if dev.index is not None else torch.cuda.current_device()
     if key not in _STREAMS:
-        _STREAMS[key] = [torch.cuda.Stream(device=dev) for _ in range(3)]
+        _STREAMS[key] = [(torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+                         for _ in range(3)]
     return _STREAMS[key]
 
 
@@ -271,10 +279,12 @@ class TrunkRunner(_Runner):
       its output gradient.
     """
 
-    def __init__(self, trunk, state, G, sample0, save, dtype=torch.float32, join=None):
+    def __init__(self, trunk, state, G, sample0, save, dtype=torch.float32, join=None,
+                 side=None):
         super().__init__(state, G, sample0, save)
         self.trunk = trunk
         self.join = join  # caller's stream when this trunk runs on a stream of its own
+        self.side = side  # stream for the weight gradients of the backward
         self.dt = dtype   # activation / sampled-weight storage (fp32, bf16 or f16)
 
     def _cin_pad(self, Cin):
@@ -315,13 +325,19 @@ class TrunkRunner(_Runner):
         st, pd = conv.stride[0], conv.padding[0]
         cp = self._cin_pad(Cin)
         if conv.mu_kernel.requires_grad:
-            splits = ops.wgrad_splits(G, B, H, W, cp, Cout, k, st, pd)
-            ws = torch.empty(splits, G, Cout, k * k * cp, device=dy.device)
-            ops.conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, cp, Cout, k, st, pd,
-                                  x_strides=xs, x_bn=x_bn, alg_cin=Cin)
-            self._reparam_bwd(conv, conv.mu_kernel, conv.rho_kernel, ws, splits, Cout, Cin,
-                              k * k, "kernel", dw_cin=cp)
-            del ws
+            side = self.side
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream())
+                for t in (x, dy) + (tuple(x_bn[:2]) if x_bn is not None else ()):
+                    t.record_stream(side)
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                splits = ops.wgrad_splits(G, B, H, W, cp, Cout, k, st, pd)
+                ws = torch.empty(splits, G, Cout, k * k * cp, device=dy.device)
+                ops.conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, cp, Cout, k, st, pd,
+                                      x_strides=xs, x_bn=x_bn, alg_cin=Cin)
+                self._reparam_bwd(conv, conv.mu_kernel, conv.rho_kernel, ws, splits, Cout, Cin,
+                                  k * k, "kernel", dw_cin=cp)
+                del ws
         if not need_dx:
             return None, None
         if dx is None:
@@ -489,6 +505,8 @@ class TrunkRunner(_Runner):
         dy0, _ = self._bn_bwd(rb, da0)
         del da0
         self._conv_bwd(rc, dy0, need_dx=False)
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
         if self.join is not None:   # the caller's stream (optimizer, all-reduce) waits for us
             ev = torch.cuda.Event()
             ev.record()
@@ -603,7 +621,7 @@ def _to_device(x, dev):
     return x if x.device == dev else x.to(dev, non_blocking=True)
 
 
-def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None, join=None):
+def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None, join=None, side=None):
     """[num_mc, B, 2048|C] for one ResNet trunk (root = the trunk unless ``state`` given)."""
     _check_trunk(trunk)
     st = state or root_state(trunk)
@@ -613,7 +631,7 @@ def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None, join=None):
     s0 = st.next_samples(num_mc) if sample0 is None else sample0
     params = list(trunk.parameters())
     save = needs_grad(params)
-    runner = TrunkRunner(trunk, st, num_mc, s0, save, st.trunk_dtype(), join)
+    runner = TrunkRunner(trunk, st, num_mc, s0, save, st.trunk_dtype(), join, side)
     x = _to_device(x, dev)
     if x.dtype != torch.float32:   # autocast callers may hand 16-bit images; stems read fp32
         x = x.float()
@@ -636,13 +654,14 @@ def run_multimodal_mc(model, inputs, bathy, sss, num_mc):
                                                  or needs_grad(head_params)):
         cur = torch.cuda.current_stream(dev)
         feats = []
-        for trunk, x, ts in zip(trunks, xs, _trunk_streams(dev)):
+        for trunk, x, (ts, side) in zip(trunks, xs, _trunk_streams(dev)):
             ts.wait_stream(cur)
             if x.is_cuda:
                 x.record_stream(ts)
             with torch.cuda.stream(ts):
-                feats.append(run_trunk_mc(trunk, x, num_mc, st, s0, join=cur))
-        for f, ts in zip(feats, _trunk_streams(dev)):
+                feats.append(run_trunk_mc(trunk, x, num_mc, st, s0, join=cur,
+                                          side=side if SIDE_WGRAD else None))
+        for f, (ts, _) in zip(feats, _trunk_streams(dev)):
             cur.wait_stream(ts)
             f.record_stream(cur)
         f_img, f_bathy, f_sss = feats
