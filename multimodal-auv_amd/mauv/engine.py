@@ -648,10 +648,13 @@ def run_multimodal_mc(model, inputs, bathy, sss, num_mc):
     head_params = [p for n, p in model.named_parameters() if not n.split(".")[0].endswith("_feat")]
     trunks = (model.image_model_feat, model.bathy_model_feat, model.sss_model_feat)
     xs = (inputs, bathy, sss)
-    # concurrent trunks need the fusion head's backward to set up the gradient arena first
-    # (it runs on the caller's stream before any trunk backward)
-    if TRUNK_STREAMS and dev.type == "cuda" and (not torch.is_grad_enabled()
-                                                 or needs_grad(head_params)):
+    # Training only: concurrent trunks need the fusion head's backward to set up the gradient
+    # arena first (it runs on the caller's stream before any trunk backward).  MC inference
+    # keeps the trunks in sequence: its chunks are sized to fill HBM with one trunk's
+    # activations (predict.mc_chunk), and three concurrent trunks measured +2 % at best while
+    # tripling the peak (caching-allocator retries when HBM is already held: 5.3k vs 9.7k/s).
+    if TRUNK_STREAMS and dev.type == "cuda" and torch.is_grad_enabled() \
+            and needs_grad(head_params):
         cur = torch.cuda.current_stream(dev)
         feats = []
         for trunk, x, (ts, side) in zip(trunks, xs, _trunk_streams(dev)):
