@@ -1,7 +1,8 @@
 // Pipelined split-fp32 implicit-GEMM convolution: the default arithmetic of every fp32 conv of
 // the three ResNet-50 trunks (models/base_models.py:15-18, models/model_utils.py:57-61) and of
 // the fusion head's linears, forward / data gradient / weight gradient, on the vector paths
-// (all convs but the 1- and 3-channel stems, which stay on conv_gemm.hip).
+// (every conv of the path; the 1- and 3-channel stems through their STEM mode over images packed
+// to 4 zero-padded NHWC channels — other channel counts fall back to conv_gemm.hip).
 //
 // Arithmetic (conv_gemm.hip header, include/mauv.h mauv_set_f32_math): each fp32 operand
 // element is split exactly into bf16 planes x = h + m + l and the product a.b is accumulated in
@@ -20,6 +21,8 @@
 // LDS images are conv_gemm16.hip's: k-contiguous operands (FWD A/B, DGRAD A) as row images
 // [rows][BK+8] (one ds_read_b128 per fragment), k-strided ones (DGRAD B, WGRAD A/B) as col images
 // [BK][rows+32] (two ds_read_b64_tr_b16).  Epilogue: conv_common.h (shared with conv_gemm.hip).
+// ABL_SPLIT_A / ABL_SPLIT_B (compile-time, never in the product build) store one plane of the
+// A / B operand instead of its exact split: timing ablation only (tools/gpubatch_ablsplit.sh).
 #include <stdlib.h>
 
 #include "conv_common.h"
@@ -291,7 +294,11 @@ void conv_split_f32(const ConvArgs a) {
       u16* dst = act ? As + off : dum;
       const int pst = act ? A_PL : 4;
       uint2 pl[3];
+#ifdef ABL_SPLIT_A
+      pl[0].x = pk_bf16(v[0], v[1]); pl[0].y = pk_bf16(v[2], v[3]); pl[1] = pl[2] = make_uint2(0, 0);
+#else
       split_bf16<3>(v, pl);
+#endif
 #pragma unroll
       for (int p = 0; p < 3; ++p) *(uint2*)(dst + p * pst) = pl[p];
     }
@@ -306,7 +313,11 @@ void conv_split_f32(const ConvArgs a) {
       u16* dst = act ? Bs + off : dum;
       const int pst = act ? B_PL : 4;
       uint2 pl[3];
+#ifdef ABL_SPLIT_B
+      pl[0].x = pk_bf16(v[0], v[1]); pl[0].y = pk_bf16(v[2], v[3]); pl[1] = pl[2] = make_uint2(0, 0);
+#else
       split_bf16<3>(v, pl);
+#endif
 #pragma unroll
       for (int p = 0; p < 3; ++p) *(uint2*)(dst + p * pst) = pl[p];
     }
