@@ -79,8 +79,10 @@ int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strides, const
  * MAUV_F32_MATH=split|split3|exact):
  *   6 split (default): every fp32 operand is split exactly into three bf16 planes
  *     x = h + m + l and the six plane products h*h, h*m, m*h, h*l, l*h, m*m run on
- *     v_mfma_f32_32x32x16_bf16 with fp32 accumulation (h*h in its own accumulator); the
- *     dropped terms are <= 2^-24 |a*b| — fp32-grade results at 2.67x the f32-MFMA rate;
+ *     v_mfma_f32_32x32x16_bf16 with fp32 accumulation (h*h in its own accumulator on the
+ *     four-wave tiles; one accumulator on the default eight-wave tiles); the dropped terms
+ *     are <= 2^-24 |a*b| — fp32-grade results at 2.67x the f32-MFMA rate;
+ *   5 split1: the same with one accumulator everywhere;
  *   3 split3: planes (h, m), products h*h, h*m, m*h (~2^-16 |a*b|; opt-in);
  *   0 exact: v_mfma_f32_32x32x2_f32 (an fmaf chain).
  * mode -1 queries.  Returns the previous mode, or < 0 for an invalid mode. */
