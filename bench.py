@@ -179,7 +179,7 @@ def main():
 
     from mauv.models import define_models, DEFAULT_PRIOR
     from mauv.train import mc_train_step
-    from mauv.predict import mc_statistics
+    from mauv.predict import mc_statistics, mc_chunk
 
     torch.manual_seed(0)
     model = define_models(None, 7, DEFAULT_PRIOR)["multimodal_model"].to(dev)
@@ -282,9 +282,15 @@ def main():
 
         def infer_run(autocast):
             # the reference predictor wraps its MC loop in torch.amp.autocast (predictors.py:55):
-            # on a GPU that is f16, which the trunks follow; autocast=False -> fp32 trunks
+            # on a GPU that is f16, which the trunks follow; autocast=False -> fp32 trunks.
+            # Training's cached blocks are released first and the warm-up runs one full MC
+            # chunk, so the timed batch reuses its activation blocks instead of growing (or,
+            # near the HBM limit, flushing and retrying) the caching allocator mid-run.
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            chunk = mc_chunk(model, args.infer_batch, args.infer_mc)
             with torch.no_grad(), torch.autocast("cuda", enabled=autocast):
-                mc_statistics(model, xi, bi, si, max(world, 2), group=group)   # warm-up
+                mc_statistics(model, xi, bi, si, max(world, 2) * chunk, group=group)   # warm-up
                 di = timed(lambda: mc_statistics(model, xi, bi, si, args.infer_mc, group=group), 1)
             return {"value": round(args.infer_mc * args.infer_batch / di, 2),
                     "unit": "MC-samples/s", "batch": args.infer_batch, "num_mc": args.infer_mc,

@@ -349,15 +349,21 @@ void conv_pipe16(const ConvArgs a) {
   if constexpr (XBN && MODE == FWD) __syncthreads();  // xbn staged
   store(S0, 0);
   __syncthreads();
-  for (int t = 0; t < nt; t += 2) {
+  for (int t = 0; t + 1 < nt; t += 2) {
     load(S0, t + 2);
     compute(0);
     store(S1, 1);
     __syncthreads();
-    load(S1, t + 3);  // (odd nt: one all-zero tile rather than a branch out of the pair)
+    load(S1, t + 3);
     compute(1);
     store(S0, 0);
     __syncthreads();
+  }
+  // odd nt (1x1 over 64 channels, 3x3 over 64: 9 taps, the stems' 7 rows): the last tile sits
+  // in buffer 0 — computed here, outside the branch-free loop body
+  if (nt & 1) {
+    compute(0);
+    __syncthreads();  // the epilogue reuses the operand buffers
   }
 
   // ---------------- epilogue ----------------
