@@ -1,4 +1,5 @@
 # A/B: bn_bwd_partial with four rows in flight per thread (libmauv_hip.so) vs before (libmauv_bnold.so)
+# (record of a measured experiment whose code was removed: see DESIGN.md; the variable it sets is no longer read)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_kernels16_gpu.py -k "bn" > gpurun_out/bu_tests.log 2>&1 || { tail -30 gpurun_out/bu_tests.log; exit 1; }

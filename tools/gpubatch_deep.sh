@@ -1,4 +1,5 @@
 # A/B: three register stages (loads three tiles ahead) in the eight-wave 128x128 split kernel
+# (record of a measured experiment whose code was removed: see DESIGN.md; the variable it sets is no longer read)
 set -o pipefail
 mkdir -p gpurun_out
 MAUV_SPLIT_DEEP=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_kernels_gpu.py tests/test_f32_math_gpu.py tests/test_model_gpu.py > gpurun_out/deep_tests.log 2>&1 || { tail -30 gpurun_out/deep_tests.log; exit 1; }

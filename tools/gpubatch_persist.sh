@@ -1,4 +1,5 @@
 # A/B: persistent 16-bit conv blocks for short-K launches (MAUV_P16_PERSIST = max stages)
+# (record of a measured experiment whose code was removed: see DESIGN.md; the variable it sets is no longer read)
 set -o pipefail
 mkdir -p gpurun_out
 MAUV_P16_PERSIST=16 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels16_gpu.py tests/test_model16_gpu.py > gpurun_out/ps_tests.log 2>&1 || { tail -30 gpurun_out/ps_tests.log; exit 1; }

@@ -1,4 +1,5 @@
 # A/B: L2 prefetch touches in the split kernel (MAUV_SPLIT_PF)
+# (record of a measured experiment whose code was removed: see DESIGN.md; the variable it sets is no longer read)
 set -o pipefail
 mkdir -p gpurun_out
 MAUV_SPLIT_PF=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_f32_math_gpu.py > gpurun_out/pf_tests.log 2>&1 || { tail -30 gpurun_out/pf_tests.log; exit 1; }
