@@ -693,6 +693,8 @@ MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx
       a.M = B * a.Hc * a.Wc;
       a.K = a.nr * a.ns * Cout;  // 0 -> the class only receives the addend / zeros
       if (a.M <= 0) continue;
+      // a tapless class accumulating into dx adds nothing (stride-2 1x1 downsample: 3 of 4)
+      if (a.K == 0 && accumulate && !addend && !bn_p1) continue;
       const int fm = f32_math();
       if ((fm == 6 || fm == 5) && conv_split_launch(DGRAD, a, fm == 5, stream)) {}
       else if (va && vb) launch_tiles<DGRAD, true, true>(a, stream);

@@ -573,6 +573,8 @@ MAUV_API int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, 
       a.M = B * a.Hc * a.Wc;
       a.K = a.nr * a.ns * Cout;
       if (a.M <= 0) continue;
+      // a tapless class accumulating into dx adds nothing (stride-2 1x1 downsample: 3 of 4)
+      if (a.K == 0 && accumulate && !addend) continue;
       if (!conv_pipe16_launch(DGRAD, dtype, pipe_args(a), stream))
         dispatch16<H_DGRAD, true>(dtype, a, stream);
     }

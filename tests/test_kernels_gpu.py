@@ -146,6 +146,32 @@ def test_stem_packed_nhwc4(cin, H, R):
     close(ws.sum(0).view(G, 64, R, R, 4)[..., :cin], torch.stack(ref))
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+@pytest.mark.parametrize("R,st,pd", [(1, 2, 0), (3, 2, 1), (1, 1, 0)])
+def test_dgrad_accumulate_into_dx(dt, R, st, pd):
+    """dx += dgrad(dy, w) (the downsample branch adding into the main branch's dx): classes of a
+    strided conv without taps leave dx untouched."""
+    from mauv import ops
+    G, B, H, Cin, Cout = 2, 2, 9, 64, 128
+    torch.manual_seed(4)
+    Ho = ops.out_hw(H, R, st, pd)
+    dy = torch.randn(G, B, Ho, Ho, Cout).to(dt)
+    w = (torch.randn(G, Cout, R, R, Cin) / (Cin * R * R) ** 0.5).to(dt)
+    dx0 = torch.randn(G, B, H, H, Cin).to(dt)
+    dx = dx0.to(dev).clone()
+    ops.conv2d_bwd_data(dy.to(dev), w.to(dev), dx, G, B, H, H, Cin, Cout, R, st, pd,
+                        accumulate=True)
+    ref = []
+    for g in range(G):
+        xg = torch.zeros(B, Cin, H, H, dtype=torch.float64, requires_grad=True)
+        F.conv2d(xg, w[g].permute(0, 3, 1, 2).double(), stride=st, padding=pd).backward(
+            dy[g].permute(0, 3, 1, 2).double())
+        ref.append(xg.grad.permute(0, 2, 3, 1))
+    ref = torch.stack(ref) + dx0.double()
+    tol = 1e-5 if dt == torch.float32 else 2 ** -7
+    close(dx.float(), ref, rtol=tol, atol=tol)
+
+
 @pytest.mark.parametrize("K,N", [(2048, 384), (384, 1284), (1284, 32), (32, 7), (128, 128)])
 def test_linear_as_1x1(K, N):
     from mauv import ops
