@@ -10,6 +10,8 @@
 // Layout: y/out/dout [G][M][C] (NHWC rows, M = B*H*W), per-group stats [G][C].
 // Statistics: per-thread Welford over a row slab, Chan merges across threads and blocks
 // (double in the final merge) — no E[x^2]-E[x]^2 cancellation.
+#include <cstdlib>
+
 #include "h16.h"
 
 using namespace mauv;
@@ -447,6 +449,139 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const typename S::T* __restr
   }
 }
 
+// bn_bwd_partial geometry: C/8 threads span a row, so a 256-thread block walks 256/(C/8)
+// rows at once; at most 16 rows per thread keeps G*nblk in the hundreds-to-thousands for the
+// deep, narrow-M layers (layer4: M = B*49 rows of 2048 channels) that one-block-per-256-rows
+// left at ~13 blocks per group, at the cost of <= 1/16 extra partial traffic per element.
+static int ew_grid(long long n4);
+
+// Row-walk forms of the two elementwise passes (the default): C/8 threads span a row, 256/(C/8)
+// rows are walked in parallel and each block takes rpb consecutive rows, so a thread keeps its
+// 8 channels' per-group parameters in registers for the whole slab and its offsets need no
+// 64-bit modulo — the grid-stride forms above reload scale/shift (L1 hits, but issue slots) and
+// divide per element group, which is what held the 16-bit passes (48 B of HBM traffic per
+// iteration) well below the fp32 ones' bandwidth.  C <= 2048.
+template <class S>
+__global__ __launch_bounds__(256) void bn_apply_rows(const typename S::T* __restrict__ y,
+                                                     const float* __restrict__ scale,
+                                                     const float* __restrict__ shift,
+                                                     const typename S::T* __restrict__ res,
+                                                     const float* __restrict__ res_scale,
+                                                     const float* __restrict__ res_shift,
+                                                     int relu, typename S::T* __restrict__ out,
+                                                     long long M, int C, int rpb) {
+  const int tpr = C / 8, rp = 256 / tpr;
+  const int tid = threadIdx.x, t_c = tid % tpr, t_r = tid / tpr;
+  if (t_r >= rp) return;
+  const int g = blockIdx.y;
+  const long long r0 = (long long)blockIdx.x * rpb;
+  const long long r1 = min(M, r0 + rpb);
+  const int c0 = 8 * t_c, gc = g * C + c0;
+  const floatx8 sc = ldf8(scale + gc), sh = ldf8(shift + gc);
+  floatx8 rsc, rsh;
+  if (res_scale) { rsc = ldf8(res_scale + gc); rsh = ldf8(res_shift + gc); }
+  const long long base = (long long)g * M * C + c0;
+#pragma unroll 2
+  for (long long r = r0 + t_r; r < r1; r += rp) {
+    const long long o = base + r * C;
+    floatx8 v = S::ld8(y + o) * sc + sh;
+    if (res) {
+      floatx8 rv = S::ld8(res + o);
+      if (res_scale) rv = rv * rsc + rsh;
+      v += rv;
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+    }
+    S::st8(out + o, v);
+  }
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void bn_bwd_apply_rows(const typename S::T* __restrict__ y,
+                                                         const typename S::T* __restrict__ out,
+                                                         const typename S::T* __restrict__ dout,
+                                                         int relu,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift,
+                                                         const float* __restrict__ k1,
+                                                         const float* __restrict__ k2,
+                                                         typename S::T* __restrict__ dy,
+                                                         typename S::T* __restrict__ dres,
+                                                         long long M, int C, int rpb) {
+  const int tpr = C / 8, rp = 256 / tpr;
+  const int tid = threadIdx.x, t_c = tid % tpr, t_r = tid / tpr;
+  if (t_r >= rp) return;
+  const int g = blockIdx.y;
+  const long long r0 = (long long)blockIdx.x * rpb;
+  const long long r1 = min(M, r0 + rpb);
+  const int c0 = 8 * t_c, gc = g * C + c0;
+  const floatx8 sc = ldf8(scale + gc), mu = ldf8(mean + gc), is = ldf8(invstd + gc);
+  const floatx8 a1 = ldf8(k1 + gc), a2 = ldf8(k2 + gc);
+  floatx8 sh = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (relu && !out) sh = ldf8(shift + gc);
+  const long long base = (long long)g * M * C + c0;
+#pragma unroll 2
+  for (long long r = r0 + t_r; r < r1; r += rp) {
+    const long long o = base + r * C;
+    floatx8 dz = S::ld8(dout + o);
+    const floatx8 yv = S::ld8(y + o);
+    if (relu) {
+      const floatx8 pre = out ? S::ld8(out + o) : yv * sc + sh;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dz[e] = pre[e] > 0.f ? dz[e] : 0.f;
+    }
+    const floatx8 xh = (yv - mu) * is;
+    S::st8(dy + o, sc * (dz - a1 - xh * a2));
+    if (dres) S::st8(dres + o, dz);
+  }
+}
+
+// Row-walk geometry: <= 8 rows per thread.
+static void rows_geometry(long long M, int C, int& nblk, int& rpb) {
+  const int rp = 256 / (C / 8);
+  const long long r = (long long)rp * 8;
+  rpb = (int)r;
+  nblk = (int)((M + r - 1) / r);
+}
+
+static bool use_rows(int C) {
+  static const int on = [] {
+    const char* e = getenv("MAUV_BN_ROWS");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on && C % 8 == 0 && C <= 2048;
+}
+
+template <class S>
+static void launch_apply(const typename S::T* y, const float* scale, const float* shift,
+                         const typename S::T* res, const float* res_scale, const float* res_shift,
+                         int relu, typename S::T* out, int G, long long M, int C,
+                         hipStream_t stream) {
+  if (use_rows(C)) {
+    int nblk, rpb;
+    rows_geometry(M, C, nblk, rpb);
+    hipLaunchKernelGGL(bn_apply_rows<S>, dim3(nblk, G), dim3(256), 0, stream, y, scale, shift,
+                       res, res_scale, res_shift, relu, out, M, C, rpb);
+  } else {
+    hipLaunchKernelGGL(bn_apply_kernel<S>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, stream, y,
+                       scale, shift, res, res_scale, res_shift, relu, out, M, C);
+  }
+}
+
+static void bwd_geometry(long long M, int C, int& nblk, int& rpb) {
+  const int rp = 256 / (C / 8);
+  long long r = (long long)rp * 16;
+  long long n = (M + r - 1) / r;
+  if (n > 1024) { n = 1024; r = (M + n - 1) / n; }
+  if (r < rp) r = rp;
+  rpb = (int)r;
+  nblk = (int)((M + r - 1) / r);
+}
+
 static void reduce_geometry(long long M, int C, int& nblk, int& rpb) {
   const RowMap rm = row_map(C);
   long long target = (M + 255) / 256;  // ~256 rows per block
@@ -489,9 +624,13 @@ MAUV_API int mauv_bn_eval_params(int G, int C, const float* gamma, const float* 
 
 // Workspace floats needed by mauv_bn_fwd_train / mauv_bn_bwd for (G, M, C).
 MAUV_API long long mauv_bn_workspace_floats(int G, long long M, int C) {
-  int nblk, rpb;
+  int nblk, rpb, bnblk, brpb;
   reduce_geometry(M, C, nblk, rpb);
-  return (long long)G * nblk * (2LL * C + 1) + 2LL * G * C + stats_ws_floats(G, nblk, C);
+  const long long fwd = (long long)G * nblk * (2LL * C + 1) + 2LL * G * C + stats_ws_floats(G, nblk, C);
+  if (C <= 0 || C % 8 != 0 || C > 2048) return fwd;
+  bwd_geometry(M, C, bnblk, brpb);
+  const long long bwd = 2LL * G * bnblk * C + 2LL * G * C;
+  return fwd > bwd ? fwd : bwd;
 }
 
 // Workspace floats of mauv_bn_stats_finalize for nblk partials per channel.
@@ -522,8 +661,7 @@ MAUV_API int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const 
     hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
                        mean, uvar, run_mean, run_var, momentum);
   if (out) {
-    hipLaunchKernelGGL(bn_apply_kernel<SF32>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, stream,
-                       y, scale, shift, res, nullptr, nullptr, relu, out, M, C);
+    launch_apply<SF32>(y, scale, shift, res, nullptr, nullptr, relu, out, G, M, C, stream);
   }
   return check_launch("bn_fwd_train");
 }
@@ -549,8 +687,7 @@ MAUV_API int mauv_bn_apply(const float* y, const float* scale, const float* shif
                            const float* res, const float* res_scale, const float* res_shift,
                            int relu, float* out, int G, long long M, int C, hipStream_t stream) {
   if (C % 8 != 0) { set_error("bn_apply: C % 8 != 0"); return kErrArg; }
-  hipLaunchKernelGGL(bn_apply_kernel<SF32>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, stream, y,
-                     scale, shift, res, res_scale, res_shift, relu, out, M, C);
+  launch_apply<SF32>(y, scale, shift, res, res_scale, res_shift, relu, out, G, M, C, stream);
   return check_launch("bn_apply");
 }
 
@@ -564,7 +701,7 @@ static int bn_bwd_impl(const typename S::T* y, const typename S::T* out,
   if (C % 8 != 0 || C > 2048) { set_error("bn_bwd: unsupported C (C % 8 != 0 or > 2048)"); return kErrArg; }
   if (relu && !out && !shift) { set_error("bn_bwd: relu mask needs out or scale/shift"); return kErrArg; }
   int nblk, rpb;
-  reduce_geometry(M, C, nblk, rpb);
+  bwd_geometry(M, C, nblk, rpb);
   const RowMap rm = row_map(C);
   float* p1 = workspace;
   float* p2 = p1 + (long long)G * nblk * C;
@@ -582,8 +719,15 @@ static int bn_bwd_impl(const typename S::T* y, const typename S::T* out,
   if (dgamma || dbeta)
     hipLaunchKernelGGL(bn_bwd_param_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C, M,
                        k1, k2, dgamma, dbeta);
-  hipLaunchKernelGGL(bn_bwd_apply<S>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, stream, y, out,
-                     dout, relu, mean, invstd, scale, shift, k1, k2, dy, dres, M, C);
+  if (use_rows(C)) {
+    int anblk, arpb;
+    rows_geometry(M, C, anblk, arpb);
+    hipLaunchKernelGGL(bn_bwd_apply_rows<S>, dim3(anblk, G), dim3(256), 0, stream, y, out, dout,
+                       relu, mean, invstd, scale, shift, k1, k2, dy, dres, M, C, arpb);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_apply<S>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, stream, y, out,
+                       dout, relu, mean, invstd, scale, shift, k1, k2, dy, dres, M, C);
+  }
   return check_launch("bn_bwd");
 }
 
@@ -607,9 +751,8 @@ MAUV_API int mauv_bn_apply_h16(int dtype, const void* y, const float* scale, con
                                int relu, void* out, int G, long long M, int C,
                                hipStream_t stream) {
   if (C % 8 != 0) { set_error("bn_apply_h16: C % 8 != 0"); return kErrArg; }
-#define L(D) hipLaunchKernelGGL(bn_apply_kernel<S16<D>>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, \
-                                stream, (const u16*)y, scale, shift, (const u16*)res, res_scale,    \
-                                res_shift, relu, (u16*)out, M, C);
+#define L(D) launch_apply<S16<D>>((const u16*)y, scale, shift, (const u16*)res, res_scale,  \
+                                  res_shift, relu, (u16*)out, G, M, C, stream);
   MAUV_DT_DISPATCH(dtype, "bn_apply_h16", L)
 #undef L
   return check_launch("bn_apply_h16");

@@ -197,7 +197,8 @@ def test_linear_as_1x1(K, N):
     close(db, dy.double().sum(1))
 
 
-@pytest.mark.parametrize("C,relu,res", [(64, True, False), (256, True, True), (2048, False, False)])
+@pytest.mark.parametrize("C,relu,res", [(64, True, False), (256, True, True), (2048, False, False),
+                                        (24, True, True)])
 def test_bn_fwd_bwd(C, relu, res):
     from mauv import ops
     G, B, H = 3, 4, 5
@@ -464,3 +465,19 @@ def test_bn_stats_finalize_segmented(nblk):
     for g in range(G):
         ref_rv = 0.9 * ref_rv + 0.1 * uvar[g]
     close(rv, ref_rv, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("C,M", [(24, 1000), (512, 1000), (2056, 37), (64, 3000)])
+def test_bn_apply_row_walk_ragged(C, M):
+    """Row-walk apply (C <= 2048; 256/(C/8) rows in parallel, 8 rows a thread) over ragged
+    row counts and a non-power-of-two C; C > 2048 takes the grid-stride form."""
+    from mauv import ops
+    G = 3
+    torch.manual_seed(11)
+    y = torch.randn(G, M, C, device=dev)
+    r = torch.randn(G, M, C, device=dev)
+    s, h = torch.randn(G, C, device=dev), torch.randn(G, C, device=dev)
+    out = torch.full((G, M, C), float("nan"), device=dev)
+    ops.bn_apply(y, s, h, r, True, out, G, M, C)
+    ref = torch.relu(y.double() * s.double()[:, None] + h.double()[:, None] + r.double())
+    assert torch.allclose(out.double(), ref, rtol=1e-6, atol=1e-6)
