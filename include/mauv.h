@@ -231,6 +231,12 @@ int mauv_maxpool_fwd(const float* x, int N, int H, int W, int C, float* y, unsig
                      hipStream_t stream);
 int mauv_maxpool_bwd(const float* dy, const unsigned char* idx, int N, int H, int W, int C,
                      float* dx, hipStream_t stream);
+/* The stem's pending BatchNorm + ReLU applied on load (out = maxpool(relu(y*scale[g] +
+ * shift[g])), group g = image / (N/G)): the 112x112 BN output is never materialised.
+ * Replaces the bn1 -> relu -> maxpool sequence of torchvision's ResNet stem
+ * (models/base_models.py:15-16 builds it).  idx nullable (inference) in every maxpool entry. */
+int mauv_maxpool_bn_fwd(const float* y, const float* scale, const float* shift, int G, int N,
+                        int H, int W, int C, float* out, unsigned char* idx, hipStream_t stream);
 int mauv_avgpool_fwd(const float* x, int N, int HW, int C, float* y, hipStream_t stream);
 int mauv_avgpool_bwd(const float* dy, int N, int HW, int C, float* dx, hipStream_t stream);
 /* 16-bit activations; the pooled features / their gradient stay fp32 (the head is fp32). */
@@ -238,6 +244,9 @@ int mauv_maxpool_fwd_h16(int dtype, const void* x, int N, int H, int W, int C, v
                          unsigned char* idx, hipStream_t stream);
 int mauv_maxpool_bwd_h16(int dtype, const void* dy, const unsigned char* idx, int N, int H,
                          int W, int C, void* dx, hipStream_t stream);
+int mauv_maxpool_bn_fwd_h16(int dtype, const void* y, const float* scale, const float* shift,
+                            int G, int N, int H, int W, int C, void* out, unsigned char* idx,
+                            hipStream_t stream);
 int mauv_avgpool_fwd_h16(int dtype, const void* x, int N, int HW, int C, float* y,
                          hipStream_t stream);
 int mauv_avgpool_bwd_h16(int dtype, const float* dy, int N, int HW, int C, void* dx,

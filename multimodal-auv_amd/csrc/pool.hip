@@ -15,7 +15,10 @@ template <class S>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const typename S::T* __restrict__ x,
                                                           int N, int H, int W, int C, int Ho,
                                                           int Wo, typename S::T* __restrict__ y,
-                                                          unsigned char* __restrict__ idx) {
+                                                          unsigned char* __restrict__ idx,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift,
+                                                          int npg) {
   const int C4 = C / 4;
   const long long total = (long long)N * Ho * Wo * C4;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
@@ -26,20 +29,36 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const typename S::T* _
     const int n = (int)(p / Ho);
     floatx4 best = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     int bi[4] = {0, 0, 0, 0};
+    floatx4 sc, sh;
+    if (scale) {  // pending BN + ReLU of the stem, applied on load (group g = n / npg)
+      const int gc = (n / npg) * C + c;
+      sc = *(const floatx4*)(scale + gc);
+      sh = *(const floatx4*)(shift + gc);
+    }
     for (int r = 0; r < 3; ++r) {
       const int ih = oh * 2 - 1 + r;
       if (ih < 0 || ih >= H) continue;
       for (int s = 0; s < 3; ++s) {
         const int iw = ow * 2 - 1 + s;
         if (iw < 0 || iw >= W) continue;
-        const floatx4 v = S::ld4(x + (((long long)n * H + ih) * W + iw) * C + c);
+        floatx4 v = S::ld4(x + (((long long)n * H + ih) * W + iw) * C + c);
+        if (scale) {
+          // exactly what bn_apply would have stored: relu(y*scale + shift) in fp32, rounded to
+          // the storage type — so maxima and tie-breaks match the materialised path
+          v = v * sc + sh;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+          alignas(16) typename S::T tmp[4];
+          S::st4(tmp, v);
+          v = S::ld4(tmp);
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (v[e] > best[e] || isnan(v[e])) { best[e] = v[e]; bi[e] = r * 3 + s; }
       }
     }
     S::st4(y + 4 * i, best);
-    *(uchar4*)(idx + 4 * i) = make_uchar4(bi[0], bi[1], bi[2], bi[3]);
+    if (idx) *(uchar4*)(idx + 4 * i) = make_uchar4(bi[0], bi[1], bi[2], bi[3]);
   }
 }
 
@@ -135,8 +154,18 @@ MAUV_API int mauv_maxpool_fwd(const float* x, int N, int H, int W, int C, float*
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   if (C % 4) { set_error("maxpool_fwd: C % 4 != 0"); return kErrArg; }
   hipLaunchKernelGGL(maxpool_fwd_kernel<SF32>, dim3(grid1((long long)N * Ho * Wo * C / 4)), dim3(256),
-                     0, stream, x, N, H, W, C, Ho, Wo, y, idx);
+                     0, stream, x, N, H, W, C, Ho, Wo, y, idx, nullptr, nullptr, 1);
   return check_launch("maxpool_fwd");
+}
+
+MAUV_API int mauv_maxpool_bn_fwd(const float* y, const float* scale, const float* shift, int G,
+                                 int N, int H, int W, int C, float* out, unsigned char* idx,
+                                 hipStream_t stream) {
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  if (C % 4 || G <= 0 || N % G) { set_error("maxpool_bn_fwd: C % 4 != 0 or N % G != 0"); return kErrArg; }
+  hipLaunchKernelGGL(maxpool_fwd_kernel<SF32>, dim3(grid1((long long)N * Ho * Wo * C / 4)), dim3(256),
+                     0, stream, y, N, H, W, C, Ho, Wo, out, idx, scale, shift, N / G);
+  return check_launch("maxpool_bn_fwd");
 }
 
 MAUV_API int mauv_maxpool_bwd(const float* dy, const unsigned char* idx, int N, int H, int W,
@@ -168,10 +197,24 @@ MAUV_API int mauv_maxpool_fwd_h16(int dtype, const void* x, int N, int H, int W,
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   if (C % 4) { set_error("maxpool_fwd_h16: C % 4 != 0"); return kErrArg; }
 #define L(D) hipLaunchKernelGGL(maxpool_fwd_kernel<S16<D>>, dim3(grid1((long long)N * Ho * Wo * C / 4)), \
-                                dim3(256), 0, stream, (const u16*)x, N, H, W, C, Ho, Wo, (u16*)y, idx);
+                                dim3(256), 0, stream, (const u16*)x, N, H, W, C, Ho, Wo, (u16*)y, idx, \
+                                nullptr, nullptr, 1);
   MAUV_DT_DISPATCH(dtype, "maxpool_fwd_h16", L)
 #undef L
   return check_launch("maxpool_fwd_h16");
+}
+
+MAUV_API int mauv_maxpool_bn_fwd_h16(int dtype, const void* y, const float* scale,
+                                     const float* shift, int G, int N, int H, int W, int C,
+                                     void* out, unsigned char* idx, hipStream_t stream) {
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  if (C % 4 || G <= 0 || N % G) { set_error("maxpool_bn_fwd_h16: C % 4 != 0 or N % G != 0"); return kErrArg; }
+#define L(D) hipLaunchKernelGGL(maxpool_fwd_kernel<S16<D>>, dim3(grid1((long long)N * Ho * Wo * C / 4)), \
+                                dim3(256), 0, stream, (const u16*)y, N, H, W, C, Ho, Wo, (u16*)out, idx, \
+                                scale, shift, N / G);
+  MAUV_DT_DISPATCH(dtype, "maxpool_bn_fwd_h16", L)
+#undef L
+  return check_launch("maxpool_bn_fwd_h16");
 }
 
 MAUV_API int mauv_maxpool_bwd_h16(int dtype, const void* dy, const unsigned char* idx, int N,

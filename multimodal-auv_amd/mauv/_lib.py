@@ -60,10 +60,12 @@ SIGNATURES = {
     # pool.hip
     "mauv_maxpool_fwd": [P, I, I, I, I, P, P, P],
     "mauv_maxpool_bwd": [P, P, I, I, I, I, P, P],
+    "mauv_maxpool_bn_fwd": [P, P, P, I, I, I, I, I, P, P, P],
     "mauv_avgpool_fwd": [P, I, I, I, P, P],
     "mauv_avgpool_bwd": [P, I, I, I, P, P],
     "mauv_maxpool_fwd_h16": [I, P, I, I, I, I, P, P, P],
     "mauv_maxpool_bwd_h16": [I, P, P, I, I, I, I, P, P],
+    "mauv_maxpool_bn_fwd_h16": [I, P, P, P, I, I, I, I, I, P, P, P],
     "mauv_avgpool_fwd_h16": [I, P, I, I, I, P, P],
     "mauv_avgpool_bwd_h16": [I, P, I, I, I, P, P],
     "mauv_pack_nchw_h16": [I, P, I, I, I, I, I, P, P],

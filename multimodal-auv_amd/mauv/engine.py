@@ -42,6 +42,9 @@ TRUNK_STREAMS = os.environ.get("MAUV_TRUNK_STREAMS", "1") == "1"
 # side stream.  Off by default: with the three trunks already concurrent it measured neutral
 # (226-229 vs 228-230 triplets/s fp32, tools/gpubatch_streams.sh).
 SIDE_WGRAD = os.environ.get("MAUV_SIDE_WGRAD", "0") == "1"
+# The stem's bn1 + ReLU applied on load inside the max-pool (the 112x112 BN output, the largest
+# activation of the trunk, is never written; its backward recomputes the ReLU mask from y).
+FUSED_STEM_POOL = os.environ.get("MAUV_FUSED_STEM_POOL", "1") == "1"
 _STREAMS = {}
 
 
@@ -415,15 +418,22 @@ class TrunkRunner(_Runner):
             ops.pack_nchw(x, B, Cin, H, W, cp, xh)
             x, xs = xh, (0, H * W * cp, W * cp, cp, 1)
         y, rc, part = self._conv(t.conv1, x, B, H, W, x_strides=xs)
-        a, rb = self._bn(t.bn1, y, part, relu=True)
-        del y, part
-        H, W = a.shape[2], a.shape[3]
+        H, W = y.shape[2], y.shape[3]
         Hp, Wp = ops.out_hw(H, 3, 2, 1), ops.out_hw(W, 3, 2, 1)
         p = torch.empty(G, B, Hp, Wp, 64, device=x.device, dtype=self.dt)
-        idx = torch.empty(G, B, Hp, Wp, 64, dtype=torch.uint8, device=x.device)
-        ops.maxpool_fwd(a, G * B, H, W, 64, p, idx)
+        idx = torch.empty(G, B, Hp, Wp, 64, dtype=torch.uint8, device=x.device) \
+            if self.save else None
+        if FUSED_STEM_POOL:   # bn1 + relu applied inside the max-pool's loads
+            _, rb = self._bn(t.bn1, y, part, relu=True, materialize=False)
+            scale, shift, _ = self.last_lazy
+            ops.maxpool_fwd(y, G * B, H, W, 64, p, idx, bn=(scale, shift, G))
+        else:
+            a, rb = self._bn(t.bn1, y, part, relu=True)
+            ops.maxpool_fwd(a, G * B, H, W, 64, p, idx)
+            del a
+        del y, part
         self.stem = (rc, rb, idx, (H, W)) if self.save else None
-        del a, idx
+        del idx
         cur, H, W = p, Hp, Wp
         for blk in t.blocks():
             y1, r1, p1 = self._conv(blk.conv1, cur, B, H, W)

@@ -300,7 +300,27 @@ def bn_bwd(y, out, dout, relu, mean, invstd, scale, G, M, C, ws, dy, dres=None, 
 
 
 # ----------------------------------------------------------------------- pooling
-def maxpool_fwd(x, N, H, W, C, y, idx):
+def maxpool_fwd(x, N, H, W, C, y, idx, bn=None):
+    """3x3/2 pad-1 max-pool of N NHWC images; idx None skips the argmax bytes (no backward).
+    bn = (scale, shift, G): x is the stem's conv output and relu(x*scale[g] + shift[g]) (its
+    pending BatchNorm + ReLU, per MC group) is applied on load, never materialised."""
+    Ho, Wo = out_hw(H, 3, 2, 1), out_hw(W, 3, 2, 1)
+    if x.numel() != N * H * W * C or y.numel() != N * Ho * Wo * C or \
+            (idx is not None and (idx.numel() != y.numel() or idx.dtype != torch.uint8)):
+        raise ValueError("maxpool_fwd: tensor sizes do not match (N, H, W, C)")
+    if bn is not None:
+        scale, shift, G = bn
+        if scale.numel() != G * C or shift.numel() != G * C or N % G:
+            raise ValueError("maxpool_fwd: bn scale/shift must be [G][C] with G | N")
+        if x.dtype in H16:
+            _h16(x.dtype, x, y)
+            check(lib.mauv_maxpool_bn_fwd_h16(H16[x.dtype], _p(x), _p(scale), _p(shift), G, N, H,
+                                              W, C, _p(y), _p(idx), stream()), "maxpool_bn_fwd_h16")
+            return
+        _f32(x, y)
+        check(lib.mauv_maxpool_bn_fwd(_p(x), _p(scale), _p(shift), G, N, H, W, C, _p(y), _p(idx),
+                                      stream()), "maxpool_bn_fwd")
+        return
     if x.dtype in H16:
         _h16(x.dtype, x, y)
         check(lib.mauv_maxpool_fwd_h16(H16[x.dtype], _p(x), N, H, W, C, _p(y), _p(idx), stream()),

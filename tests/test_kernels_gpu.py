@@ -481,3 +481,34 @@ def test_bn_apply_row_walk_ragged(C, M):
     ops.bn_apply(y, s, h, r, True, out, G, M, C)
     ref = torch.relu(y.double() * s.double()[:, None] + h.double()[:, None] + r.double())
     assert torch.allclose(out.double(), ref, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16],
+                         ids=["fp32", "bf16", "f16"])
+def test_maxpool_bn_fused_matches_materialised(dt):
+    """Stem bn1 + ReLU applied inside the max-pool == bn_apply then max-pool, bit for bit
+    (pooled values and argmax bytes), per MC group; idx=None skips the argmax."""
+    from mauv import ops
+    G, B, H, W, C = 2, 3, 17, 15, 64
+    N = G * B
+    torch.manual_seed(21)
+    y = (torch.randn(G, B, H, W, C, device=dev) * 2).to(dt)
+    s, h = torch.randn(G, C, device=dev), torch.randn(G, C, device=dev)
+    s[:, :8] = 0.0            # ties: whole windows of zeros after the ReLU
+    a = torch.empty_like(y)
+    ops.bn_apply(y, s, h, None, True, a, G, B * H * W, C)
+    Ho, Wo = ops.out_hw(H, 3, 2, 1), ops.out_hw(W, 3, 2, 1)
+    p_ref = torch.empty(G, B, Ho, Wo, C, device=dev, dtype=dt)
+    i_ref = torch.empty(G, B, Ho, Wo, C, device=dev, dtype=torch.uint8)
+    ops.maxpool_fwd(a, N, H, W, C, p_ref, i_ref)
+    p = torch.full_like(p_ref, float("nan"))
+    i = torch.full_like(i_ref, 255)
+    ops.maxpool_fwd(y, N, H, W, C, p, i, bn=(s, h, G))
+    assert torch.equal(p.view(torch.int16 if dt != torch.float32 else torch.int32),
+                       p_ref.view(torch.int16 if dt != torch.float32 else torch.int32))
+    assert torch.equal(i, i_ref)
+    p2 = torch.full_like(p_ref, float("nan"))
+    ops.maxpool_fwd(y, N, H, W, C, p2, None, bn=(s, h, G))
+    assert torch.equal(p2, p_ref)
+    ref = F.max_pool2d(a.float().reshape(N, H, W, C).permute(0, 3, 1, 2), 3, 2, 1)
+    assert torch.equal(p_ref.float().reshape(N, Ho, Wo, C).permute(0, 3, 1, 2), ref)
