@@ -227,6 +227,7 @@ int mauv_bn_bwd_h16(int dtype, const void* y, const void* out, const void* dout,
                     void* dres, float* dgamma, float* dbeta, hipStream_t stream);
 
 /* ---- pooling (pool.hip): torchvision stem maxpool 3x3/2 pad 1 and adaptive avgpool ------ */
+/* max-pool forward: C % 8 == 0 (the stem: 64); backward: C % 4 == 0. */
 int mauv_maxpool_fwd(const float* x, int N, int H, int W, int C, float* y, unsigned char* idx,
                      hipStream_t stream);
 int mauv_maxpool_bwd(const float* dy, const unsigned char* idx, int N, int H, int W, int C,

@@ -10,8 +10,9 @@ using namespace mauv;
 namespace mauv {
 
 // Tie-break as torch's max_pool2d: first maximum in (kh, kw) scan order; NaN wins.
-// One thread per 4 channels of one output pixel (C % 4 == 0; the stem has C = 64).
-template <class S>
+// One thread per 8 channels of one output pixel (C % 8 == 0, the stem has C = 64; one 16-B
+// load per tap for 16-bit storage); pixel decomposition in 32-bit when the output fits.
+template <class S, class I>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const typename S::T* __restrict__ x,
                                                           int N, int H, int W, int C, int Ho,
                                                           int Wo, typename S::T* __restrict__ y,
@@ -19,21 +20,23 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const typename S::T* _
                                                           const float* __restrict__ scale,
                                                           const float* __restrict__ shift,
                                                           int npg) {
-  const int C4 = C / 4;
-  const long long total = (long long)N * Ho * Wo * C4;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c = 4 * (int)(i % C4);
-    long long p = i / C4;
-    const int ow = (int)(p % Wo); p /= Wo;
-    const int oh = (int)(p % Ho);
-    const int n = (int)(p / Ho);
-    floatx4 best = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    int bi[4] = {0, 0, 0, 0};
-    floatx4 sc, sh;
+  const I C8 = (I)(C / 8);
+  const I total = (I)N * Ho * Wo * C8;
+  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
+    const int c = 8 * (int)(i % C8);
+    I p = i / C8;
+    const int ow = (int)(p % (I)Wo); p /= (I)Wo;
+    const int oh = (int)(p % (I)Ho);
+    const int n = (int)(p / (I)Ho);
+    floatx8 best;
+    int bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    floatx8 sc, sh;
     if (scale) {  // pending BN + ReLU of the stem, applied on load (group g = n / npg)
       const int gc = (n / npg) * C + c;
-      sc = *(const floatx4*)(scale + gc);
-      sh = *(const floatx4*)(shift + gc);
+      sc = ldf8(scale + gc);
+      sh = ldf8(shift + gc);
     }
     for (int r = 0; r < 3; ++r) {
       const int ih = oh * 2 - 1 + r;
@@ -41,26 +44,36 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const typename S::T* _
       for (int s = 0; s < 3; ++s) {
         const int iw = ow * 2 - 1 + s;
         if (iw < 0 || iw >= W) continue;
-        floatx4 v = S::ld4(x + (((long long)n * H + ih) * W + iw) * C + c);
+        floatx8 v = S::ld8(x + (((long long)n * H + ih) * W + iw) * C + c);
         if (scale) {
           // exactly what bn_apply would have stored: relu(y*scale + shift) in fp32, rounded to
           // the storage type — so maxima and tie-breaks match the materialised path
           v = v * sc + sh;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
-          alignas(16) typename S::T tmp[4];
-          S::st4(tmp, v);
-          v = S::ld4(tmp);
+          for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+          alignas(16) typename S::T tmp[8];
+          S::st8(tmp, v);
+          v = S::ld8(tmp);
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < 8; ++e)
           if (v[e] > best[e] || isnan(v[e])) { best[e] = v[e]; bi[e] = r * 3 + s; }
       }
     }
-    S::st4(y + 4 * i, best);
-    if (idx) *(uchar4*)(idx + 4 * i) = make_uchar4(bi[0], bi[1], bi[2], bi[3]);
+    S::st8(y + 8 * (long long)i, best);
+    if (idx) {
+      uint2 b;
+      b.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+      b.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+      *(uint2*)(idx + 8 * (long long)i) = b;
+    }
   }
 }
+
+template <class S>
+static void launch_maxpool_fwd(const typename S::T* x, int N, int H, int W, int C, int Ho, int Wo,
+                               typename S::T* y, unsigned char* idx, const float* scale,
+                               const float* shift, int npg, hipStream_t stream);
 
 template <class S>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const typename S::T* __restrict__ dy,
@@ -147,14 +160,26 @@ static int grid1(long long n) {
   return (int)(b < 1 ? 1 : b);
 }
 
+template <class S>
+static void launch_maxpool_fwd(const typename S::T* x, int N, int H, int W, int C, int Ho, int Wo,
+                               typename S::T* y, unsigned char* idx, const float* scale,
+                               const float* shift, int npg, hipStream_t stream) {
+  const long long total = (long long)N * Ho * Wo * (C / 8);
+  if (total + (long long)8192 * 256 < (1LL << 31))
+    hipLaunchKernelGGL((maxpool_fwd_kernel<S, int>), dim3(grid1(total)), dim3(256), 0, stream, x, N,
+                       H, W, C, Ho, Wo, y, idx, scale, shift, npg);
+  else
+    hipLaunchKernelGGL((maxpool_fwd_kernel<S, long long>), dim3(grid1(total)), dim3(256), 0, stream,
+                       x, N, H, W, C, Ho, Wo, y, idx, scale, shift, npg);
+}
+
 }  // namespace mauv
 
 MAUV_API int mauv_maxpool_fwd(const float* x, int N, int H, int W, int C, float* y,
                               unsigned char* idx, hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  if (C % 4) { set_error("maxpool_fwd: C % 4 != 0"); return kErrArg; }
-  hipLaunchKernelGGL(maxpool_fwd_kernel<SF32>, dim3(grid1((long long)N * Ho * Wo * C / 4)), dim3(256),
-                     0, stream, x, N, H, W, C, Ho, Wo, y, idx, nullptr, nullptr, 1);
+  if (C % 8) { set_error("maxpool_fwd: C % 8 != 0"); return kErrArg; }
+  launch_maxpool_fwd<SF32>(x, N, H, W, C, Ho, Wo, y, idx, nullptr, nullptr, 1, stream);
   return check_launch("maxpool_fwd");
 }
 
@@ -162,9 +187,8 @@ MAUV_API int mauv_maxpool_bn_fwd(const float* y, const float* scale, const float
                                  int N, int H, int W, int C, float* out, unsigned char* idx,
                                  hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  if (C % 4 || G <= 0 || N % G) { set_error("maxpool_bn_fwd: C % 4 != 0 or N % G != 0"); return kErrArg; }
-  hipLaunchKernelGGL(maxpool_fwd_kernel<SF32>, dim3(grid1((long long)N * Ho * Wo * C / 4)), dim3(256),
-                     0, stream, y, N, H, W, C, Ho, Wo, out, idx, scale, shift, N / G);
+  if (C % 8 || G <= 0 || N % G) { set_error("maxpool_bn_fwd: C % 8 != 0 or N % G != 0"); return kErrArg; }
+  launch_maxpool_fwd<SF32>(y, N, H, W, C, Ho, Wo, out, idx, scale, shift, N / G, stream);
   return check_launch("maxpool_bn_fwd");
 }
 
@@ -195,10 +219,9 @@ MAUV_API int mauv_avgpool_bwd(const float* dy, int N, int HW, int C, float* dx,
 MAUV_API int mauv_maxpool_fwd_h16(int dtype, const void* x, int N, int H, int W, int C, void* y,
                                   unsigned char* idx, hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  if (C % 4) { set_error("maxpool_fwd_h16: C % 4 != 0"); return kErrArg; }
-#define L(D) hipLaunchKernelGGL(maxpool_fwd_kernel<S16<D>>, dim3(grid1((long long)N * Ho * Wo * C / 4)), \
-                                dim3(256), 0, stream, (const u16*)x, N, H, W, C, Ho, Wo, (u16*)y, idx, \
-                                nullptr, nullptr, 1);
+  if (C % 8) { set_error("maxpool_fwd_h16: C % 8 != 0"); return kErrArg; }
+#define L(D) launch_maxpool_fwd<S16<D>>((const u16*)x, N, H, W, C, Ho, Wo, (u16*)y, idx, nullptr, \
+                                        nullptr, 1, stream);
   MAUV_DT_DISPATCH(dtype, "maxpool_fwd_h16", L)
 #undef L
   return check_launch("maxpool_fwd_h16");
@@ -208,10 +231,9 @@ MAUV_API int mauv_maxpool_bn_fwd_h16(int dtype, const void* y, const float* scal
                                      const float* shift, int G, int N, int H, int W, int C,
                                      void* out, unsigned char* idx, hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  if (C % 4 || G <= 0 || N % G) { set_error("maxpool_bn_fwd_h16: C % 4 != 0 or N % G != 0"); return kErrArg; }
-#define L(D) hipLaunchKernelGGL(maxpool_fwd_kernel<S16<D>>, dim3(grid1((long long)N * Ho * Wo * C / 4)), \
-                                dim3(256), 0, stream, (const u16*)y, N, H, W, C, Ho, Wo, (u16*)out, idx, \
-                                scale, shift, N / G);
+  if (C % 8 || G <= 0 || N % G) { set_error("maxpool_bn_fwd_h16: C % 8 != 0 or N % G != 0"); return kErrArg; }
+#define L(D) launch_maxpool_fwd<S16<D>>((const u16*)y, N, H, W, C, Ho, Wo, (u16*)out, idx, scale, \
+                                        shift, N / G, stream);
   MAUV_DT_DISPATCH(dtype, "maxpool_bn_fwd_h16", L)
 #undef L
   return check_launch("maxpool_bn_fwd_h16");

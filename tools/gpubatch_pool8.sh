@@ -1,0 +1,12 @@
+# max-pool forward at 8 channels per thread with 32-bit pixel decomposition: parity + bench + inference trace
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_kernels_gpu.py tests/test_kernels16_gpu.py tests/test_model_gpu.py tests/test_model16_gpu.py > gpurun_out/p8_tests.log 2>&1 || { tail -30 gpurun_out/p8_tests.log; exit 1; }
+tail -n 1 gpurun_out/p8_tests.log
+for i in 1 2; do
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --exact-steps 0 --no-roofline > gpurun_out/p8_b.log 2>&1 || exit 1
+python3 -c "import json;d=json.loads(open('gpurun_out/p8_b.log').read().strip().splitlines()[-1]);print(d['value'], d['bf16_train']['value'], d['inference']['value'])"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/p8_prof_inf -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-bf16 --exact-steps 0 --no-roofline > gpurun_out/p8_prof_inf.log 2>&1 || exit 1
+echo done
