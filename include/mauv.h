@@ -226,6 +226,20 @@ int mauv_bn_bwd_h16(int dtype, const void* y, const void* out, const void* dout,
                     const float* shift, int G, long long M, int C, float* workspace, void* dy,
                     void* dres, float* dgamma, float* dbeta, hipStream_t stream);
 
+/* Block-output BN apply (+ReLU, +residual as mauv_bn_apply) that also writes the ReLU mask
+ * bits of the stored output, mask[G][M][C/8] (bit e of byte j: out[8j+e] > 0), and the
+ * BN + ReLU backward that reads them instead of the output (dres = dz as in mauv_bn_bwd).
+ * dtype -1 = fp32, 0 = bf16, 1 = f16; C % 8 == 0, C <= 2048.  Same results as
+ * mauv_bn_apply / mauv_bn_bwd with `out`; replaces the same torchvision Bottleneck
+ * bn3 -> += identity -> relu (and its autograd) as they do. */
+int mauv_bn_apply_mask(int dtype, const void* y, const float* scale, const float* shift,
+                       const void* res, const float* res_scale, const float* res_shift, void* out,
+                       unsigned char* mask, int G, long long M, int C, hipStream_t stream);
+int mauv_bn_bwd_mask(int dtype, const void* y, const unsigned char* mask, const void* dout,
+                     const float* mean, const float* invstd, const float* scale, int G,
+                     long long M, int C, float* workspace, void* dy, void* dres, float* dgamma,
+                     float* dbeta, hipStream_t stream);
+
 /* ---- pooling (pool.hip): torchvision stem maxpool 3x3/2 pad 1 and adaptive avgpool ------ */
 /* max-pool forward: C % 8 == 0 (the stem: 64); backward: C % 4 == 0. */
 int mauv_maxpool_fwd(const float* x, int N, int H, int W, int C, float* y, unsigned char* idx,

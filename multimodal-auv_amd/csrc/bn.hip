@@ -329,7 +329,8 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const typename S::T* __res
                                                       const float* __restrict__ shift,
                                                       long long M, int C, int rpb, RowMap rm,
                                                       float* __restrict__ p1,
-                                                      float* __restrict__ p2) {
+                                                      float* __restrict__ p2,
+                                                      const unsigned char* __restrict__ mask) {
   // one 8-channel group per thread (C % 8 == 0, C <= 2048): tpr threads span a row, rp rows
   // are walked in parallel
   const int tpr = C / 8, rp = 256 / tpr;
@@ -344,12 +345,16 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const typename S::T* __res
   if (t_r < rp) {
     const floatx8 mu = ldf8(mean + gc), is = ldf8(invstd + gc);
     floatx8 sc, sh;
-    if (relu && !out) { sc = ldf8(scale + gc); sh = ldf8(shift + gc); }
+    if (relu && !out && !mask) { sc = ldf8(scale + gc); sh = ldf8(shift + gc); }
     for (long long r = r0 + t_r; r < r1; r += rp) {
       const long long o = go + r * C + c0;
       const floatx8 yv = S::ld8(y + o);
       floatx8 dz = S::ld8(dout + o);
-      if (relu) {
+      if (mask) {  // ReLU mask bits written by the forward's bn_apply (one byte per 8 channels)
+        const unsigned m = mask[(go + r * C + c0) >> 3];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dz[e] = (m >> e) & 1u ? dz[e] : 0.f;
+      } else if (relu) {
         const floatx8 pre = out ? S::ld8(out + o) : yv * sc + sh;
 #pragma unroll
         for (int e = 0; e < 8; ++e) dz[e] = pre[e] > 0.f ? dz[e] : 0.f;
@@ -469,7 +474,8 @@ __global__ __launch_bounds__(256) void bn_apply_rows(const typename S::T* __rest
                                                      const float* __restrict__ res_scale,
                                                      const float* __restrict__ res_shift,
                                                      int relu, typename S::T* __restrict__ out,
-                                                     long long M, int C, int rpb) {
+                                                     long long M, int C, int rpb,
+                                                     unsigned char* __restrict__ mask) {
   const int tpr = C / 8, rp = 256 / tpr;
   const int tid = threadIdx.x, t_c = tid % tpr, t_r = tid / tpr;
   if (t_r >= rp) return;
@@ -495,6 +501,15 @@ __global__ __launch_bounds__(256) void bn_apply_rows(const typename S::T* __rest
       for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
     }
     S::st8(out + o, v);
+    if (mask) {  // bit e = (stored out > 0): the value as rounded to the storage type
+      alignas(16) typename S::T tmp[8];
+      S::st8(tmp, v);
+      const floatx8 q = S::ld8(tmp);
+      unsigned m = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m |= (q[e] > 0.f ? 1u : 0u) << e;
+      mask[o >> 3] = (unsigned char)m;
+    }
   }
 }
 
@@ -511,7 +526,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rows(const typename S::T* __
                                                          const float* __restrict__ k2,
                                                          typename S::T* __restrict__ dy,
                                                          typename S::T* __restrict__ dres,
-                                                         long long M, int C, int rpb) {
+                                                         long long M, int C, int rpb,
+                                                         const unsigned char* __restrict__ mask) {
   const int tpr = C / 8, rp = 256 / tpr;
   const int tid = threadIdx.x, t_c = tid % tpr, t_r = tid / tpr;
   if (t_r >= rp) return;
@@ -522,14 +538,18 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rows(const typename S::T* __
   const floatx8 sc = ldf8(scale + gc), mu = ldf8(mean + gc), is = ldf8(invstd + gc);
   const floatx8 a1 = ldf8(k1 + gc), a2 = ldf8(k2 + gc);
   floatx8 sh = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (relu && !out) sh = ldf8(shift + gc);
+  if (relu && !out && !mask) sh = ldf8(shift + gc);
   const long long base = (long long)g * M * C + c0;
 #pragma unroll 2
   for (long long r = r0 + t_r; r < r1; r += rp) {
     const long long o = base + r * C;
     floatx8 dz = S::ld8(dout + o);
     const floatx8 yv = S::ld8(y + o);
-    if (relu) {
+    if (mask) {
+      const unsigned m = mask[o >> 3];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dz[e] = (m >> e) & 1u ? dz[e] : 0.f;
+    } else if (relu) {
       const floatx8 pre = out ? S::ld8(out + o) : yv * sc + sh;
 #pragma unroll
       for (int e = 0; e < 8; ++e) dz[e] = pre[e] > 0.f ? dz[e] : 0.f;
@@ -569,12 +589,12 @@ template <class S>
 static void launch_apply(const typename S::T* y, const float* scale, const float* shift,
                          const typename S::T* res, const float* res_scale, const float* res_shift,
                          int relu, typename S::T* out, int G, long long M, int C,
-                         hipStream_t stream) {
-  if (use_rows(C)) {
+                         hipStream_t stream, unsigned char* mask = nullptr) {
+  if (mask || use_rows(C)) {
     int nblk, rpb;
     rows_geometry(M, C, nblk, rpb);
     hipLaunchKernelGGL(bn_apply_rows<S>, dim3(nblk, G), dim3(256), 0, stream, y, scale, shift,
-                       res, res_scale, res_shift, relu, out, M, C, rpb);
+                       res, res_scale, res_shift, relu, out, M, C, rpb, mask);
   } else {
     hipLaunchKernelGGL(bn_apply_kernel<S>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, stream, y,
                        scale, shift, res, res_scale, res_shift, relu, out, M, C);
@@ -707,9 +727,10 @@ static int bn_bwd_impl(const typename S::T* y, const typename S::T* out,
                        const float* invstd, const float* scale, const float* shift, int G,
                        long long M, int C, float* workspace, typename S::T* dy,
                        typename S::T* dres, float* dgamma, float* dbeta, const float* pre_p1,
-                       const float* pre_p2, int pre_nblk, hipStream_t stream) {
+                       const float* pre_p2, int pre_nblk, hipStream_t stream,
+                       const unsigned char* mask = nullptr) {
   if (C % 8 != 0 || C > 2048) { set_error("bn_bwd: unsupported C (C % 8 != 0 or > 2048)"); return kErrArg; }
-  if (relu && !out && !shift) { set_error("bn_bwd: relu mask needs out or scale/shift"); return kErrArg; }
+  if (relu && !out && !shift && !mask) { set_error("bn_bwd: relu mask needs out or scale/shift"); return kErrArg; }
   int nblk, rpb;
   bwd_geometry(M, C, nblk, rpb);
   const RowMap rm = row_map(C);
@@ -722,18 +743,18 @@ static int bn_bwd_impl(const typename S::T* y, const typename S::T* out,
                        C, M, pre_p1, pre_p2, k1, k2);
   } else {
     hipLaunchKernelGGL(bn_bwd_partial<S>, dim3(nblk, G), dim3(256), 0, stream, y, out, dout,
-                       relu, mean, invstd, scale, shift, M, C, rpb, rm, p1, p2);
+                       relu, mean, invstd, scale, shift, M, C, rpb, rm, p1, p2, mask);
     hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, nblk, C,
                        M, p1, p2, k1, k2);
   }
   if (dgamma || dbeta)
     hipLaunchKernelGGL(bn_bwd_param_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C, M,
                        k1, k2, dgamma, dbeta);
-  if (use_rows(C)) {
+  if (mask || use_rows(C)) {
     int anblk, arpb;
     rows_geometry(M, C, anblk, arpb);
     hipLaunchKernelGGL(bn_bwd_apply_rows<S>, dim3(anblk, G), dim3(256), 0, stream, y, out, dout,
-                       relu, mean, invstd, scale, shift, k1, k2, dy, dres, M, C, arpb);
+                       relu, mean, invstd, scale, shift, k1, k2, dy, dres, M, C, arpb, mask);
   } else {
     hipLaunchKernelGGL(bn_bwd_apply<S>, dim3(ew_grid(M * C / 8), G), dim3(256), 0, stream, y, out,
                        dout, relu, mean, invstd, scale, shift, k1, k2, dy, dres, M, C);
@@ -777,5 +798,43 @@ MAUV_API int mauv_bn_bwd_h16(int dtype, const void* y, const void* out, const vo
                                         invstd, scale, shift, G, M, C, workspace, (u16*)dy,       \
                                         (u16*)dres, dgamma, dbeta, nullptr, nullptr, 0, stream);
   MAUV_DT_DISPATCH(dtype, "bn_bwd_h16", L)
+#undef L
+}
+
+// Block-output BN apply that also writes the ReLU mask bits of the stored output (training):
+// mask[G][M][C/8], bit e of byte j = out[8j + e] > 0.  The backward then reads 1 bit per
+// element instead of the 2-4 B output (mauv_bn_bwd_mask).  dtype -1 = fp32, 0 = bf16, 1 = f16.
+MAUV_API int mauv_bn_apply_mask(int dtype, const void* y, const float* scale, const float* shift,
+                                const void* res, const float* res_scale, const float* res_shift,
+                                void* out, unsigned char* mask, int G, long long M, int C,
+                                hipStream_t stream) {
+  if (C % 8 != 0 || C > 2048 || !mask) { set_error("bn_apply_mask: C % 8 != 0, C > 2048 or no mask"); return kErrArg; }
+  if (dtype < 0) {
+    launch_apply<SF32>((const float*)y, scale, shift, (const float*)res, res_scale, res_shift, 1,
+                       (float*)out, G, M, C, stream, mask);
+    return check_launch("bn_apply_mask");
+  }
+#define L(D) launch_apply<S16<D>>((const u16*)y, scale, shift, (const u16*)res, res_scale,  \
+                                  res_shift, 1, (u16*)out, G, M, C, stream, mask);
+  MAUV_DT_DISPATCH(dtype, "bn_apply_mask", L)
+#undef L
+  return check_launch("bn_apply_mask");
+}
+
+// BN + ReLU backward with the ReLU mask from mauv_bn_apply_mask (instead of the output).
+MAUV_API int mauv_bn_bwd_mask(int dtype, const void* y, const unsigned char* mask,
+                              const void* dout, const float* mean, const float* invstd,
+                              const float* scale, int G, long long M, int C, float* workspace,
+                              void* dy, void* dres, float* dgamma, float* dbeta,
+                              hipStream_t stream) {
+  if (!mask) { set_error("bn_bwd_mask: no mask"); return kErrArg; }
+  if (dtype < 0)
+    return bn_bwd_impl<SF32>((const float*)y, nullptr, (const float*)dout, 1, mean, invstd, scale,
+                             nullptr, G, M, C, workspace, (float*)dy, (float*)dres, dgamma, dbeta,
+                             nullptr, nullptr, 0, stream, mask);
+#define L(D) return bn_bwd_impl<S16<D>>((const u16*)y, nullptr, (const u16*)dout, 1, mean, invstd,  \
+                                        scale, nullptr, G, M, C, workspace, (u16*)dy, (u16*)dres, \
+                                        dgamma, dbeta, nullptr, nullptr, 0, stream, mask);
+  MAUV_DT_DISPATCH(dtype, "bn_bwd_mask", L)
 #undef L
 }

@@ -61,6 +61,8 @@ SIGNATURES = {
     "mauv_maxpool_fwd": [P, I, I, I, I, P, P, P],
     "mauv_maxpool_bwd": [P, P, I, I, I, I, P, P],
     "mauv_maxpool_bn_fwd": [P, P, P, I, I, I, I, I, P, P, P],
+    "mauv_bn_apply_mask": [I, P, P, P, P, P, P, P, P, I, LL, I, P],
+    "mauv_bn_bwd_mask": [I, P, P, P, P, P, P, I, LL, I, P, P, P, P, P, P],
     "mauv_avgpool_fwd": [P, I, I, I, P, P],
     "mauv_avgpool_bwd": [P, I, I, I, P, P],
     "mauv_maxpool_fwd_h16": [I, P, I, I, I, I, P, P, P],

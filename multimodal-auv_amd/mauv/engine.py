@@ -45,6 +45,10 @@ SIDE_WGRAD = os.environ.get("MAUV_SIDE_WGRAD", "0") == "1"
 # The stem's bn1 + ReLU applied on load inside the max-pool (the 112x112 BN output, the largest
 # activation of the trunk, is never written; its backward recomputes the ReLU mask from y).
 FUSED_STEM_POOL = os.environ.get("MAUV_FUSED_STEM_POOL", "1") == "1"
+# Training block outputs (bn3 + residual + ReLU) also write 1-bit ReLU masks, and their
+# backward reads those instead of the 2-4 B stored output (MAUV_BN_RELU_MASK=0: read the output).
+# Not with the dgrad BN epilogue, which takes its mask from the output.
+BN_RELU_MASK = os.environ.get("MAUV_BN_RELU_MASK", "1") == "1" and not DGRAD_BN_EPILOGUE
 _STREAMS = {}
 
 
@@ -241,11 +245,11 @@ class _Runner:
 # ----------------------------------------------------------------------------- trunk
 class _BN:
     """Saved state of one BatchNorm (+ReLU) for the backward."""
-    __slots__ = ("bn", "y", "out", "stats", "relu", "M", "C", "batch_stats")
+    __slots__ = ("bn", "y", "out", "stats", "relu", "M", "C", "batch_stats", "mask")
 
-    def __init__(self, bn, y, out, stats, relu, M, C, batch_stats):
+    def __init__(self, bn, y, out, stats, relu, M, C, batch_stats, mask=None):
         self.bn, self.y, self.out, self.stats, self.relu = bn, y, out, stats, relu
-        self.M, self.C, self.batch_stats = M, C, batch_stats
+        self.M, self.C, self.batch_stats, self.mask = M, C, batch_stats, mask
 
     @property
     def scale(self):
@@ -375,12 +379,16 @@ class TrunkRunner(_Runner):
         else:
             ops.bn_eval_params(G, C, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                bn.eps, scale, shift)
-        out = None
+        out = mask = None
         if materialize:
             out = torch.empty_like(y)
-            ops.bn_apply(y, scale, shift, res, relu, out, G, M, C, res_bn=res_bn)
-        rec = _BN(bn, y, out if relu else None, stats, relu, M, C, batch_stats) \
-            if self.save else None
+            if BN_RELU_MASK and relu and self.save and C <= 2048:
+                mask = torch.empty(G * M * C // 8, dtype=torch.uint8, device=y.device)
+                ops.bn_apply_mask(y, scale, shift, res, out, mask, G, M, C, res_bn=res_bn)
+            else:
+                ops.bn_apply(y, scale, shift, res, relu, out, G, M, C, res_bn=res_bn)
+        rec = _BN(bn, y, out if relu and mask is None else None, stats, relu, M, C, batch_stats,
+                  mask) if self.save else None
         self.last_lazy = (scale, shift, int(relu))  # for a consumer applying it on load
         return out, rec
 
@@ -395,8 +403,12 @@ class TrunkRunner(_Runner):
         dg = bn.weight.grad if bn.weight.requires_grad else None
         db = bn.bias.grad if bn.bias.requires_grad else None
         s = rec.stats
-        ops.bn_bwd(rec.y, rec.out, dout, rec.relu, s[0], s[1], s[2], G, M, C, ws, dy, dres, dg,
-                   db, shift=s[3], pre=pre)
+        if rec.mask is not None:
+            assert pre is None
+            ops.bn_bwd_mask(rec.y, rec.mask, dout, s[0], s[1], s[2], G, M, C, ws, dy, dres, dg, db)
+        else:
+            ops.bn_bwd(rec.y, rec.out, dout, rec.relu, s[0], s[1], s[2], G, M, C, ws, dy, dres,
+                       dg, db, shift=s[3], pre=pre)
         return dy, dres
 
     # ---- schedule ----

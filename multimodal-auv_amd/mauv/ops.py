@@ -299,6 +299,39 @@ def bn_bwd(y, out, dout, relu, mean, invstd, scale, G, M, C, ws, dy, dres=None, 
                           _p(p1), _p(p2), nb, stream()), "bn_bwd")
 
 
+def _dt_code(t):
+    return -1 if t.dtype == torch.float32 else H16[t.dtype]
+
+
+def bn_apply_mask(y, scale, shift, res, out, mask, G, M, C, res_bn=None):
+    """bn_apply with relu, also writing the ReLU mask bits of out: mask uint8 [G*M*C/8]."""
+    rs, rh = res_bn if res_bn is not None else (None, None)
+    if mask.dtype != torch.uint8 or mask.numel() * 8 != G * M * C or out.numel() != G * M * C \
+            or y.numel() != G * M * C or (res is not None and res.numel() != G * M * C):
+        raise ValueError("bn_apply_mask: sizes do not match (G, M, C)")
+    if y.dtype in H16:
+        _h16(y.dtype, y, res, out)
+    else:
+        _f32(y, res, out)
+    check(lib.mauv_bn_apply_mask(_dt_code(y), _p(y), _p(scale), _p(shift), _p(res), _p(rs),
+                                 _p(rh), _p(out), _p(mask), G, M, C, stream()), "bn_apply_mask")
+
+
+def bn_bwd_mask(y, mask, dout, mean, invstd, scale, G, M, C, ws, dy, dres=None, dgamma=None,
+                dbeta=None):
+    """BN + ReLU backward with the mask bits of bn_apply_mask in place of the output."""
+    if mask.dtype != torch.uint8 or mask.numel() * 8 != G * M * C or dout.numel() != G * M * C:
+        raise ValueError("bn_bwd_mask: sizes do not match (G, M, C)")
+    if y.dtype in H16:
+        _h16(y.dtype, y, dout, dy, dres)
+    else:
+        _f32(y, dout, dy, dres)
+    _f32(mean, invstd, scale, ws, dgamma, dbeta)
+    check(lib.mauv_bn_bwd_mask(_dt_code(y), _p(y), _p(mask), _p(dout), _p(mean), _p(invstd),
+                               _p(scale), G, M, C, _p(ws), _p(dy), _p(dres), _p(dgamma),
+                               _p(dbeta), stream()), "bn_bwd_mask")
+
+
 # ----------------------------------------------------------------------- pooling
 def maxpool_fwd(x, N, H, W, C, y, idx, bn=None):
     """3x3/2 pad-1 max-pool of N NHWC images; idx None skips the argmax bytes (no backward).

@@ -512,3 +512,41 @@ def test_maxpool_bn_fused_matches_materialised(dt):
     assert torch.equal(p2, p_ref)
     ref = F.max_pool2d(a.float().reshape(N, H, W, C).permute(0, 3, 1, 2), 3, 2, 1)
     assert torch.equal(p_ref.float().reshape(N, Ho, Wo, C).permute(0, 3, 1, 2), ref)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+@pytest.mark.parametrize("C,M,res_bn", [(256, 300, False), (2048, 37, True), (24, 1000, False)])
+def test_bn_relu_mask_path_matches_output_path(dt, C, M, res_bn):
+    """bn_apply_mask / bn_bwd_mask (1-bit ReLU masks) == bn_apply / bn_bwd reading the stored
+    output, bit for bit: out, dy, dres, dgamma, dbeta."""
+    from mauv import ops
+    G = 3
+    torch.manual_seed(23)
+    y = (torch.randn(G, M, C, device=dev) * 2).to(dt)
+    r = torch.randn(G, M, C, device=dev).to(dt)
+    s, h = torch.randn(G, C, device=dev), torch.randn(G, C, device=dev)
+    s[:, :8] = 0.0          # outputs exactly 0 -> masked
+    rb = (torch.randn(G, C, device=dev), torch.randn(G, C, device=dev)) if res_bn else None
+    out_ref = torch.empty_like(y)
+    ops.bn_apply(y, s, h, r, True, out_ref, G, M, C, res_bn=rb)
+    out = torch.full_like(y, float("nan"))
+    mask = torch.empty(G * M * C // 8, dtype=torch.uint8, device=dev)
+    ops.bn_apply_mask(y, s, h, r, out, mask, G, M, C, res_bn=rb)
+    assert torch.equal(out, out_ref)
+    bits = ((mask.view(-1, 1).int() >> torch.arange(8, device=dev)) & 1).view(G, M, C)
+    assert torch.equal(bits.bool(), out_ref.float() > 0)
+    mean, invstd = torch.randn(G, C, device=dev), torch.rand(G, C, device=dev) + 0.5
+    dout = torch.randn(G, M, C, device=dev).to(dt)
+    res = []
+    for use_mask in (False, True):
+        ws = torch.empty(ops.bn_workspace_floats(G, M, C), device=dev)
+        dy, dres = torch.empty_like(y), torch.empty_like(y)
+        dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        if use_mask:
+            ops.bn_bwd_mask(y, mask, dout, mean, invstd, s, G, M, C, ws, dy, dres, dg, db)
+        else:
+            ops.bn_bwd(y, out_ref, dout, True, mean, invstd, s, G, M, C, ws, dy, dres, dg, db,
+                       shift=h)
+        res.append((dy, dres, dg, db))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
