@@ -455,9 +455,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const typename S::T* __restr
 }
 
 // bn_bwd_partial geometry: C/8 threads span a row, so a 256-thread block walks 256/(C/8)
-// rows at once; at most 16 rows per thread keeps G*nblk in the hundreds-to-thousands for the
-// deep, narrow-M layers (layer4: M = B*49 rows of 2048 channels) that one-block-per-256-rows
-// left at ~13 blocks per group, at the cost of <= 1/16 extra partial traffic per element.
+// rows at once; at most 32 rows per thread keeps G*nblk in the hundreds for the deep,
+// narrow-M layers (layer4: M = B*49 rows of 2048 channels) that one-block-per-256-rows left at
+// ~13 blocks per group, at the cost of <= 1/32 extra partial traffic per element (32 vs 16 vs
+// 8 rows per thread with the ReLU masks: 234.5-235.5 vs 231.8-232.5 vs 230.9-232.0 fp32
+// triplets/s, 574-575 vs 562-565 vs 554 bf16 on one box, tools/gpubatch_rpt2.sh).
 static int ew_grid(long long n4);
 
 // Row-walk forms of the two elementwise passes (the default): C/8 threads span a row, 256/(C/8)
@@ -602,7 +604,7 @@ static void launch_apply(const typename S::T* y, const float* scale, const float
 }
 
 static void bwd_geometry(long long M, int C, int& nblk, int& rpb) {
-  static const int rpt = env_int("MAUV_BN_PARTIAL_RPT", 16);
+  static const int rpt = env_int("MAUV_BN_PARTIAL_RPT", 32);
   const int rp = 256 / (C / 8);
   long long r = (long long)rp * rpt;
   long long n = (M + r - 1) / r;
