@@ -43,6 +43,17 @@ class DistributedMC(nn.Module):
     def mc_forward(self, *args, **kw):
         return self.module.mc_forward(*args, **kw)
 
+    def all_ranks(self, flag):
+        """Logical AND of a per-rank decision over the group (one tiny all-reduce): the
+        training loop skips a batch on every rank or on none, so the gradient all-reduces of
+        later steps stay paired (the reference's DataParallel has one global loss)."""
+        if self.world == 1:
+            return bool(flag)
+        dev = next(self.module.parameters()).device
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(t.item())
+
     def allreduce_grads(self):
         """Average the flat gradient arena across ranks (bucketed RCCL all-reduce)."""
         st = root_state(self.module)

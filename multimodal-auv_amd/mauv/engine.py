@@ -190,8 +190,16 @@ class _Runner:
         self.st, self.G, self.s0, self.save = state, G, sample0, save
 
     def _eps(self, m, name):
+        """Explicit epsilons from a test provider (None: Philox).  Asked once per layer and
+        runner: the backward reuses the forward's draw, as Philox regenerates the same one."""
         fn = self.st.eps_provider
-        return None if fn is None else fn(m, name, self.G)
+        if fn is None:
+            return None
+        cache = self.__dict__.setdefault("_eps_cache", {})
+        key = (id(m), name)
+        if key not in cache:
+            cache[key] = fn(m, name, self.G)
+        return cache[key]
 
     # ---- Bayesian parameter sampling (mauv_reparam_sample) ----
     def _sample(self, m, mu, rho, name, out, Cout, Cin, RS, bias=False, out_gstride=0,

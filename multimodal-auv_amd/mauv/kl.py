@@ -91,6 +91,10 @@ class _KL(torch.autograd.Function):
 
 def kl_of_modules(modules, root=None):
     modules = [m for m in modules if is_bayesian(m)]
+    dev = _entries(modules[:1])[0][0].device
+    if dev.type != "cuda":
+        raise RuntimeError("mauv get_kl_loss: the Bayesian layers live on the host; the KL "
+                           "reduction runs in libmauv_hip on a ROCm device (model.to('cuda'))")
     owner_mod = root if root is not None else modules[0]
     key = "_mauv_kltab"
     tab = owner_mod.__dict__.get(key)

@@ -38,6 +38,15 @@ def _f32(*ts):
                 (t.device, t.dtype, t.is_contiguous(), t.shape)
 
 
+def _dev(dt, *ts):
+    """Every tensor handed to a kernel is a contiguous device tensor of dtype ``dt``: a host
+    pointer reaching a HIP kernel is a memory-access fault the caller cannot catch."""
+    for t in ts:
+        if t is not None and not (t.is_cuda and t.dtype == dt and t.is_contiguous()):
+            raise ValueError(f"mauv kernel operand must be a contiguous {dt} ROCm tensor, got "
+                             f"{t.dtype} on {t.device} (contiguous={t.is_contiguous()})")
+
+
 def out_hw(H, R, stride, pad):
     return (H + 2 * pad - R) // stride + 1
 
@@ -404,46 +413,62 @@ def pack_nchw(x, B, C, H, W, Cp, y):
 
 # ----------------------------------------------------------------------- head
 def attn_t(qkv, rows, t):
+    _dev(torch.float32, qkv, t)
     check(lib.mauv_attn_t(_p(qkv), rows, _p(t), stream()), "attn_t")
 
 
 def attn_t_bwd(dt, t, rows, dqkv):
+    _dev(torch.float32, dt, t, dqkv)
     check(lib.mauv_attn_t_bwd(_p(dt), _p(t), rows, _p(dqkv), stream()), "attn_t_bwd")
 
 
 def attn_out(qkv, s, rows, comb, ld, off):
+    _dev(torch.float32, qkv, s, comb)
     check(lib.mauv_attn_out(_p(qkv), _p(s), rows, _p(comb), ld, off, stream()), "attn_out")
 
 
 def attn_out_bwd(dcomb, ld, off, qkv, s, rows, dqkv, ds):
+    _dev(torch.float32, dcomb, qkv, s, dqkv, ds)
     check(lib.mauv_attn_out_bwd(_p(dcomb), ld, off, _p(qkv), _p(s), rows, _p(dqkv), _p(ds),
                                 stream()), "attn_out_bwd")
 
 
 def colsum(dy, G, rows, N, out, accumulate=False):
+    _dev(torch.float32, dy, out)
     check(lib.mauv_colsum(_p(dy), G, rows, N, _p(out), int(accumulate), stream()), "colsum")
 
 
 def mc_mean_ce(logits, labels, G, B, C, mean, loss, pred=None):
+    _dev(torch.float32, logits, mean, loss)
+    _dev(torch.int64, labels, pred)
     check(lib.mauv_mc_mean_ce(_p(logits), _p(labels), G, B, C, _p(mean), _p(loss), _p(pred),
                               stream()), "mc_mean_ce")
 
 
 def mc_mean_bwd(dmean, gloss, mean, labels, G, B, C, dlogits):
+    _dev(torch.float32, dmean, gloss, mean, dlogits)
+    _dev(torch.int64, labels)
     check(lib.mauv_mc_mean_bwd(_p(dmean), _p(gloss), _p(mean), _p(labels), G, B, C,
                                _p(dlogits), stream()), "mc_mean_bwd")
 
 
 def mc_stats(logits, G, B, C, eps_h, sums, accumulate=False):
+    _dev(torch.float32, logits)
+    _dev(torch.float64, sums)
     check(lib.mauv_mc_stats(_p(logits), G, B, C, eps_h, _p(sums), int(accumulate), stream()),
           "mc_stats")
 
 
 def mc_finalize(sums, N, B, C, eps_pred, mean_prob=None, var_unc=None, alea=None,
                 pred_entropy=None, pred=None):
+    _dev(torch.float64, sums)
+    _dev(torch.float32, mean_prob, var_unc, alea, pred_entropy)
+    _dev(torch.int64, pred)
     check(lib.mauv_mc_finalize(_p(sums), N, B, C, eps_pred, _p(mean_prob), _p(var_unc),
                                _p(alea), _p(pred_entropy), _p(pred), stream()), "mc_finalize")
 
 
 def nonfinite_count(t, out):
+    _dev(torch.float32, t)
+    _dev(torch.int32, out)
     check(lib.mauv_nonfinite_count(_p(t), t.numel(), _p(out), stream()), "nonfinite_count")

@@ -8,28 +8,56 @@ batched launches (``mc_forward``, chunked to fit HBM) and the statistics are one
 reduction (mauv_mc_stats / mauv_mc_finalize) whose partial sums all-reduce across ranks for
 MC-sharded multi-GPU inference.
 
-Numerics: the reference autocasts to fp16 on CUDA (predictors.py:55); mauv runs the model's
-compute dtype (fp32 by default) and always reduces in fp32/fp64.
+Numerics: like the reference (predictors.py:55) the MC passes run under
+``torch.amp.autocast(device_type='cuda')``, which the engine follows with f16 trunks
+(activations and sampled weights 16-bit, fp32 accumulation and BN statistics); the fusion head
+and every reduction stay fp32/fp64.
 """
 import csv
 import logging
+import math
 
 import torch
 import torch.distributed as dist
 
 from . import mchead
+from .engine import root_state
 from .kl import unwrap
 
+# peak live activation channels per image of one MC sample, in units of the layer-1 grid
+# (H/4 x W/4): a layer-1 bottleneck without saving holds its input (256), y1 and y2 (64 each),
+# y3, the downsample residual and the output (256 each) -> 1152; the stem's conv output
+# (64 ch at H/2 x W/2) is 256 of them.  The trunks run one after another in inference.
+_PEAK_CH_L1 = 1152
+_ALLOC_SLACK = 1.25   # caching-allocator rounding and the BN / statistics buffers
 
-def mc_chunk(model, batch_size, num_mc, budget_bytes=None):
-    """How many MC samples to batch per launch for inference (activation memory bound)."""
+
+def mc_chunk(model, batch_size, num_mc, budget_bytes=None, hw=None, dtype=None, device=None):
+    """How many MC samples to batch per launch for inference, from the activation footprint
+    of the largest trunk input (``hw`` = [(H, W), ...] of the three images), the trunk storage
+    dtype and the device memory actually available; chunks are balanced (100 samples at a
+    limit of 22 -> five chunks of 20)."""
     core = unwrap(model)
     if budget_bytes is None:
         budget_bytes = getattr(core, "mc_infer_budget_bytes", 64 << 30)
-    # peak live activations ≈ 4 x the largest NHWC tensor (stem out, 64 x H/2 x W/2) per
-    # trunk image, fp32; sonar tiles are 256 px in the reference
-    per_sample = 4 * 4 * 64 * 128 * 128 * batch_size
-    return max(1, min(num_mc, int(budget_bytes // max(per_sample, 1))))
+        dev = device if device is not None else _param_device(core)
+        if dev is not None and dev.type == "cuda":
+            free, _ = torch.cuda.mem_get_info(dev)
+            cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+            budget_bytes = min(budget_bytes, int(0.5 * (free + cached)))
+    esize = torch.tensor([], dtype=dtype or torch.float32).element_size()
+    hw = hw or [(256, 256)]
+    grid = max(math.ceil(h / 4) * math.ceil(w / 4) for h, w in hw)
+    per_sample = esize * _PEAK_CH_L1 * grid * batch_size * _ALLOC_SLACK
+    limit = max(1, min(num_mc, int(budget_bytes // max(per_sample, 1))))
+    n_chunks = math.ceil(num_mc / limit) if num_mc > 0 else 1
+    return max(1, math.ceil(num_mc / n_chunks))
+
+
+def _param_device(core):
+    for p in core.parameters():
+        return p.device
+    return None
 
 
 def local_mc_count(num_mc, rank, world):
@@ -46,8 +74,11 @@ def mc_statistics(model, inputs, bathy, sss, num_mc, eps_h=1e-7, eps_pred=1e-8, 
     rank, world = (dist.get_rank(group), dist.get_world_size(group)) if group is not None \
         else (0, 1)
     local = local_mc_count(num_mc, rank, world)
-    chunk = chunk or mc_chunk(model, B, max(local, 1))
     core = model if hasattr(model, "mc_forward") else unwrap(model)
+    if chunk is None:
+        dt = root_state(unwrap(model)).trunk_dtype()
+        chunk = mc_chunk(model, B, max(local, 1), dtype=dt, device=inputs.device,
+                         hw=[t.shape[-2:] for t in (inputs, bathy, sss)])
     sums = None
     done = 0
     while done < local:
@@ -64,10 +95,23 @@ def mc_statistics(model, inputs, bathy, sss, num_mc, eps_h=1e-7, eps_pred=1e-8, 
     return mchead.mc_finalize(sums, num_mc, C, eps_pred)
 
 
+def _shard_group(model):
+    """MC samples shard across ranks when the model is wrapped in mauv.ddp.DistributedMC (each
+    rank then passes the same batches); a bare model predicts alone."""
+    if getattr(model, "_mauv_wrapper", False) and dist.is_available() and dist.is_initialized() \
+            and getattr(model, "world", 1) > 1:
+        return model.group if model.group is not None else dist.group.WORLD
+    return None
+
+
 def multimodal_predict_and_save(multimodal_model, dataloader, device, csv_path,
                                 num_mc_samples=10, sss_patch_type="", channel_patch_type="",
                                 model_type="multimodal"):
-    """inference/predictors.py:9-97 (model kept in .train(): BN uses batch statistics)."""
+    """inference/predictors.py:9-97 (model kept in .train(): BN uses batch statistics; MC
+    passes under torch.amp.autocast as predictors.py:55 -> f16 trunks on a ROCm device)."""
+    device = torch.device(device)
+    amp_device = "cuda" if device.type == "cuda" else "cpu"
+    group = _shard_group(multimodal_model)
     multimodal_model.train()
     logging.info(f"CSV will be saved to: {csv_path}")
     with open(csv_path, mode="w", newline="") as fh:
@@ -80,11 +124,16 @@ def multimodal_predict_and_save(multimodal_model, dataloader, device, csv_path,
                 bathy = bathy.to(device, non_blocking=True)
                 sss = sss.to(device, non_blocking=True)
                 if hasattr(unwrap(multimodal_model), "mc_forward"):
-                    st = mc_statistics(multimodal_model, inputs, bathy, sss, num_mc_samples)
+                    with torch.amp.autocast(device_type=amp_device):
+                        st = mc_statistics(multimodal_model, inputs, bathy, sss,
+                                           num_mc_samples, group=group)
                     pred, var, alea = st["pred"], st["var"], st["aleatoric"]
                 else:  # foreign model: reference sequential loop
-                    P = torch.stack([torch.softmax(multimodal_model(inputs, bathy, sss), 1)
-                                     for _ in range(num_mc_samples)])
+                    probs = []
+                    for _ in range(num_mc_samples):
+                        with torch.amp.autocast(device_type=amp_device):
+                            probs.append(torch.softmax(multimodal_model(inputs, bathy, sss), 1))
+                    P = torch.stack(probs).float()
                     var = torch.var(P, dim=0).mean(dim=1)
                     alea = torch.mean(-torch.sum(P * torch.log(P + 1e-7), dim=-1), dim=0)
                     pred = torch.argmax(P.mean(0), dim=1)

@@ -11,8 +11,9 @@ Signatures, return values, CSV rows, KL weighting and skip rules follow
   (multimodal.py:141) is one fused scan over the flat gradient arena + one host sync instead
   of ~700 per-tensor syncs.
 
-Models without ``mc_forward`` (e.g. the reference tests' dummy modules) run the reference's
-sequential loop unchanged.
+Models without ``mc_forward`` (e.g. the reference tests' dummy modules, which run on
+``device='cpu'``) run the reference's sequential loop and its torch maths unchanged; the fused
+kernels are used only on ROCm tensors (a host pointer must never reach a HIP kernel).
 """
 import csv
 import logging
@@ -55,7 +56,39 @@ def _grads_finite(model):
             for p, v in zip(st.arena.params, st.arena.views)):
         return mchead.all_finite(st.arena.flat)
     grads = [p.grad for p in model.parameters() if p.grad is not None]
-    return True if not grads else mchead.all_finite(grads)
+    if not grads:
+        return True
+    if all(g.is_cuda for g in grads):
+        return mchead.all_finite(grads)
+    # foreign model on the host: the reference's per-tensor scan (multimodal.py:141)
+    return not any(torch.isnan(g).any() or torch.isinf(g).any() for g in grads)
+
+
+def _all_ranks(model, flag):
+    """A DistributedMC model agrees on a per-rank decision (logical AND over ranks), so that
+    every rank skips the same batches and the gradient all-reduces stay paired."""
+    return model.all_ranks(flag) if hasattr(model, "all_ranks") else flag
+
+
+def mc_eval_stats(logits, labels, eps_pred, eps_h):
+    """CE of the MC-mean logits, argmax, and the MC uncertainty statistics of one eval batch
+    (multimodal.py:287-310 / unimodal.py:285-300): fused kernels for ROCm logits, the
+    reference's torch maths for a foreign model's host logits."""
+    N, _, C = logits.shape
+    if logits.is_cuda:
+        ce, _, predicted = mchead.mc_mean_ce(logits, labels)
+        st = mchead.mc_finalize(mchead.mc_stats(logits, eps_h), N, C, eps_pred)
+        return ce, predicted, st
+    out_mean = logits.mean(0)
+    ce = torch.nn.functional.cross_entropy(out_mean, labels)
+    predicted = torch.max(out_mean, 1)[1]
+    P = torch.softmax(logits.float(), dim=2)
+    mean_p = P.mean(0)
+    st = dict(mean_prob=mean_p,
+              predictive_entropy=-torch.sum(mean_p * torch.log(mean_p + eps_pred), dim=1),
+              aleatoric=torch.mean(-torch.sum(P * torch.log(P + eps_h), dim=2), dim=0),
+              var=torch.var(P, dim=0).mean(dim=1), pred=torch.argmax(mean_p, dim=1))
+    return ce, predicted, st
 
 
 def mc_loss(model, inputs_tuple, labels, criterion, num_mc, batch_size, kl_w):
@@ -77,13 +110,13 @@ def mc_train_step(model, inputs_tuple, labels, criterion, optimizer, num_mc, bat
     skip, backward, NaN/Inf gradient guard, optimizer step + zero_grad."""
     loss, output, predicted, ce, scaled_kl = mc_loss(model, inputs_tuple, labels, criterion,
                                                      num_mc, batch_size, kl_w)
-    if not torch.isfinite(loss).item():
+    if not _all_ranks(model, bool(torch.isfinite(loss).item())):
         logging.warning(f"Skipping batch due to NaN/Inf loss: {loss}")
         return None
     loss.backward()
     if hasattr(model, "allreduce_grads"):  # mauv.ddp.DistributedMC: one RCCL all-reduce
         model.allreduce_grads()
-    stepped = _grads_finite(model)
+    stepped = _grads_finite(model)   # identical on every rank after the all-reduce
     if stepped:
         optimizer.step()
         optimizer.zero_grad()
@@ -208,12 +241,10 @@ def evaluate_multimodal_model(multimodal_model, dataloader, device, epoch, total
                     logits = mc_logits(multimodal_model, num_mc, inputs, bathy, sss)
                     kl = get_kl_loss(multimodal_model)
                     kl_scaled = kl / len(dataloader) * kl_w
-                    ce, _, predicted = mchead.mc_mean_ce(logits, labels)
+                    ce, predicted, st = mc_eval_stats(logits, labels, 1e-8, 1e-8)
                     total_loss += (ce + kl_scaled).item()
                     correct += int((predicted == labels).sum().item())
                     total += labels.size(0)
-                    st = mchead.mc_finalize(mchead.mc_stats(logits, 1e-8), num_mc,
-                                            logits.shape[2], 1e-8)
                     pu = st["predictive_entropy"]
                     all_pu.extend(pu.cpu().numpy())
                     all_mu.extend((pu - st["aleatoric"]).cpu().numpy())
@@ -309,12 +340,10 @@ def evaluate_unimodal_model(model, dataloader, device, epoch, csv_path, total_nu
                     labels = batch["label"].long().to(device, non_blocking=True)
                     logits = mc_logits(model, num_mc, x)
                     kl = get_kl_loss(model)
-                    ce, _, predicted = mchead.mc_mean_ce(logits, labels)
+                    ce, predicted, st = mc_eval_stats(logits, labels, 1e-7, 1e-7)
                     total_loss += (ce + kl_w * (kl / dataloader.batch_size)).item()
                     correct += int((predicted == labels).sum().item())
                     total += labels.size(0)
-                    st = mchead.mc_finalize(mchead.mc_stats(logits, 1e-7), num_mc,
-                                            logits.shape[2], 1e-7)
                     all_ep.extend(st["var"].cpu().numpy())
                     all_al.extend(st["aleatoric"].cpu().numpy())
                     all_pred.extend(predicted.cpu().numpy())

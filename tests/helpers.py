@@ -88,3 +88,68 @@ def max_rel(a, b):
     a = a.detach().double().cpu()
     b = b.detach().double().cpu()
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def forward_order(oracle_model, *inputs):
+    """[(module name, eps name, shape)] in the order one oracle forward draws its epsilons —
+    the order the reference's bayesian-torch layers consume torch's generator."""
+    names = {id(mod): n for n, mod in oracle_model.named_modules()}
+    order = []
+
+    def src(layer, name, shape):
+        order.append((names[id(layer)], name, shape))
+        return torch.zeros(shape)
+    bayes_ref.set_eps_source(src)
+    try:
+        with torch.no_grad():
+            oracle_model(*inputs)
+    finally:
+        bayes_ref.set_eps_source(None)
+    return order
+
+
+class ReplayEps:
+    """eps_provider for the mauv engine that replays ``eps_generator_source(seed)`` — the
+    stream the golden run fed the reference — in the reference's consumption order: pass k of
+    the sequential MC loop draws every layer's epsilon in forward order before pass k+1.  The
+    engine asks per layer for the next G passes; each request that runs past the passes
+    generated so far draws whole passes from the generator, so chunked MC consumption matches
+    the sequential stream."""
+
+    def __init__(self, model, order, seed):
+        self.g = torch.Generator().manual_seed(seed)
+        self.order = order
+        self.names = {id(mod): n for n, mod in model.named_modules()}
+        self.queues = {(n, e): [] for n, e, _ in order}
+
+    def _draw_pass(self):
+        for n, e, shape in self.order:
+            self.queues[(n, e)].append(torch.randn(shape, generator=self.g).reshape(-1))
+
+    def __call__(self, module, name, G):
+        q = self.queues[(self.names[id(module)], name)]
+        while len(q) < G:
+            self._draw_pass()
+        out, q[:G] = q[:G], []
+        return torch.stack(out).cuda().contiguous()
+
+
+class ListLoader:
+    """Minimal DataLoader stand-in (iterable of batches with ``batch_size``), as the golden
+    run fed the reference loops (tests/golden/make_golden.py)."""
+
+    def __init__(self, batches, batch_size):
+        self.batches, self.batch_size = batches, batch_size
+
+    def __iter__(self):
+        return iter(self.batches)
+
+    def __len__(self):
+        return len(self.batches)
+
+
+class NullWriter:
+    """SummaryWriter stand-in (tensorboard is not installed)."""
+
+    def add_scalar(self, *a, **k):
+        pass

@@ -1,0 +1,278 @@
+"""The drop-in loop functions on the HIP path against the REFERENCE's own outputs.
+
+tests/golden/make_golden.py ran the reference's ``train_multimodal_model``,
+``evaluate_multimodal_model``, ``multimodal_predict_and_save`` and ``train_unimodal_model``
+(train/multimodal.py:25-202,204-369, inference/predictors.py:9-97, train/unimodal.py:21-175)
+on CPU, with epsilons drawn from ``eps_generator_source(SEED_EPS + k)`` in forward order.
+Here the same functions are imported from the drop-in package at the reference's module paths
+(``Multimodal_AUV.train.multimodal`` ...), the model runs on the GPU through libmauv_hip, and
+the engine is fed the same epsilon stream (tests.helpers.ReplayEps: pass k of the sequential
+MC loop draws every layer before pass k+1) — so the CSV rows, losses, accuracies and updated
+parameters must be the reference's.
+
+Tolerances (fp32 GPU vs the reference's fp32 CPU run; the model is the same, the arithmetic
+order differs).  Quantities downstream of an Adam step, and the MC variance, are judged
+against a float64 run of the oracle instead: the HIP result must be as accurate as the
+reference's own fp32 result (within 3x its error vs float64).  Adam's first update is
+lr*g/(|g|+1e-8), a sign for almost every element, so wherever a gradient is within rounding of
+zero (the CE and KL gradients cancel there) any two fp32 runs differ by up to 2 lr; the
+probability variance is a difference of squares.
+  loss / KL terms      relative 1e-5       (dominated by the KL sum over 73 M weights)
+  cross-entropy        absolute 2e-5
+  uncertainties        predictive entropy 1e-5 abs; epistemic difference 2e-6 abs;
+                       aleatoric 1e-5 abs; MC variance of the probabilities 3e-8 abs — a
+                       difference-of-squares statistic: a per-probability error dp moves it by
+                       ~2 std(p) dp, and std(p) ~1e-3 here (var ~1e-6), so dp <= 1e-5
+                       (logits within ~1e-4) bounds it at ~3e-8
+  accuracy / classes   exact
+  parameters after Adam  digest (sum, sum|p|, sum p^2 over 146.8 M / 47.0 M values) rel 1e-6;
+                       fc2.mu_weight 1e-7 abs
+"""
+import copy
+import csv
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import loops_ref
+from oracle.model_ref import define_models as oracle_define, DEFAULT_PRIOR
+from tests.golden.common import SEED_MODEL, SEED_EPS, SEED_DATA, make_batches, \
+    eps_generator_source, param_digest
+from tests.helpers import forward_order, ReplayEps, ListLoader, NullWriter
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+G = json.load(open(os.path.join(HERE, "golden.json")))
+A = np.load(os.path.join(HERE, "golden.npz"))
+DEV = torch.device("cuda")
+
+
+def _pair(key):
+    """Oracle model (reference weights recipe: torch.manual_seed(SEED_MODEL) + define_models)
+    and the drop-in model holding the same state."""
+    from Multimodal_AUV.models.model_utils import define_models
+    torch.manual_seed(SEED_MODEL)
+    o = oracle_define(None, 7, DEFAULT_PRIOR)[key]
+    m = define_models(DEV, 7, DEFAULT_PRIOR)[key]
+    m.load_state_dict(o.state_dict())
+    return o, m.to(DEV)
+
+
+def _batches():
+    return make_batches(SEED_DATA, 2, B=2, S_opt=64, S_son=64)
+
+
+def _replay(m, o, seed, *inputs):
+    from mauv.engine import root_state
+    root_state(m).eps_provider = ReplayEps(m, forward_order(copy.deepcopy(o), *inputs), seed)
+
+
+def _rel(a, b, tol):
+    assert abs(float(a) - float(b)) <= tol * abs(float(b)), (a, b)
+
+
+def _digest_close(d, ref, rel=1e-6):
+    assert d["n"] == ref["n"]
+    for k in ("sum", "abs", "sq"):
+        assert abs(d[k] - ref[k]) <= rel * abs(ref[k]), (k, d[k], ref[k])
+
+
+def _oracle_g5(dtype=torch.float32):
+    """The reference's G5 epoch replayed on the CPU oracle (tests/test_oracle_golden.py pins
+    the fp32 run to the golden).  float64: the 'truth' the fp32 runs are judged against."""
+    from oracle import bayes_ref
+    torch.manual_seed(SEED_MODEL)
+    o = oracle_define(None, 7, DEFAULT_PRIOR)["multimodal_model"].to(dtype)
+    bayes_ref.set_eps_source(eps_generator_source(SEED_EPS + 1))
+    res = []
+    try:
+        opt = torch.optim.Adam(o.parameters(), lr=5e-5)
+        crit = torch.nn.CrossEntropyLoss()
+        for b in _batches():
+            res.append(loops_ref.train_step_multimodal(
+                o, b["main_image"].to(dtype), b["bathy_image"].to(dtype),
+                b["sss_image"].to(dtype), b["label"], crit, opt, 0, 2, 2, 2))
+    finally:
+        bayes_ref.set_eps_source(None)
+    return o, res
+
+
+def _oracle_trained_g5():
+    """The G5-trained model state (the reference evaluated / predicted with that model)."""
+    return _oracle_g5()[0]
+
+
+def _as_accurate(gpu, ref, truth, floor):
+    """The HIP result is as accurate as the reference's own fp32 CPU result: its max error vs
+    the float64 run is within 3x the reference's (+ an absolute floor of a few fp32 ulps)."""
+    gpu, ref, truth = (np.asarray(v, dtype=np.float64) for v in (gpu, ref, truth))
+    eg, er = np.abs(gpu - truth).max(), np.abs(ref - truth).max()
+    assert eg <= 3.0 * er + floor, (eg, er, floor)
+
+
+def test_g5_train_multimodal_model(tmp_path):
+    import Multimodal_AUV.train.multimodal as mm
+    o, m = _pair("multimodal_model")
+    batches = _batches()
+    b0 = batches[0]
+    _replay(m, o, SEED_EPS + 1, b0["main_image"], b0["bathy_image"], b0["sss_image"])
+    opt = torch.optim.Adam(m.parameters(), lr=5e-5)
+    csv5 = tmp_path / "run" / "multimodal_training.csv"
+    csv5.parent.mkdir(parents=True)
+    loss, acc = mm.train_multimodal_model(m, ListLoader(batches, 2), torch.nn.CrossEntropyLoss(),
+                                          opt, epoch=0, device=DEV, model_type="multimodal",
+                                          total_num_epochs=2, num_mc=2, sum_writer=NullWriter(),
+                                          csv_path=str(csv5))
+    o64, r64 = _oracle_g5(torch.float64)
+    _as_accurate(loss, G["g5_loss"], sum(float(r["loss"]) for r in r64) / 4, 1e-6 * G["g5_loss"])
+    assert acc == G["g5_acc"]
+    rows = list(csv.reader(open(csv5)))
+    ref = G["g5_csv"]
+    assert rows[0] == ref[0] and len(rows) == len(ref)
+    got, want = rows[1], ref[1]
+    assert [got[i] for i in (0, 1, 3, 4, 7, 8)] == [want[i] for i in (0, 1, 3, 4, 7, 8)]
+    _rel(got[2], want[2], 1e-5)
+    _rel(got[5], want[5], 1e-5)
+    # cross-entropy of the second batch: after one Adam step, whose sign-like first update
+    # flips wherever a gradient is within rounding of zero (fp32 CPU and GPU alike)
+    _as_accurate(float(got[6]), float(want[6]), float(r64[-1]["ce"]), 2e-6)
+    # the reference saves the model every 5 epochs (multimodal.py:189-190; epoch 0 included)
+    assert (tmp_path / "models" / "bayesian_model_typemultimodal_bathy_patchnone_sss_patchnone.pth"
+            ).exists()
+    _digest_close(param_digest(m), G["g5_param_digest"])
+    _as_accurate(m.fc2.mu_weight.detach().cpu().numpy(), A["g5_fc2_mu_weight"],
+                 o64.fc2.mu_weight.detach().numpy(), 1e-7)
+
+
+def test_g6_evaluate_and_predict(tmp_path, monkeypatch):
+    import Multimodal_AUV.train.multimodal as mm
+    import Multimodal_AUV.inference.predictors as pr
+    from Multimodal_AUV.models.model_utils import define_models
+    o = _oracle_trained_g5()
+    m = define_models(DEV, 7, DEFAULT_PRIOR)["multimodal_model"]
+    m.load_state_dict(o.state_dict())
+    m = m.to(DEV)
+    batches = _batches()
+    b0 = batches[0]
+    _replay(m, o, SEED_EPS + 2, b0["main_image"], b0["bathy_image"], b0["sss_image"])
+    csv6 = tmp_path / "run" / "multimodal_test.csv"
+    csv6.parent.mkdir(parents=True)
+    acc6 = mm.evaluate_multimodal_model(m, ListLoader(batches, 2), DEV, epoch=0,
+                                        total_num_epochs=2, num_mc=3, model_type="multimodal",
+                                        csv_path=str(csv6))
+    assert acc6 == G["g6_eval_acc"]
+    rows = list(csv.reader(open(csv6)))
+    ref = G["g6_eval_csv"]
+    assert rows[0] == ref[0] and len(rows) == len(ref)
+    got, want = rows[1], ref[1]
+    assert [got[i] for i in (0, 1, 3, 8, 9)] == [want[i] for i in (0, 1, 3, 8, 9)]
+    _rel(got[2], want[2], 1e-5)                               # test loss
+    assert abs(float(got[4]) - float(want[4])) <= 1e-5        # predictive entropy
+    assert abs(float(got[5]) - float(want[5])) <= 2e-6        # epistemic = H[p_bar] - E[H[p]]
+    _rel(got[6], want[6], 1e-5)                               # scaled KL
+    assert abs(float(got[7]) - float(want[7])) <= 2e-5        # cross-entropy
+
+    # predictors.py at fp32, as the golden was taken: the reference's CPU autocast (bf16)
+    # crashes at predictors.py:74, so make_golden.py disabled autocast; the same switch here
+    real_autocast = torch.amp.autocast
+    monkeypatch.setattr(torch.amp, "autocast",
+                        lambda *a, **k: real_autocast(device_type="cuda", enabled=False))
+    _replay(m, o, SEED_EPS + 3, b0["main_image"], b0["bathy_image"], b0["sss_image"])
+    pred_loader = [(b["main_image"], b["bathy_image"], b["sss_image"],
+                    [f"img{i}_{j}" for j in range(2)]) for i, b in enumerate(batches)]
+    csvp = tmp_path / "pred.csv"
+    pr.multimodal_predict_and_save(m, pred_loader, DEV, str(csvp), num_mc_samples=4)
+    rows = list(csv.reader(open(csvp)))
+    ref = G["g6_predict_csv"]
+    assert rows[0] == ref[0] and len(rows) == len(ref)
+    # float64 truth for the same weights and epsilons
+    from oracle import bayes_ref
+    o64 = copy.deepcopy(o).double()
+    bayes_ref.set_eps_source(eps_generator_source(SEED_EPS + 3))
+    try:
+        var64 = torch.cat([loops_ref.predict_batch(o64, b["main_image"].double(),
+                                                   b["bathy_image"].double(),
+                                                   b["sss_image"].double(), 4)[1]
+                           for b in batches]).numpy()
+    finally:
+        bayes_ref.set_eps_source(None)
+    for got, want in zip(rows[1:], ref[1:]):
+        assert got[0] == want[0] and int(got[1]) == int(want[1])
+        assert abs(float(got[3]) - float(want[3])) <= 1e-5, (got, want)
+    _as_accurate([float(r[2]) for r in rows[1:]], [float(r[2]) for r in ref[1:]], var64, 1e-9)
+
+
+def test_g6_predict_under_autocast(tmp_path):
+    """The drop-in predictor autocasts like predictors.py:55 (f16 trunks on the GPU): classes
+    equal to the reference's fp32 golden, aleatoric entropy within SURVEY §8c's 16-bit row
+    (1e-2), MC variance within 1e-4 absolute (the golden values are ~1e-6: f16 rounding of
+    the trunk activations is visible there, so only its scale is checked)."""
+    import Multimodal_AUV.inference.predictors as pr
+    from Multimodal_AUV.models.model_utils import define_models
+    o = _oracle_trained_g5()
+    m = define_models(DEV, 7, DEFAULT_PRIOR)["multimodal_model"]
+    m.load_state_dict(o.state_dict())
+    m = m.to(DEV)
+    batches = _batches()
+    b0 = batches[0]
+    _replay(m, o, SEED_EPS + 3, b0["main_image"], b0["bathy_image"], b0["sss_image"])
+    pred_loader = [(b["main_image"], b["bathy_image"], b["sss_image"],
+                    [f"img{i}_{j}" for j in range(2)]) for i, b in enumerate(batches)]
+    seen = []
+    from mauv import engine
+    real = engine.TrunkRunner.__init__
+
+    def spy(self, trunk, state, G, sample0, save, dtype=torch.float32, *a, **k):
+        seen.append(dtype)
+        real(self, trunk, state, G, sample0, save, dtype, *a, **k)
+    engine.TrunkRunner.__init__ = spy
+    try:
+        csvp = tmp_path / "pred16.csv"
+        pr.multimodal_predict_and_save(m, pred_loader, DEV, str(csvp), num_mc_samples=4)
+    finally:
+        engine.TrunkRunner.__init__ = real
+    assert seen and all(d == torch.float16 for d in seen), seen
+    rows = list(csv.reader(open(csvp)))
+    for got, want in zip(rows[1:], G["g6_predict_csv"][1:]):
+        assert got[0] == want[0] and int(got[1]) == int(want[1])
+        assert abs(float(got[2]) - float(want[2])) <= 1e-4
+        assert abs(float(got[3]) - float(want[3])) <= 1e-2
+
+
+def test_g7_train_unimodal_model(tmp_path):
+    import Multimodal_AUV.train.unimodal as um
+    o, m = _pair("image_model")
+    batches = _batches()
+    _replay(m, o, SEED_EPS + 4, batches[0]["main_image"])
+    opt = torch.optim.Adam(m.parameters(), lr=1e-5)
+    csv7 = tmp_path / "run" / "image.csv"
+    csv7.parent.mkdir(parents=True)
+    acc, loss = um.train_unimodal_model(m, ListLoader(batches, 2), torch.nn.CrossEntropyLoss(),
+                                        opt, epoch=1, total_num_epochs=3, num_mc=2,
+                                        sum_writer=NullWriter(), device=DEV, model_type="image",
+                                        csv_path=str(csv7))
+    assert acc == G["g7_acc"]
+    # float64 truth: the reference's epoch on the oracle in double precision
+    from oracle import bayes_ref
+    torch.manual_seed(SEED_MODEL)
+    o64 = oracle_define(None, 7, DEFAULT_PRIOR)["image_model"].double()
+    bayes_ref.set_eps_source(eps_generator_source(SEED_EPS + 4))
+    try:
+        opt64 = torch.optim.Adam(o64.parameters(), lr=1e-5)
+        loss64 = sum(float(loops_ref.train_step_unimodal(
+            o64, b["main_image"].double(), b["label"], torch.nn.CrossEntropyLoss(), opt64, 1, 3,
+            2, 2)["loss"]) for b in batches) / 4
+    finally:
+        bayes_ref.set_eps_source(None)
+    _as_accurate(loss, G["g7_loss"], loss64, 1e-6 * G["g7_loss"])
+    rows = list(csv.reader(open(csv7)))
+    ref = G["g7_csv"]
+    assert rows[0] == ref[0] and len(rows) == len(ref)
+    got, want = rows[1], ref[1]
+    assert [got[i] for i in (0, 1, 3, 4)] == [want[i] for i in (0, 1, 3, 4)]
+    assert float(got[2]) == float(loss)
+    _digest_close(param_digest(m), G["g7_param_digest"])

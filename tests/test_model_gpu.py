@@ -42,14 +42,19 @@ def _assert_grads_as_accurate(hip, cpu, truth):
     assert h[2] <= 2.0 * c[2] + 1e-4, (h, c)
 
 
-@pytest.mark.parametrize("S,B,N", [(64, 2, 3), (96, 3, 2)])
-def test_multimodal_train_step_parity(S, B, N):
+@pytest.mark.parametrize("S_opt,S_son,B,N", [
+    (64, 64, 2, 3), (96, 96, 3, 2),
+    (224, 256, 2, 2),    # BASELINE configs[1]/[2] tile sizes (gradients included)
+    (224, 128, 2, 2),    # configs[4] sonar sweep: layer4 of the sonar trunks at 4x4
+    (224, 512, 1, 2),    # configs[4] sonar sweep: 512 px sonar patches
+])
+def test_multimodal_train_step_parity(S_opt, S_son, B, N):
     from mauv.engine import root_state
     from mauv.kl import get_kl_loss
     from mauv import mchead
     o, m = build_pair()
     o_pre = copy.deepcopy(o)   # fresh running statistics for the fp64 'truth' run
-    batch = make_batches(SEED_DATA, 1, B=B, S_opt=S, S_son=S)[0]
+    batch = make_batches(SEED_DATA, 1, B=B, S_opt=S_opt, S_son=S_son)[0]
     x, b, s, y = batch["main_image"], batch["bathy_image"], batch["sss_image"], batch["label"]
 
     def oracle_loss(model, dt=torch.float32):
@@ -164,21 +169,26 @@ def test_unimodal_resnet50custom_parity():
     _assert_grads_as_accurate(list(m.parameters()), list(o.parameters()), list(o64.parameters()))
 
 
-def test_predict_uncertainty_parity():
-    """Fused MC statistics (HIP) vs predictors.py maths on the oracle (fp32, no autocast)."""
+@pytest.mark.parametrize("N,chunk", [(5, 5), (7, 3)])
+def test_predict_uncertainty_parity(N, chunk):
+    """Fused MC statistics (HIP) vs predictors.py maths on the oracle (fp32, no autocast);
+    chunk < N takes the multi-chunk accumulate path configs[3] runs (mc_stats accumulate)."""
     from mauv.engine import root_state
     from mauv.predict import mc_statistics
+    from tests.helpers import ReplayEps, forward_order
+    from tests.golden.common import eps_generator_source
     o, m = build_pair()
     batch = make_batches(SEED_DATA, 1, B=3, S_opt=64, S_son=64)[0]
     x, b, s = batch["main_image"], batch["bathy_image"], batch["sss_image"]
-    N = 5
-    bridge = EpsBridge(o, m, 5)
-    with bridge:
+    order = forward_order(copy.deepcopy(o), x, b, s)
+    bayes_ref.set_eps_source(eps_generator_source(5))
+    try:
         pred_o, var_o, alea_o, P = loops_ref.predict_batch(o, x, b, s, N)
-    bridge.collect()
-    root_state(m).eps_provider = bridge.provider
+    finally:
+        bayes_ref.set_eps_source(None)
+    root_state(m).eps_provider = ReplayEps(m, order, 5)
     with torch.no_grad():
-        st = mc_statistics(m, *_cuda(x, b, s), N, chunk=N)
+        st = mc_statistics(m, *_cuda(x, b, s), N, chunk=chunk)
     assert torch.equal(st["pred"].cpu(), pred_o)
     np.testing.assert_allclose(st["var"].cpu().numpy(), var_o.numpy(), atol=1e-6, rtol=1e-3)
     np.testing.assert_allclose(st["aleatoric"].cpu().numpy(), alea_o.numpy(), atol=1e-5)
@@ -198,3 +208,58 @@ def test_full_resolution_forward():
     with torch.no_grad():
         logits = m.mc_forward(*_cuda(x, b, s), 2)
     _assert_close(logits, o_logits)
+
+
+def test_mc_statistics_chunking_is_exact():
+    """Chunked MC inference == one chunk: each sample's weights come from Philox keyed by its
+    sample index and BN statistics are per sample, so the logits are bit-identical and only
+    the float64 summation order of the statistics differs."""
+    from mauv.engine import root_state
+    from mauv.predict import mc_statistics
+    _, m = build_pair()
+    batch = make_batches(SEED_DATA, 1, B=16, S_opt=64, S_son=64)[0]
+    x, b, s = _cuda(batch["main_image"], batch["bathy_image"], batch["sss_image"])
+    st = root_state(m)
+    out = []
+    for chunk in (20, 6):
+        st.offset = 0
+        with torch.no_grad(), torch.autocast("cuda"):
+            out.append(mc_statistics(m, x, b, s, 20, chunk=chunk))
+    a, c = out
+    assert torch.equal(a["pred"], c["pred"])
+    for k in ("mean_prob", "var", "aleatoric", "predictive_entropy"):
+        assert (a[k] - c[k]).abs().max().item() <= 1e-6 * max(1.0, a[k].abs().max().item()), k
+
+
+def test_configs3_full_size_inference_properties():
+    """BASELINE configs[3] at full size: 100 MC passes over 256 triplets (224 optical, 256
+    sonar) under autocast as predictors.py:55 — the multi-chunk path — gives finite,
+    well-formed statistics: probabilities sum to 1, unbiased variance >= 0 and bounded by
+    p(1-p) N/(N-1), 0 <= aleatoric <= log C, predictive entropy >= aleatoric (Jensen),
+    class = argmax of the mean probability."""
+    import math
+    from mauv.predict import mc_statistics, mc_chunk
+    _, m = build_pair()
+    g = torch.Generator().manual_seed(99)
+    B, N, C = 256, 100, 7
+    x = torch.randn(B, 3, 224, 224, generator=g).cuda()
+    bathy = torch.rand(B, 3, 256, 256, generator=g)
+    bathy[:, 2] = 0
+    bathy = bathy.cuda()
+    sss = torch.rand(B, 1, 256, 256, generator=g).cuda()
+    chunk = mc_chunk(m, B, N, dtype=torch.float16, device=x.device,
+                     hw=[(224, 224), (256, 256), (256, 256)])
+    assert 1 <= chunk < N   # the accumulate path
+    with torch.no_grad(), torch.autocast("cuda"):
+        st = mc_statistics(m, x, bathy, sss, N)
+    mp, var, alea, ent, pred = (st[k].cpu() for k in
+                                ("mean_prob", "var", "aleatoric", "predictive_entropy", "pred"))
+    for t in (mp, var, alea, ent):
+        assert torch.isfinite(t).all()
+    assert (mp.sum(1) - 1).abs().max().item() < 1e-5
+    assert (var >= 0).all()
+    assert (var <= (mp * (1 - mp)).mean(1) * N / (N - 1) + 1e-6).all()
+    assert (alea >= -1e-6).all() and (alea <= math.log(C) + 1e-5).all()
+    # H[p_bar] (eps 1e-8) >= E[H[p]] (eps 1e-7) up to the different log epsilons
+    assert (ent - alea >= -1e-4).all()
+    assert torch.equal(pred, mp.argmax(1))
