@@ -14,6 +14,9 @@ drives the reference's OWN code:
   G6  train/multimodal.py:evaluate_multimodal_model + inference/predictors.py:
       multimodal_predict_and_save (CSV rows)
   G7  train/unimodal.py:train_unimodal_model (ResNet50Custom BNN, config 1 path, 64x64)
+  G8  train/loop_utils.py:train_and_evaluate_multimodal_model (epoch driver, 2 epochs)
+  G9  train/loop_utils.py:train_and_evaluate_unimodal_model (epoch driver, range(1, 3))
+      (``--loops``: writes golden_loops.json only)
 
 Epsilons come from one seeded torch.Generator consumed in forward order, so the oracle
 (``oracle/``) reproduces them by running the same module order.  Outputs land in
@@ -178,10 +181,56 @@ def main():
     bayes_ref.set_eps_source(None)
 
     here = os.path.dirname(os.path.abspath(__file__))
+    if "--loops" in sys.argv:   # G8/G9 only (golden_loops.json); G3-G7 stay as committed
+        loops_golden(mu, SummaryWriter, prior, tmp, here)
+        return
     with open(os.path.join(here, "golden.json"), "w") as f:
         json.dump(out, f, indent=1)
     np.savez_compressed(os.path.join(here, "golden.npz"), **arrays)
     print(json.dumps({k: v for k, v in out.items() if not k.endswith("csv")}, indent=1)[:2000])
+
+
+def loops_golden(mu, SummaryWriter, prior, tmp, here):
+    """G8: train/loop_utils.py:162-250 train_and_evaluate_multimodal_model (2 epochs, one
+    train and one test batch, num_mc=2; StepLR(step_size=1, gamma=0.5) so the scheduler's
+    two steps per epoch (:233, :246) show in the CSV lr column), optimizer and scheduler from
+    the reference's define_optimizers_and_schedulers (:13-63).
+    G9: train_and_evaluate_unimodal_model (:65-159; epochs range(1, 3)) on the image model."""
+    lu = importlib.import_module("Multimodal_AUV.train.loop_utils")
+    batches = make_batches(SEED_DATA, n_batches=2, B=2, S_opt=64, S_son=64)
+    out = {}
+    opt_p = {k: {"lr": 5e-5} for k in ("image_model", "bathy_model", "sss_model",
+                                        "multimodal_model")}
+    sch_p = {k: {"step_size": 1, "gamma": 0.5} for k in opt_p}
+    torch.manual_seed(SEED_MODEL)
+    models = mu.define_models(torch.device("cpu"), 7, prior)
+    crit, opts, schs = lu.define_optimizers_and_schedulers(models, opt_p, sch_p)
+    bayes_ref.set_eps_source(eps_generator_source(SEED_EPS + 5))
+    d8 = os.path.join(tmp, "g8", "csvs")
+    lu.train_and_evaluate_multimodal_model(
+        ListLoader(batches[:1], 2), ListLoader(batches[1:], 2), models["multimodal_model"], crit,
+        opts["multimodal_model"], schs["multimodal_model"], num_epochs=2, num_mc=2,
+        device=torch.device("cpu"), model_type="multimodal", bathy_patch_type=None,
+        sss_patch_type=None, csv_path=d8, sum_writer=SummaryWriter())
+    out["g8_train_csv"] = list(csv.reader(open(os.path.join(d8, "multimodal_training.csv"))))
+    out["g8_test_csv"] = list(csv.reader(open(os.path.join(d8, "multimodal_test.csv"))))
+    out["g8_lr_after"] = opts["multimodal_model"].param_groups[0]["lr"]
+    out["g8_param_digest"] = param_digest(models["multimodal_model"])
+    bayes_ref.set_eps_source(eps_generator_source(SEED_EPS + 6))
+    d9 = os.path.join(tmp, "g9")
+    os.makedirs(d9, exist_ok=True)
+    lu.train_and_evaluate_unimodal_model(
+        models["image_model"], ListLoader(batches[:1], 2), ListLoader(batches[1:], 2), crit,
+        opts["image_model"], schs["image_model"], num_epochs=3, device=torch.device("cpu"),
+        model_name="image", save_dir=d9, num_mc=2, sum_writer=SummaryWriter())
+    out["g9_train_csv"] = list(csv.reader(open(os.path.join(d9, "image.csv"))))
+    out["g9_eval_csv"] = list(csv.reader(open(os.path.join(d9, "image_evaluate.csv"))))
+    out["g9_lr_after"] = opts["image_model"].param_groups[0]["lr"]
+    out["g9_param_digest"] = param_digest(models["image_model"])
+    bayes_ref.set_eps_source(None)
+    with open(os.path.join(here, "golden_loops.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1)[:3000])
 
 
 if __name__ == "__main__":

@@ -276,3 +276,138 @@ def test_g7_train_unimodal_model(tmp_path):
     assert [got[i] for i in (0, 1, 3, 4)] == [want[i] for i in (0, 1, 3, 4)]
     assert float(got[2]) == float(loss)
     _digest_close(param_digest(m), G["g7_param_digest"])
+
+
+GL = json.load(open(os.path.join(HERE, "golden_loops.json")))
+_LOOP_KEYS = ("image_model", "bathy_model", "sss_model", "multimodal_model")
+
+
+def _all_models():
+    from Multimodal_AUV.models.model_utils import define_models
+    torch.manual_seed(SEED_MODEL)
+    o = oracle_define(None, 7, DEFAULT_PRIOR)
+    m = define_models(DEV, 7, DEFAULT_PRIOR)
+    for k in _LOOP_KEYS:
+        m[k].load_state_dict(o[k].state_dict())
+        m[k] = m[k].to(DEV)
+    return o, m
+
+
+def _close_rows(got, want, exact, rel=(), absol=()):
+    assert [got[i] for i in exact] == [want[i] for i in exact], (got, want)
+    for i, tol in rel:
+        _rel(got[i], want[i], tol)
+    for i, tol in absol:
+        assert abs(float(got[i]) - float(want[i])) <= tol, (i, got, want)
+
+
+def test_g8_train_and_evaluate_multimodal_model(tmp_path):
+    """loop_utils.py:162-250 through the drop-in: two epochs of train + evaluate with the
+    optimizer / StepLR from define_optimizers_and_schedulers (FusedAdam on the GPU), the
+    scheduler stepped after training and after evaluation.  Post-Adam quantities get the
+    headroom G5's float64 analysis measured for the reference's own fp32 run (~2e-5 CE)."""
+    import Multimodal_AUV.train.loop_utils as lu
+    o, m = _all_models()
+    b = _batches()
+    opt_p = {k: {"lr": 5e-5} for k in _LOOP_KEYS}
+    sch_p = {k: {"step_size": 1, "gamma": 0.5} for k in _LOOP_KEYS}
+    crit, opts, schs = lu.define_optimizers_and_schedulers(m, opt_p, sch_p)
+    _replay(m["multimodal_model"], o["multimodal_model"], SEED_EPS + 5,
+            b[0]["main_image"], b[0]["bathy_image"], b[0]["sss_image"])
+    d = tmp_path / "csvs"
+    lu.train_and_evaluate_multimodal_model(
+        ListLoader(b[:1], 2), ListLoader(b[1:], 2), m["multimodal_model"], crit,
+        opts["multimodal_model"], schs["multimodal_model"], num_epochs=2, num_mc=2, device=DEV,
+        model_type="multimodal", bathy_patch_type=None, sss_patch_type=None, csv_path=str(d),
+        sum_writer=NullWriter())
+    tr = list(csv.reader(open(d / "multimodal_training.csv")))
+    te = list(csv.reader(open(d / "multimodal_test.csv")))
+    assert len(tr) == len(GL["g8_train_csv"]) == 3 and len(te) == len(GL["g8_test_csv"]) == 3
+    assert tr[0] == GL["g8_train_csv"][0] and te[0] == GL["g8_test_csv"][0]
+    for e, (got, want) in enumerate(zip(tr[1:], GL["g8_train_csv"][1:])):
+        _close_rows(got, want, (0, 1, 3, 4, 7, 8), rel=((2, 1e-4), (5, 1e-4)),
+                    absol=((6, 2e-5 if e == 0 else 1e-4),))
+    for got, want in zip(te[1:], GL["g8_test_csv"][1:]):
+        _close_rows(got, want, (0, 1, 3, 8, 9), rel=((2, 1e-4), (6, 1e-4)),
+                    absol=((4, 1e-4), (5, 1e-5), (7, 1e-4)))
+    assert opts["multimodal_model"].param_groups[0]["lr"] == GL["g8_lr_after"]
+    _digest_close(param_digest(m["multimodal_model"]), GL["g8_param_digest"])
+
+
+def _oracle_g9(dtype):
+    """G9's driver (loop_utils.py:65-159: epochs 1..2, train step, MC eval, scheduler step)
+    replayed on the oracle -> per epoch (eval loss, MC variance, aleatoric entropy)."""
+    import torch.nn.functional as F
+    from oracle import bayes_ref
+    torch.manual_seed(SEED_MODEL)
+    o = oracle_define(None, 7, DEFAULT_PRIOR)["image_model"].to(dtype)
+    b = _batches()
+    opt = torch.optim.Adam(o.parameters(), lr=5e-5)
+    sch = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5)
+    bayes_ref.set_eps_source(eps_generator_source(SEED_EPS + 6))
+    out = []
+    try:
+        for e in (1, 2):
+            loops_ref.train_step_unimodal(o, b[0]["main_image"].to(dtype), b[0]["label"],
+                                          torch.nn.CrossEntropyLoss(), opt, e, 3, 2, 2)
+            with torch.no_grad():
+                lg = torch.stack([o(b[1]["main_image"].to(dtype)) for _ in range(2)])
+                kl = bayes_ref.get_kl_loss(o)
+                loss = F.cross_entropy(lg.mean(0), b[1]["label"]) + 2 ** (e + 1) / 8 * kl / 2
+                P = torch.softmax(lg, -1)
+                out.append((loss.item() / 2, torch.var(P, 0).mean(1).mean().item(),
+                            torch.mean(-torch.sum(P * torch.log(P + 1e-7), -1), 0).mean().item()))
+            sch.step()
+    finally:
+        bayes_ref.set_eps_source(None)
+    return out
+
+
+def test_g9_train_and_evaluate_unimodal_model(tmp_path):
+    """loop_utils.py:65-159 through the drop-in (epochs range(1, num_epochs), one scheduler
+    step per epoch) on the Bayesian ResNet50Custom image model.
+
+    After an Adam step the eval statistics are chaotic in the arithmetic: each of the 47 M
+    parameters moves by ~+-lr (5e-5) and moves the other way wherever its gradient's sign is
+    within rounding, so the reference's own fp32 run and the same run in float64 differ by
+    ~0.04 in the eval logits (7e-5 with lr = 0); the reference's fp32 run on 1 CPU thread
+    instead of 8 differs from itself by 5e-3 in the first epoch's eval loss and 9 % in its MC
+    variance.  The eval columns (loss, MC variance, aleatoric entropy) are therefore judged
+    against that measured spread of fp32 implementations: the golden (8 threads), the oracle
+    on 1 thread and a float64 replay span a per-column scale (largest pairwise difference
+    over the epochs); the HIP value must lie within 3 scales of the float64 value."""
+    import Multimodal_AUV.train.loop_utils as lu
+    o, m = _all_models()
+    b = _batches()
+    opt_p = {k: {"lr": 5e-5} for k in _LOOP_KEYS}
+    sch_p = {k: {"step_size": 1, "gamma": 0.5} for k in _LOOP_KEYS}
+    crit, opts, schs = lu.define_optimizers_and_schedulers(m, opt_p, sch_p)
+    _replay(m["image_model"], o["image_model"], SEED_EPS + 6, b[0]["main_image"])
+    lu.train_and_evaluate_unimodal_model(
+        m["image_model"], ListLoader(b[:1], 2), ListLoader(b[1:], 2), crit, opts["image_model"],
+        schs["image_model"], num_epochs=3, device=DEV, model_name="image",
+        save_dir=str(tmp_path), num_mc=2, sum_writer=NullWriter())
+    tr = list(csv.reader(open(tmp_path / "image.csv")))
+    ev = list(csv.reader(open(tmp_path / "image_evaluate.csv")))
+    assert tr[0] == GL["g9_train_csv"][0] and ev[0] == GL["g9_eval_csv"][0]
+    assert len(tr) == len(GL["g9_train_csv"]) == 3 and len(ev) == len(GL["g9_eval_csv"]) == 3
+    for got, want in zip(tr[1:], GL["g9_train_csv"][1:]):
+        _close_rows(got, want, (0, 1, 3, 4), rel=((2, 1e-4),))
+    for got, want in zip(ev[1:], GL["g9_eval_csv"][1:]):
+        _close_rows(got, want, (0, 1, 3))
+    t64 = np.array(_oracle_g9(torch.float64))
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        t1 = np.array(_oracle_g9(torch.float32))
+    finally:
+        torch.set_num_threads(nt)
+    for col, j in ((2, 0), (4, 1), (5, 2)):
+        gpu = np.array([float(r[col]) for r in ev[1:]])
+        ref = np.array([float(r[col]) for r in GL["g9_eval_csv"][1:]])
+        scale = max(np.abs(ref - t64[:, j]).max(), np.abs(t1[:, j] - t64[:, j]).max(),
+                    np.abs(t1[:, j] - ref).max())
+        assert (np.abs(gpu - t64[:, j]) <= 3 * scale + 1e-7 * np.abs(t64[:, j])).all(), \
+            (col, gpu, ref, t64[:, j])
+    assert opts["image_model"].param_groups[0]["lr"] == GL["g9_lr_after"]
+    _digest_close(param_digest(m["image_model"]), GL["g9_param_digest"])
