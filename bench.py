@@ -51,17 +51,52 @@ def synthetic_batch(B, S_opt, S_son, device, seed):
     return [t.to(device) for t in (x, bathy, sss, y)]
 
 
+def _host_cpu():
+    """CPU model, physical cores of the host, CPUs this process may run on."""
+    model, cores = platform.processor() or platform.machine(), set()
+    try:
+        phys = core = None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name":
+                    model = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    core = v
+                elif not k and phys is not None:
+                    cores.add((phys, core))
+                    phys = core = None
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"cpu_model": model, "host_physical_cores": len(cores) or None,
+            "host_logical_cpus": os.cpu_count(), "usable_cpus": usable}
+
+
 def cpu_baseline(args):
-    """Reference-semantics CPU path (oracle = torch-CPU restatement, sequential MC loop,
-    per-pass KL, torch Adam) on a bounded sample: B=2, num_mc=2 at full resolution, scaled
-    to the GPU workload's per-triplet cost (work is linear in num_mc)."""
+    """Reference-semantics CPU path (oracle = torch-CPU restatement of the reference's loops:
+    sequential MC loop, per-pass epsilon draws and KL, torch Adam) timed on bounded samples
+    of the same workloads on this host:
+      * configs[1] training (the headline unit): B=2, num_mc=2 at full resolution, scaled to
+        num_mc=5 (work is linear in num_mc and B);
+      * configs[0] in full: unimodal optical BNN (ResNet50Custom(3, 7)), B=8, 224 px,
+        num_mc=5, train/unimodal.py's step;
+      * configs[3] inference: predictors.py's MC loop at B=4, num_mc=2 (fp32: the reference's
+        CPU autocast crashes at predictors.py:74), per MC-sample triplet."""
     from oracle.model_ref import define_models, DEFAULT_PRIOR
     from oracle import loops_ref
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     threads = max(1, min(threads, os.cpu_count() or 1))
     torch.set_num_threads(threads)
     torch.manual_seed(0)
-    model = define_models(None, 7, DEFAULT_PRIOR)["multimodal_model"]
+    models = define_models(None, 7, DEFAULT_PRIOR)
+    model = models["multimodal_model"]
     opt = torch.optim.Adam(model.parameters(), lr=5e-5)
     crit = torch.nn.CrossEntropyLoss()
     Bc, Nc = 2, 2
@@ -73,12 +108,39 @@ def cpu_baseline(args):
         loops_ref.train_step_multimodal(model, x, b, s, y, crit, opt, 0, 2, Nc, Bc)
     dt = (time.perf_counter() - t0) / reps
     per_triplet = dt / Bc * (args.num_mc / Nc)
-    return {"value": round(1.0 / per_triplet, 4), "unit": "triplets/s", "cores": threads,
-            "kind": "port",
-            "sample": f"oracle train step, B={Bc}, num_mc={Nc} (scaled x{args.num_mc}/{Nc} to "
-                      f"num_mc={args.num_mc}), {args.optical}/{args.sonar} px, torch-CPU fp32, "
-                      f"{reps} timed steps of {dt:.2f} s",
-            "host": platform.processor() or platform.machine()}
+    out = {"value": round(1.0 / per_triplet, 4), "unit": "triplets/s", "cores": threads,
+           "kind": "port",
+           "sample": f"oracle train step, B={Bc}, num_mc={Nc} (scaled x{args.num_mc}/{Nc} to "
+                     f"num_mc={args.num_mc}), {args.optical}/{args.sonar} px, torch-CPU fp32, "
+                     f"{reps} timed steps of {dt:.2f} s"}
+    out.update(_host_cpu())
+    # configs[0]: the unimodal CPU path, timed in full
+    uni = models["image_model"]
+    uopt = torch.optim.Adam(uni.parameters(), lr=5e-5)
+    xu, _, _, yu = synthetic_batch(8, args.optical, args.sonar, "cpu", 2)
+    loops_ref.train_step_unimodal(uni, xu, yu, crit, uopt, 0, 2, args.num_mc, 8)   # warm-up
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        loops_ref.train_step_unimodal(uni, xu, yu, crit, uopt, 0, 2, args.num_mc, 8)
+    du = (time.perf_counter() - t0) / reps
+    out["configs0_unimodal"] = {
+        "value": round(8 / du, 4), "unit": "images/s", "ms_per_step": round(du * 1e3, 1),
+        "sample": f"configs[0] in full: ResNet50Custom(3,7) BNN, B=8, {args.optical} px, "
+                  f"num_mc={args.num_mc}, train/unimodal.py step, {reps} timed steps"}
+    # configs[3]: MC inference
+    Bi, Ni = 4, 2
+    xi, bi, si, _ = synthetic_batch(Bi, args.optical, args.sonar, "cpu", 3)
+    loops_ref.predict_batch(model, xi, bi, si, Ni)   # warm-up
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        loops_ref.predict_batch(model, xi, bi, si, Ni)
+    di = (time.perf_counter() - t0) / reps
+    out["inference"] = {
+        "value": round(Bi * Ni / di, 4), "unit": "MC-samples/s",
+        "sample": f"predictors.py MC loop, B={Bi}, num_mc={Ni}, {args.optical}/{args.sonar} px, "
+                  f"fp32, {reps} timed batches of {di:.2f} s (per MC-sample triplet; the "
+                  f"GPU number is B=256, num_mc=100)"}
+    return out
 
 
 def pmc_traffic():
@@ -163,8 +225,8 @@ def main():
     ap.add_argument("--no-bf16", action="store_true",
                     help="skip the bf16 training measurement (configs[2] per-GPU slice)")
     ap.add_argument("--bf16-steps", type=int, default=5)
-    ap.add_argument("--infer-fp32", action="store_true",
-                    help="also time MC inference with fp32 trunks (default: autocast f16 only)")
+    ap.add_argument("--no-infer-fp32", action="store_true",
+                    help="skip MC inference with fp32 trunks (autocast off)")
     ap.add_argument("--exact-steps", type=int, default=2,
                     help="also time the fp32 step with exact f32 MFMA products (0 = skip)")
     args = ap.parse_args()
@@ -276,29 +338,50 @@ def main():
 
     infer = None
     if not args.no_infer:
+        from mauv.predict import multimodal_predict_and_save
         opt.zero_grad(set_to_none=True)
         xi, bi, si, _ = synthetic_batch(args.infer_batch, args.optical, args.sonar, dev, 99)
         group = dist.group.WORLD if world > 1 else None
+        names = [f"tile{i}" for i in range(args.infer_batch)]
+        loader = [(xi, bi, si, names)]
+        pred_csv = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mauv_bench_pred_r{rank}.csv")
+        hw = [(args.optical, args.optical), (args.sonar, args.sonar), (args.sonar, args.sonar)]
 
-        def infer_run(autocast):
-            # the reference predictor wraps its MC loop in torch.amp.autocast (predictors.py:55):
-            # on a GPU that is f16, which the trunks follow; autocast=False -> fp32 trunks.
+        def warm(dtype):
             # Training's cached blocks are released first and the warm-up runs one full MC
-            # chunk, so the timed batch reuses its activation blocks instead of growing (or,
-            # near the HBM limit, flushing and retrying) the caching allocator mid-run.
+            # chunk per rank, so the timed batch reuses its activation blocks instead of
+            # growing (or, near the HBM limit, flushing and retrying) the caching allocator.
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
-            chunk = mc_chunk(model, args.infer_batch, args.infer_mc)
-            with torch.no_grad(), torch.autocast("cuda", enabled=autocast):
-                mc_statistics(model, xi, bi, si, max(world, 2) * chunk, group=group)   # warm-up
-                di = timed(lambda: mc_statistics(model, xi, bi, si, args.infer_mc, group=group), 1)
-            return {"value": round(args.infer_mc * args.infer_batch / di, 2),
-                    "unit": "MC-samples/s", "batch": args.infer_batch, "num_mc": args.infer_mc,
-                    "ms_per_batch": round(di * 1e3, 1), "sharding": "mc" if world > 1 else "none",
-                    "dtype": "f16 (torch.autocast, as predictors.py:55)" if autocast else "fp32"}
-        infer = infer_run(True)
-        if args.infer_fp32:
-            infer["fp32"] = infer_run(False)
+            return mc_chunk(model, args.infer_batch, args.infer_mc, dtype=dtype, device=dev,
+                            hw=hw)
+
+        # the drop-in predictor exactly as a user calls it (inference/predictors.py:9-97):
+        # its own torch.amp.autocast (predictors.py:55 -> f16 trunks), MC samples sharded
+        # across ranks under DistributedMC, fused statistics, CSV rows written
+        chunk = warm(torch.float16)
+        multimodal_predict_and_save(model, loader, dev, pred_csv,
+                                    num_mc_samples=max(world, 2) * chunk)
+        di = timed(lambda: multimodal_predict_and_save(model, loader, dev, pred_csv,
+                                                       num_mc_samples=args.infer_mc), 1)
+        infer = {"value": round(args.infer_mc * args.infer_batch / di, 2),
+                 "unit": "MC-samples/s", "batch": args.infer_batch, "num_mc": args.infer_mc,
+                 "ms_per_batch": round(di * 1e3, 1), "mc_chunk": chunk,
+                 "sharding": "mc" if world > 1 else "none",
+                 "path": "Multimodal_AUV.inference.predictors.multimodal_predict_and_save",
+                 "dtype": "f16 trunks (the predictor's own torch.amp.autocast, predictors.py:55)"}
+        if not args.no_infer_fp32:
+            # fp32 trunks: the same MC statistics with autocast off
+            chunk32 = warm(torch.float32)
+            with torch.no_grad():
+                mc_statistics(model, xi, bi, si, max(world, 2) * chunk32, group=group)
+                d32 = timed(lambda: mc_statistics(model, xi, bi, si, args.infer_mc,
+                                                  group=group), 1)
+            infer["fp32"] = {"value": round(args.infer_mc * args.infer_batch / d32, 2),
+                             "unit": "MC-samples/s", "ms_per_batch": round(d32 * 1e3, 1),
+                             "mc_chunk": chunk32,
+                             "dtype": "fp32 trunks (split-fp32 convs), autocast off",
+                             "path": "mauv.predict.mc_statistics"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -277,13 +277,16 @@ int mauv_pack_nchw_f32(const float* x, int B, int C, int H, int W, int Cp, float
 
 /* ---- fusion head + MC head (head.hip) ----------------------------------------------------
  * AdditiveAttention.forward (models/base_models.py:43-52) epilogues around the q|k|v and
- * score GEMMs: t = tanh(q + k); o = v * softmax(s, dim=1) into the concat slot (:86). */
-int mauv_attn_t(const float* qkv, int rows, float* t, hipStream_t stream);
-int mauv_attn_t_bwd(const float* dt, const float* t, int rows, float* dqkv, hipStream_t stream);
-int mauv_attn_out(const float* qkv, const float* s, int rows, float* comb, int comb_ld,
+ * score GEMMs (qkv rows [q | k | v], each hid wide; the reference's model: hid = 128):
+ * t = tanh(q + k); o = v * softmax(s, dim=1) into the concat slot (:86) of ld comb_ld. */
+int mauv_attn_t(const float* qkv, int rows, int hid, float* t, hipStream_t stream);
+int mauv_attn_t_bwd(const float* dt, const float* t, int rows, int hid, float* dqkv,
+                    hipStream_t stream);
+int mauv_attn_out(const float* qkv, const float* s, int rows, int hid, float* comb, int comb_ld,
                   int comb_off, hipStream_t stream);
 int mauv_attn_out_bwd(const float* dcomb, int comb_ld, int comb_off, const float* qkv,
-                      const float* s, int rows, float* dqkv, float* ds, hipStream_t stream);
+                      const float* s, int rows, int hid, float* dqkv, float* ds,
+                      hipStream_t stream);
 /* bias gradients of the linear layers */
 int mauv_colsum(const float* dy, int G, int rows, int N, float* out, int accumulate,
                 hipStream_t stream);

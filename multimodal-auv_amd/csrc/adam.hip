@@ -18,7 +18,12 @@ __global__ __launch_bounds__(256) void adam_kernel(const MauvAdamEntry* __restri
                                                    float lr, float beta1, float beta2, float eps,
                                                    float wd, float step_size, float bc2_sqrt) {
   const MauvAdamEntry t = tab[blockIdx.y];
-  const long long n4 = t.numel / 4;
+  // 16-byte vector path only when all four tensors are 16-byte aligned (a parameter may be
+  // a view at any offset); otherwise every element takes the scalar loop below
+  const bool aligned = ((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
+                         reinterpret_cast<uintptr_t>(t.exp_avg) |
+                         reinterpret_cast<uintptr_t>(t.exp_avg_sq)) & 15) == 0;
+  const long long n4 = aligned ? t.numel / 4 : 0;
   const float omb1 = 1.0f - beta1, omb2 = 1.0f - beta2;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
     floatx4 p = ((const floatx4*)t.param)[i];
@@ -54,7 +59,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const MauvAdamEntry* __restri
 }  // namespace mauv
 
 // One Adam step (bias-correction step index `step` >= 1, shared by the table) for n tensors.
-// Every pointer must be 16-byte aligned (PyTorch allocations are).
+// Entries whose pointers are all 16-byte aligned take 16-byte vector loads, others scalar ones.
 MAUV_API int mauv_adam_step(const MauvAdamEntry* table, int n, float lr, float beta1,
                             float beta2, float eps, float weight_decay, long long step,
                             hipStream_t stream) {

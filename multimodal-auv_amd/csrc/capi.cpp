@@ -23,4 +23,4 @@ int check_launch(const char* what) {
 MAUV_API const char* mauv_last_error(void) { return mauv::g_last_error.c_str(); }
 
 // ABI version of include/mauv.h this library implements.
-MAUV_API int mauv_abi_version(void) { return 2; }
+MAUV_API int mauv_abi_version(void) { return 3; }

@@ -16,76 +16,83 @@ using namespace mauv;
 
 namespace mauv {
 
-constexpr int HID = 128;
-
+// qkv rows are [q | k | v], each `hid` wide (the reference model: hid = 128, d_model 2048)
 __global__ __launch_bounds__(256) void attn_t_kernel(const float* __restrict__ qkv, int rows,
-                                                     float* __restrict__ t) {
-  const long long total = (long long)rows * HID;
+                                                     int hid, float* __restrict__ t) {
+  const long long total = (long long)rows * hid;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const long long r = i / HID;
-    const int j = (int)(i - r * HID);
-    t[i] = tanhf(qkv[r * 3 * HID + j] + qkv[r * 3 * HID + HID + j]);
+    const long long r = i / hid;
+    const int j = (int)(i - r * hid);
+    t[i] = tanhf(qkv[r * 3 * hid + j] + qkv[r * 3 * hid + hid + j]);
   }
 }
 
 __global__ __launch_bounds__(256) void attn_t_bwd_kernel(const float* __restrict__ dt,
                                                          const float* __restrict__ t, int rows,
-                                                         float* __restrict__ dqkv) {
-  const long long total = (long long)rows * HID;
+                                                         int hid, float* __restrict__ dqkv) {
+  const long long total = (long long)rows * hid;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const long long r = i / HID;
-    const int j = (int)(i - r * HID);
+    const long long r = i / hid;
+    const int j = (int)(i - r * hid);
     const float tv = t[i];
     const float d = dt[i] * (1.0f - tv * tv);
-    dqkv[r * 3 * HID + j] = d;
-    dqkv[r * 3 * HID + HID + j] = d;
+    dqkv[r * 3 * hid + j] = d;
+    dqkv[r * 3 * hid + hid + j] = d;
   }
 }
 
-// one wave per row; lane owns columns lane and lane+64
-__global__ __launch_bounds__(256) void attn_out_kernel(const float* __restrict__ qkv,
-                                                       const float* __restrict__ s, int rows,
-                                                       float* __restrict__ comb, int comb_ld,
-                                                       int comb_off) {
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (r >= rows) return;
-  const float s0 = s[(long long)r * HID + lane], s1 = s[(long long)r * HID + lane + 64];
-  float m = fmaxf(s0, s1);
+// softmax over the hidden dim of one row, one wave per row (lane j covers j, j+64, ...):
+// returns the row max and 1 / sum exp(s - max)
+__device__ __forceinline__ void row_softmax_norm(const float* __restrict__ s, int hid, int lane,
+                                                 float& m, float& inv) {
+  m = -INFINITY;
+  for (int j = lane; j < hid; j += 64) m = fmaxf(m, s[j]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  const float e0 = expf(s0 - m), e1 = expf(s1 - m);
-  const float inv = 1.0f / wave_sum(e0 + e1);
-  const float* v = qkv + (long long)r * 3 * HID + 2 * HID;
+  float e = 0.f;
+  for (int j = lane; j < hid; j += 64) e += expf(s[j] - m);
+  inv = 1.0f / wave_sum(e);
+}
+
+__global__ __launch_bounds__(256) void attn_out_kernel(const float* __restrict__ qkv,
+                                                       const float* __restrict__ s, int rows,
+                                                       int hid, float* __restrict__ comb,
+                                                       int comb_ld, int comb_off) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float* sr = s + (long long)r * hid;
+  float m, inv;
+  row_softmax_norm(sr, hid, lane, m, inv);
+  const float* v = qkv + (long long)r * 3 * hid + 2 * hid;
   float* o = comb + (long long)r * comb_ld + comb_off;
-  o[lane] = v[lane] * (e0 * inv);
-  o[lane + 64] = v[lane + 64] * (e1 * inv);
+  for (int j = lane; j < hid; j += 64) o[j] = v[j] * (expf(sr[j] - m) * inv);
 }
 
 __global__ __launch_bounds__(256) void attn_out_bwd_kernel(const float* __restrict__ dcomb,
                                                            int comb_ld, int comb_off,
                                                            const float* __restrict__ qkv,
                                                            const float* __restrict__ s, int rows,
-                                                           float* __restrict__ dqkv,
+                                                           int hid, float* __restrict__ dqkv,
                                                            float* __restrict__ ds) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= rows) return;
-  const float s0 = s[(long long)r * HID + lane], s1 = s[(long long)r * HID + lane + 64];
-  float m = fmaxf(s0, s1);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  const float e0 = expf(s0 - m), e1 = expf(s1 - m);
-  const float inv = 1.0f / wave_sum(e0 + e1);
-  const float a0 = e0 * inv, a1 = e1 * inv;
-  const float* v = qkv + (long long)r * 3 * HID + 2 * HID;
+  const float* sr = s + (long long)r * hid;
+  float m, inv;
+  row_softmax_norm(sr, hid, lane, m, inv);
+  const float* v = qkv + (long long)r * 3 * hid + 2 * hid;
   const float* d = dcomb + (long long)r * comb_ld + comb_off;
-  const float d0 = d[lane], d1 = d[lane + 64];
-  float* dv = dqkv + (long long)r * 3 * HID + 2 * HID;
-  dv[lane] = d0 * a0;
-  dv[lane + 64] = d1 * a1;
-  const float da0 = d0 * v[lane], da1 = d1 * v[lane + 64];
-  const float dot = wave_sum(a0 * da0 + a1 * da1);
-  ds[(long long)r * HID + lane] = a0 * (da0 - dot);
-  ds[(long long)r * HID + lane + 64] = a1 * (da1 - dot);
+  float* dv = dqkv + (long long)r * 3 * hid + 2 * hid;
+  float dot = 0.f;
+  for (int j = lane; j < hid; j += 64) {
+    const float a = expf(sr[j] - m) * inv;
+    dv[j] = d[j] * a;
+    dot += a * d[j] * v[j];
+  }
+  dot = wave_sum(dot);
+  for (int j = lane; j < hid; j += 64) {
+    const float a = expf(sr[j] - m) * inv;
+    ds[(long long)r * hid + j] = a * (d[j] * v[j] - dot);
+  }
 }
 
 // out[g][n] (+)= sum_rows dy[g][row][n]
@@ -242,24 +249,39 @@ static int grid1(long long n, int cap = 4096) {
 
 }  // namespace mauv
 
-MAUV_API int mauv_attn_t(const float* qkv, int rows, float* t, hipStream_t stream) {
-  hipLaunchKernelGGL(attn_t_kernel, dim3(grid1((long long)rows * HID)), dim3(256), 0, stream, qkv, rows, t);
+static bool attn_args_ok(int rows, int hid) {
+  if (rows < 0 || hid < 1) {
+    set_error("attn: rows must be >= 0 and hid >= 1");
+    return false;
+  }
+  return true;
+}
+MAUV_API int mauv_attn_t(const float* qkv, int rows, int hid, float* t, hipStream_t stream) {
+  if (!attn_args_ok(rows, hid)) return -1;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(attn_t_kernel, dim3(grid1((long long)rows * hid)), dim3(256), 0, stream, qkv, rows, hid, t);
   return check_launch("attn_t");
 }
-MAUV_API int mauv_attn_t_bwd(const float* dt, const float* t, int rows, float* dqkv,
+MAUV_API int mauv_attn_t_bwd(const float* dt, const float* t, int rows, int hid, float* dqkv,
                              hipStream_t stream) {
-  hipLaunchKernelGGL(attn_t_bwd_kernel, dim3(grid1((long long)rows * HID)), dim3(256), 0, stream, dt, t, rows, dqkv);
+  if (!attn_args_ok(rows, hid)) return -1;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(attn_t_bwd_kernel, dim3(grid1((long long)rows * hid)), dim3(256), 0, stream, dt, t, rows, hid, dqkv);
   return check_launch("attn_t_bwd");
 }
-MAUV_API int mauv_attn_out(const float* qkv, const float* s, int rows, float* comb, int comb_ld,
-                           int comb_off, hipStream_t stream) {
-  hipLaunchKernelGGL(attn_out_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, qkv, s, rows, comb, comb_ld, comb_off);
+MAUV_API int mauv_attn_out(const float* qkv, const float* s, int rows, int hid, float* comb,
+                           int comb_ld, int comb_off, hipStream_t stream) {
+  if (!attn_args_ok(rows, hid)) return -1;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(attn_out_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, qkv, s, rows, hid, comb, comb_ld, comb_off);
   return check_launch("attn_out");
 }
 MAUV_API int mauv_attn_out_bwd(const float* dcomb, int comb_ld, int comb_off, const float* qkv,
-                               const float* s, int rows, float* dqkv, float* ds,
+                               const float* s, int rows, int hid, float* dqkv, float* ds,
                                hipStream_t stream) {
-  hipLaunchKernelGGL(attn_out_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, dcomb, comb_ld, comb_off, qkv, s, rows, dqkv, ds);
+  if (!attn_args_ok(rows, hid)) return -1;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(attn_out_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, dcomb, comb_ld, comb_off, qkv, s, rows, hid, dqkv, ds);
   return check_launch("attn_out_bwd");
 }
 MAUV_API int mauv_colsum(const float* dy, int G, int rows, int N, float* out, int accumulate,

@@ -73,10 +73,10 @@ SIGNATURES = {
     "mauv_pack_nchw_h16": [I, P, I, I, I, I, I, P, P],
     "mauv_pack_nchw_f32": [P, I, I, I, I, I, P, P],
     # head.hip
-    "mauv_attn_t": [P, I, P, P],
-    "mauv_attn_t_bwd": [P, P, I, P, P],
-    "mauv_attn_out": [P, P, I, P, I, I, P],
-    "mauv_attn_out_bwd": [P, I, I, P, P, I, P, P, P],
+    "mauv_attn_t": [P, I, I, P, P],
+    "mauv_attn_t_bwd": [P, P, I, I, P, P],
+    "mauv_attn_out": [P, P, I, I, P, I, I, P],
+    "mauv_attn_out_bwd": [P, I, I, P, P, I, I, P, P, P],
     "mauv_colsum": [P, I, I, I, P, I, P],
     "mauv_mc_mean_ce": [P, P, I, I, I, P, P, P, P],
     "mauv_mc_mean_bwd": [P, P, P, P, I, I, I, P, P],

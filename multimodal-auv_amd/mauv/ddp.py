@@ -6,8 +6,16 @@ The reference replicates every parameter and buffer to every GPU inside every fo
 gradients in backward.  Here each rank owns a full model, runs its own minibatch shard with
 its own Philox epsilon stream (as each DataParallel replica samples its own epsilons) and its
 own BN batch statistics (as each replica normalises its own chunk), and gradients meet in
-ONE bucketed all-reduce of the flat gradient arena per step (146.8 M fp32 = 587 MB) over
-xGMI.  Parameters are broadcast from rank 0 once at wrap time.
+bucketed all-reduces of the flat gradient arena (146.8 M fp32 = 587 MB per step) over xGMI.
+Parameters are broadcast from rank 0 once at wrap time.
+
+Overlap: the three ResNet-50 trunks run their backward on streams of their own and own
+contiguous slices of the arena (~47 M floats each).  When a trunk's backward has written its
+last gradient, the engine calls ``grad_ready_hook`` on that trunk's stream and its slice
+all-reduces (async, 64 MB buckets) while the other trunks are still in backward; the fusion
+head's slice and any trunk that finished before the KL backward (which writes every slice)
+go in ``allreduce_grads`` after the backward.  The order of collectives is the autograd
+order of the trunk nodes, identical on every rank.
 
 ``DistributedMC`` deliberately does not subclass DistributedDataParallel: the reference's
 loops special-case DDP by calling ``model.module(...)`` (train/multimodal.py:109-110), which
@@ -23,25 +31,73 @@ from .engine import root_state
 class DistributedMC(nn.Module):
     _mauv_wrapper = True
 
-    def __init__(self, module, group=None, bucket_bytes=64 << 20):
+    def __init__(self, module, group=None, bucket_bytes=64 << 20, overlap=True):
         super().__init__()
         self.module = module
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.bucket_elems = max(1, bucket_bytes // 4)
+        self.overlap = overlap
         with torch.no_grad():
             for t in list(module.parameters()) + list(module.buffers()):
                 dist.broadcast(t.data, src=dist.get_global_rank(group, 0) if group else 0,
                                group=group)
         st = root_state(module)
         st.seed = (st.seed + 0x9E3779B97F4A7C15 * (self.rank + 1)) % (1 << 62)
+        self._pending = []      # async works of the trunk slices issued during backward
+        self._done = []         # [start, end) arena ranges they cover
+        self._kl_mark = 0
+        if overlap and self.world > 1:
+            st.grad_ready_hook = self._trunk_ready
 
+    # ---- forward: the model's, unchanged ----
     def forward(self, *args, **kw):
+        self._begin_step()
         return self.module(*args, **kw)
 
     def mc_forward(self, *args, **kw):
+        self._begin_step()
         return self.module.mc_forward(*args, **kw)
+
+    def _begin_step(self):
+        if torch.is_grad_enabled():
+            self._kl_mark = root_state(self.module).kl_bwd_count
+
+    # ---- gradient exchange ----
+    def _slice_of(self, trunk):
+        """[start, end) of ``trunk``'s parameters in the flat arena (contiguous by the
+        parameter order of the model), or None."""
+        st = root_state(self.module)
+        arena = st.arena
+        ids = {id(p) for p in trunk.parameters() if p.requires_grad}
+        idx = [i for i, p in enumerate(arena.params) if id(p) in ids]
+        if not idx or idx != list(range(idx[0], idx[-1] + 1)):
+            return None
+        start = arena.offsets[idx[0]]
+        end = arena.offsets[idx[-1] + 1] if idx[-1] + 1 < len(arena.offsets) else arena.numel
+        return start, end
+
+    def _allreduce_range(self, flat, start, end, async_op):
+        works = []
+        for off in range(start, end, self.bucket_elems):
+            w = dist.all_reduce(flat[off:min(end, off + self.bucket_elems)], group=self.group,
+                                async_op=async_op)
+            if async_op:
+                works.append(w)
+        return works
+
+    def _trunk_ready(self, trunk):
+        """Engine hook (trunk stream current): all-reduce this trunk's arena slice now, unless
+        the KL backward — which adds into every slice — has not been issued yet this step."""
+        st = root_state(self.module)
+        if st.kl_bwd_count <= self._kl_mark:   # the loops always add get_kl_loss (:114)
+            return
+        rng = self._slice_of(trunk)
+        if rng is None:
+            return
+        self._pending += self._allreduce_range(st.arena.flat, *rng, async_op=True)
+        self._done.append(rng)
 
     def all_ranks(self, flag):
         """Logical AND of a per-rank decision over the group (one tiny all-reduce): the
@@ -55,14 +111,28 @@ class DistributedMC(nn.Module):
         return bool(t.item())
 
     def allreduce_grads(self):
-        """Average the flat gradient arena across ranks (bucketed RCCL all-reduce)."""
+        """Average the flat gradient arena across ranks: wait for the trunk slices issued
+        during backward, all-reduce the rest in buckets, scale by 1/world."""
         st = root_state(self.module)
-        if st.arena is None or self.world == 1:
+        if self.world == 1:
+            self._pending, self._done = [], []
+            return
+        if st.arena is None:   # a foreign module (no engine arena): reduce its p.grad tensors
+            for p in self.module.parameters():
+                if p.grad is not None:
+                    dist.all_reduce(p.grad, group=self.group)
+                    p.grad.mul_(1.0 / self.world)
             return
         flat = st.arena.flat
-        n = flat.numel()
-        for off in range(0, n, self.bucket_elems):
-            dist.all_reduce(flat[off:off + self.bucket_elems], group=self.group)
+        for w in self._pending:
+            w.wait()
+        done = sorted(self._done)
+        self._pending, self._done = [], []
+        cur = 0
+        for a, b in done + [(flat.numel(), flat.numel())]:
+            if cur < a:
+                self._allreduce_range(flat, cur, a, async_op=False)
+            cur = max(cur, b)
         flat.mul_(1.0 / self.world)
 
     def state_dict(self, *a, **k):

@@ -63,16 +63,22 @@ def _trunk_streams(dev):
 
 # ----------------------------------------------------------------------------- root state
 class GradArena:
-    """Flat fp32 gradient buffer; every ``p.grad`` is a view into it."""
+    """Flat fp32 gradient buffer; every ``p.grad`` is a view into it.  Each view starts on a
+    16-byte boundary (offsets rounded up to 4 floats; the gaps stay zero), as the fused Adam's
+    and the NaN scan's 16-byte vector loads require."""
+
+    ALIGN = 4
 
     def __init__(self, params, device):
         self.params = [p for p in params if p.requires_grad]
-        self.numel = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(self.numel, device=device)
-        self.views, off = [], 0
+        offs, off = [], 0
         for p in self.params:
-            self.views.append(self.flat[off:off + p.numel()].view_as(p))
-            off += p.numel()
+            offs.append(off)
+            off += (p.numel() + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        self.numel = off
+        self.flat = torch.zeros(self.numel, device=device)
+        self.views = [self.flat[o:o + p.numel()].view_as(p) for p, o in zip(self.params, offs)]
+        self.offsets = offs
 
     def ensure(self):
         ptrs_none = [p.grad is None for p in self.params]
@@ -111,6 +117,12 @@ class RootState:
         # trunk activation/weight storage: None = follow torch.autocast (the reference's
         # predictor runs under torch.amp.autocast, inference/predictors.py:55), else a dtype
         self.precision = None
+        # data-parallel hooks (mauv.ddp.DistributedMC): called with a trunk module when that
+        # trunk's backward has written its last gradient (on the trunk's stream), so its
+        # slice of the arena can be all-reduced while the other trunks still run backward;
+        # kl_bwd_count counts issued KL backwards (they write into every trunk's slice)
+        self.grad_ready_hook = None
+        self.kl_bwd_count = 0
 
     def trunk_dtype(self):
         if self.precision is not None:
@@ -248,6 +260,69 @@ class _Runner:
         dx = torch.empty(G, rows, K, device=dy.device)
         ops.conv2d_bwd_data(dy, w, dx, G, rows, 1, 1, K, N, 1, 1, 0)
         return dx
+
+
+    # ---- AdditiveAttention (base_models.py:43-52): q|k|v as ONE GEMM over [Wq;Wk;Wv] ----
+    @staticmethod
+    def _att_dims(att):
+        return att.query_projection.in_features, att.query_projection.out_features
+
+    def _qkv(self, att, f, rows):
+        G, dev = self.G, f.device
+        D, Hd = self._att_dims(att)
+        w = torch.empty(G, 3 * Hd, D, device=dev)
+        b = torch.empty(G, 3 * Hd, device=dev)
+        for j, lin in enumerate((att.query_projection, att.key_projection,
+                                 att.value_projection)):
+            self._sample(lin, lin.mu_weight, lin.rho_weight, "weight",
+                         w.view(G, -1)[:, j * Hd * D:], Hd, D, 1, out_gstride=3 * Hd * D)
+            self._sample(lin, lin.mu_bias, lin.rho_bias, "bias", b[:, j * Hd:], Hd, 1, 1,
+                         bias=True, out_gstride=3 * Hd)
+        qkv = torch.empty(G, rows, 3 * Hd, device=dev)
+        ops.conv2d_fwd(f, w, qkv, G, rows, 1, 1, D, 3 * Hd, 1, 1, 0, bias=b)
+        return qkv, w
+
+    def _qkv_bwd(self, att, f, w, dqkv, rows, need_df=True):
+        G, dev = self.G, dqkv.device
+        D, Hd = self._att_dims(att)
+        lins = (att.query_projection, att.key_projection, att.value_projection)
+        if any(l.mu_weight.requires_grad for l in lins):
+            splits = ops.wgrad_splits(G, rows, 1, 1, D, 3 * Hd, 1, 1, 0)
+            ws = torch.empty(splits, G, 3 * Hd, D, device=dev)
+            ops.conv2d_bwd_weight(f, dqkv, ws, splits, G, rows, 1, 1, D, 3 * Hd, 1, 1, 0)
+            db = torch.empty(G, 3 * Hd, device=dev)
+            ops.colsum(dqkv, G, rows, 3 * Hd, db)
+            for j, lin in enumerate(lins):
+                self._reparam_bwd(lin, lin.mu_weight, lin.rho_weight,
+                                  ws.view(splits, G, -1)[:, :, j * Hd * D:], splits, Hd, D, 1,
+                                  "weight", dw_gstride=3 * Hd * D, dw_sstride=G * 3 * Hd * D)
+                self._reparam_bwd(lin, lin.mu_bias, lin.rho_bias, db[:, j * Hd:], 1, Hd, 1, 1,
+                                  "bias", bias=True, dw_gstride=3 * Hd)
+        if not need_df:
+            return None
+        df = torch.empty(G, rows, D, device=dev)
+        ops.conv2d_bwd_data(dqkv, w, df, G, rows, 1, 1, D, 3 * Hd, 1, 1, 0)
+        return df
+
+    def _attention(self, att, f, rows, out, ld, off):
+        """o = v * softmax(Wm tanh(q + k) + bm) into out[:, :, off:off+Hd] (row stride ld)."""
+        Hd = self._att_dims(att)[1]
+        qkv, wqkv = self._qkv(att, f, rows)
+        t = torch.empty(self.G, rows, Hd, device=f.device)
+        ops.attn_t(qkv, self.G * rows, Hd, t)
+        s, rm_ = self._linear(att.attention_mechanism, t, rows)
+        ops.attn_out(qkv, s, self.G * rows, Hd, out, ld, off)
+        return (att, f, wqkv, qkv, t, s, rm_) if self.save else None
+
+    def _attention_bwd(self, rec, dout, ld, off, rows, need_df=True):
+        att, f, wqkv, qkv, t, s, rm_ = rec
+        Hd = self._att_dims(att)[1]
+        dqkv = torch.empty_like(qkv)
+        ds = torch.empty_like(s)
+        ops.attn_out_bwd(dout, ld, off, qkv, s, self.G * rows, Hd, dqkv, ds)
+        dt = self._linear_bwd(rm_, ds)
+        ops.attn_t_bwd(dt, t, self.G * rows, Hd, dqkv)
+        return self._qkv_bwd(att, f, wqkv, dqkv, rows, need_df)
 
 
 # ----------------------------------------------------------------------------- trunk
@@ -537,6 +612,8 @@ class TrunkRunner(_Runner):
         self._conv_bwd(rc, dy0, need_dx=False)
         if self.side is not None:
             torch.cuda.current_stream().wait_stream(self.side)
+        if self.st.grad_ready_hook is not None:
+            self.st.grad_ready_hook(self.trunk)
         if self.join is not None:   # the caller's stream (optimizer, all-reduce) waits for us
             ev = torch.cuda.Event()
             ev.record()
@@ -552,62 +629,26 @@ class HeadRunner(_Runner):
         super().__init__(state, G, sample0, save)
         self.m = model
 
-    def _qkv(self, att, f, rows):
-        G, dev = self.G, f.device
-        w = torch.empty(G, 384, 2048, device=dev)
-        b = torch.empty(G, 384, device=dev)
-        for j, lin in enumerate((att.query_projection, att.key_projection,
-                                 att.value_projection)):
-            self._sample(lin, lin.mu_weight, lin.rho_weight, "weight",
-                         w.view(G, -1)[:, j * 128 * 2048:], 128, 2048, 1,
-                         out_gstride=384 * 2048)
-            self._sample(lin, lin.mu_bias, lin.rho_bias, "bias", b[:, j * 128:], 128, 1, 1,
-                         bias=True, out_gstride=384)
-        qkv = torch.empty(G, rows, 384, device=dev)
-        ops.conv2d_fwd(f, w, qkv, G, rows, 1, 1, 2048, 384, 1, 1, 0, bias=b)
-        return qkv, w
-
-    def _qkv_bwd(self, att, f, w, dqkv, rows):
-        G, dev = self.G, dqkv.device
-        lins = (att.query_projection, att.key_projection, att.value_projection)
-        if any(l.mu_weight.requires_grad for l in lins):
-            splits = ops.wgrad_splits(G, rows, 1, 1, 2048, 384, 1, 1, 0)
-            ws = torch.empty(splits, G, 384, 2048, device=dev)
-            ops.conv2d_bwd_weight(f, dqkv, ws, splits, G, rows, 1, 1, 2048, 384, 1, 1, 0)
-            db = torch.empty(G, 384, device=dev)
-            ops.colsum(dqkv, G, rows, 384, db)
-            for j, lin in enumerate(lins):
-                self._reparam_bwd(lin, lin.mu_weight, lin.rho_weight,
-                                  ws.view(splits, G, -1)[:, :, j * 128 * 2048:], splits, 128,
-                                  2048, 1, "weight", dw_gstride=384 * 2048,
-                                  dw_sstride=G * 384 * 2048)
-                self._reparam_bwd(lin, lin.mu_bias, lin.rho_bias, db[:, j * 128:], 1, 128, 1, 1,
-                                  "bias", bias=True, dw_gstride=384)
-        df = torch.empty(G, rows, 2048, device=dev)
-        ops.conv2d_bwd_data(dqkv, w, df, G, rows, 1, 1, 2048, 384, 1, 1, 0)
-        return df
-
     def run_forward(self, f_img, f_bathy, f_sss):
         m, G = self.m, self.G
         rows = f_img.shape[1]
         self.rows = rows
-        comb = torch.empty(G, rows, 384, device=f_img.device)
+        atts = (m.attention_image, m.attention_bathy, m.attention_sss)
+        widths = [self._att_dims(a)[1] for a in atts]
+        ld = sum(widths)
+        comb = torch.empty(G, rows, ld, device=f_img.device)
         self.att_recs = []
-        for j, (att, f) in enumerate(((m.attention_image, f_img), (m.attention_bathy, f_bathy),
-                                      (m.attention_sss, f_sss))):
-            f = f.contiguous()
-            qkv, wqkv = self._qkv(att, f, rows)
-            t = torch.empty(G, rows, 128, device=f.device)
-            ops.attn_t(qkv, G * rows, t)
-            s, rm_ = self._linear(att.attention_mechanism, t, rows)
-            ops.attn_out(qkv, s, G * rows, comb, 384, 128 * j)
-            if self.save:
-                self.att_recs.append((att, f, wqkv, qkv, t, s, rm_))
+        off = 0
+        for att, f, w in zip(atts, (f_img, f_bathy, f_sss), widths):
+            self.att_recs.append((self._attention(att, f.contiguous(), rows, comb, ld, off),
+                                  ld, off))
+            off += w
         h1, self.r_fc = self._linear(m.fc, comb, rows)
         h2, self.r_fc1 = self._linear(m.fc1, h1, rows)
         out, self.r_fc2 = self._linear(m.fc2, h2, rows)
         if not self.save:
             self.r_fc = self.r_fc1 = self.r_fc2 = None
+            self.att_recs = []
         return out
 
     def run_backward(self, dlogits):
@@ -617,16 +658,101 @@ class HeadRunner(_Runner):
         dh1 = self._linear_bwd(self.r_fc1, dh2)
         dcomb = self._linear_bwd(self.r_fc, dh1)
         self.r_fc = self.r_fc1 = self.r_fc2 = None
-        dfs = []
-        for j, (att, f, wqkv, qkv, t, s, rm_) in enumerate(self.att_recs):
-            dqkv = torch.empty_like(qkv)
-            ds = torch.empty_like(s)
-            ops.attn_out_bwd(dcomb, 384, 128 * j, qkv, s, self.G * rows, dqkv, ds)
-            dt = self._linear_bwd(rm_, ds)
-            ops.attn_t_bwd(dt, t, self.G * rows, dqkv)
-            dfs.append(self._qkv_bwd(att, f, wqkv, dqkv, rows))
+        dfs = tuple(self._attention_bwd(rec, dcomb, ld, off, rows)
+                    for rec, ld, off in self.att_recs)
         self.att_recs = []
-        return tuple(dfs)
+        return dfs
+
+
+class AttentionRunner(_Runner):
+    """A standalone AdditiveAttention.forward (base_models.py:43-52) for G samples:
+    [rows, d_model] -> [G, rows, hidden]."""
+
+    def __init__(self, att, state, G, sample0, save):
+        super().__init__(state, G, sample0, save)
+        self.att = att
+
+    def run_forward(self, f):
+        self.shape = f.shape
+        D, Hd = self._att_dims(self.att)
+        if f.shape[-1] != D:
+            raise ValueError(f"AdditiveAttention expects {D} features, got {f.shape[-1]}")
+        rows = f.numel() // D
+        self.rows = rows
+        # every sample reads the same input: expand over the MC groups
+        f3 = f.reshape(1, rows, D).float().expand(self.G, rows, D).contiguous()
+        out = torch.empty(self.G, rows, Hd, device=f.device)
+        self.rec = self._attention(self.att, f3, rows, out, Hd, 0)
+        return out.reshape(self.G, *self.shape[:-1], Hd)
+
+    def run_backward(self, dout):
+        Hd = self._att_dims(self.att)[1]
+        self.st.grads(dout.device)
+        df = self._attention_bwd(self.rec, dout.reshape(self.G, self.rows, Hd).contiguous(),
+                                 Hd, 0, self.rows)
+        self.rec = None
+        return (df.sum(0).reshape(self.shape),)
+
+
+class LayerRunner(_Runner):
+    """A standalone bayesian-torch layer (Conv2dReparameterization /
+    LinearReparameterization.forward: w = mu + softplus(rho) eps, then F.conv2d / F.linear)
+    for one MC sample, with its backward (dx, dmu, drho) — for layers called outside the
+    compiled trunk / head schedules.  fp32, NCHW / [..., in_features] like the reference."""
+
+    def __init__(self, layer, state, sample0, save):
+        super().__init__(state, 1, sample0, save)
+        self.m = layer
+
+    def run_forward(self, x):
+        m = self.m
+        self.shape = x.shape
+        if isinstance(m, LinearReparameterization):
+            rows = x.numel() // m.in_features
+            x3 = x.reshape(1, rows, m.in_features).float().contiguous()
+            y, self.rec = self._linear(m, x3, rows)
+            return y.reshape(*x.shape[:-1], m.out_features)
+        B, C, H, W = x.shape
+        x = x.float().contiguous()
+        k, st, pd = m.kernel_size, m.stride[0], m.padding[0]
+        w = torch.empty(1, m.out_channels, k, k, C, device=x.device)
+        self._sample(m, m.mu_kernel, m.rho_kernel, "kernel", w, m.out_channels, C, k * k)
+        bias = None
+        if m.mu_bias is not None:
+            bias = torch.empty(1, m.out_channels, device=x.device)
+            self._sample(m, m.mu_bias, m.rho_bias, "bias", bias, m.out_channels, 1, 1, bias=True)
+        Ho, Wo = ops.out_hw(H, k, st, pd), ops.out_hw(W, k, st, pd)
+        y = torch.empty(1, B, Ho, Wo, m.out_channels, device=x.device)
+        xs = (0, C * H * W, W, 1, H * W)   # the NCHW input read in place
+        ops.conv2d_fwd(x, w, y, 1, B, H, W, C, m.out_channels, k, st, pd, bias=bias,
+                       x_strides=xs)
+        self.rec = (x, xs, w, (B, C, H, W, Ho, Wo)) if self.save else None
+        return y[0].permute(0, 3, 1, 2)
+
+    def run_backward(self, dy):
+        m = self.m
+        self.st.grads(dy.device)
+        if isinstance(m, LinearReparameterization):
+            dx = self._linear_bwd(self.rec, dy.reshape(1, -1, m.out_features).contiguous())
+            self.rec = None
+            return (dx.reshape(self.shape),)
+        x, xs, w, (B, C, H, W, Ho, Wo) = self.rec
+        self.rec = None
+        k, st, pd, Co = m.kernel_size, m.stride[0], m.padding[0], m.out_channels
+        dyh = dy.permute(0, 2, 3, 1).contiguous().float()   # NCHW grad -> NHWC
+        if m.mu_kernel.requires_grad:
+            splits = ops.wgrad_splits(1, B, H, W, C, Co, k, st, pd)
+            ws = torch.empty(splits, 1, Co, k * k * C, device=dy.device)
+            ops.conv2d_bwd_weight(x, dyh, ws, splits, 1, B, H, W, C, Co, k, st, pd,
+                                  x_strides=xs)
+            self._reparam_bwd(m, m.mu_kernel, m.rho_kernel, ws, splits, Co, C, k * k, "kernel")
+        if m.mu_bias is not None and m.mu_bias.requires_grad:
+            db = torch.empty(1, Co, device=dy.device)
+            ops.colsum(dyh, 1, B * Ho * Wo, Co, db)
+            self._reparam_bwd(m, m.mu_bias, m.rho_bias, db, 1, Co, 1, 1, "bias", bias=True)
+        dx = torch.empty(1, B, H, W, C, device=dy.device)
+        ops.conv2d_bwd_data(dyh, w, dx, 1, B, H, W, C, Co, k, st, pd)
+        return (dx[0].permute(0, 3, 1, 2).contiguous(),)
 
 
 # ----------------------------------------------------------------------------- entry points
@@ -703,3 +829,26 @@ def run_multimodal_mc(model, inputs, bathy, sss, num_mc):
     save = needs_grad(head_params) or any(f.requires_grad for f in (f_img, f_bathy, f_sss))
     runner = HeadRunner(model, st, num_mc, s0, save)
     return _run(runner, head_params, (f_img, f_bathy, f_sss), save)
+
+
+def _standalone(module, runner_cls, x, *extra):
+    st = root_state(module)
+    dev = next(module.parameters()).device
+    if dev.type != "cuda":
+        raise RuntimeError("mauv: the layer must be on a ROCm device (module.to('cuda'))")
+    params = list(module.parameters())
+    save = needs_grad(params) or (torch.is_grad_enabled() and x.requires_grad)
+    runner = runner_cls(module, st, *extra, save)
+    return _run(runner, params, (_to_device(x, dev),), save)
+
+
+def run_attention_mc(att, f, num_mc):
+    """[num_mc, ..., hidden] of a standalone AdditiveAttention for num_mc MC samples."""
+    s0 = root_state(att).next_samples(num_mc)
+    return _standalone(att, AttentionRunner, f, num_mc, s0)
+
+
+def run_layer(layer, x):
+    """One stochastic forward of a standalone Bayesian conv / linear layer (differentiable)."""
+    s0 = root_state(layer).next_samples(1)
+    return _standalone(layer, LayerRunner, x, s0)

@@ -86,6 +86,7 @@ class _KL(torch.autograd.Function):
         st.grads(dev)
         coef = g.reshape(1).float().contiguous()
         ops.kl_bwd(tab.bwd_table(dev), tab.n, coef)
+        st.kl_bwd_count += 1
         return None, None
 
 

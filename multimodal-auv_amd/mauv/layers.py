@@ -3,9 +3,10 @@
 ``Conv2dReparameterization`` / ``LinearReparameterization`` keep the exact parameter names
 and shapes the reference's checkpoints use (``mu_kernel, rho_kernel`` OIHW;
 ``mu_weight, rho_weight, mu_bias, rho_bias``) so ``state_dict`` / ``load_state_dict`` are
-interchangeable with the reference.  They are parameter holders:
-the MC-batched engine (``mauv.engine``) samples and consumes them inside HIP kernels.  A
-layer's own ``forward`` runs one sample through the same kernels (inference only).
+interchangeable with the reference.  Inside the models they are
+parameter holders: the MC-batched engine (``mauv.engine``) samples and consumes them inside
+HIP kernels.  A layer's own ``forward`` runs one sample through the same kernels, with the
+engine's backward (``engine.LayerRunner``).
 
 ``dnn_to_bnn`` mirrors bayesian-torch's MOPED conversion used at
 ``models/model_utils.py:26-28,35`` (mu <- w, rho <- log(expm1(delta*|w|) + 1e-20)).
@@ -15,7 +16,6 @@ import math
 import torch
 import torch.nn as nn
 
-from . import ops
 
 
 def _pair(v):
@@ -80,28 +80,11 @@ class Conv2dReparameterization(_BayesBase):
                 f"stride={self.stride}, padding={self.padding}, bias={self.bias}")
 
     def forward(self, x, return_kl=True):
-        """One MC sample through the HIP conv (NCHW in/out, no autograd; the model engine
-        is the differentiable path)."""
-        if torch.is_grad_enabled() and self.mu_kernel.requires_grad:
-            raise RuntimeError("mauv: standalone Bayesian-layer autograd is not supported; "
-                               "run the enclosing model (engine path)")
-        B, C, H, W = x.shape
-        k, (st, _), (pd, _) = self.kernel_size, self.stride, self.padding
-        x = x.contiguous().float()
-        w = torch.empty(1, self.out_channels, k, k, C, device=x.device)
-        seed, s0 = _standalone_rng(self)
-        ops.reparam_sample(self.mu_kernel, self.rho_kernel, w, 1, seed, s0, 0,
-                           self.out_channels, C, k * k)
-        Ho, Wo = ops.out_hw(H, k, st, pd), ops.out_hw(W, k, st, pd)
-        y = torch.empty(1, B, Ho, Wo, self.out_channels, device=x.device)
-        bias = None
-        if self.mu_bias is not None:
-            bias = torch.empty(1, self.out_channels, device=x.device)
-            ops.reparam_sample(self.mu_bias, self.rho_bias, bias, 1, seed, s0, 1,
-                               self.out_channels, 1, 1)
-        ops.conv2d_fwd(x, w, y, 1, B, H, W, C, self.out_channels, k, st, pd, bias=bias,
-                       x_strides=(0, C * H * W, W, 1, H * W))
-        out = y[0].permute(0, 3, 1, 2)
+        """One MC sample (bayesian-torch Conv2dReparameterization.forward): w = mu +
+        softplus(rho) * eps, F.conv2d — NCHW in / out through the HIP sampler and implicit
+        GEMM, differentiable (dx, dmu, drho by the engine's backward kernels)."""
+        from .engine import run_layer
+        out = run_layer(self, x)
         if return_kl and not self.dnn_to_bnn_flag:
             return out, self.kl_loss()
         return out
@@ -134,37 +117,13 @@ class LinearReparameterization(_BayesBase):
         return f"in_features={self.in_features}, out_features={self.out_features}, bias={self.bias}"
 
     def forward(self, x, return_kl=True):
-        """One MC sample through the HIP GEMM (no autograd; see Conv2dReparameterization)."""
-        if torch.is_grad_enabled() and self.mu_weight.requires_grad:
-            raise RuntimeError("mauv: standalone Bayesian-layer autograd is not supported; "
-                               "run the enclosing model (engine path)")
-        shp = x.shape
-        x = x.reshape(-1, self.in_features).contiguous().float()
-        M = x.shape[0]
-        w = torch.empty(1, self.out_features, self.in_features, device=x.device)
-        seed, s0 = _standalone_rng(self)
-        ops.reparam_sample(self.mu_weight, self.rho_weight, w, 1, seed, s0, 0,
-                           self.out_features, self.in_features, 1)
-        bias = None
-        if self.mu_bias is not None:
-            bias = torch.empty(1, self.out_features, device=x.device)
-            ops.reparam_sample(self.mu_bias, self.rho_bias, bias, 1, seed, s0, 1,
-                               self.out_features, 1, 1)
-        y = torch.empty(1, M, self.out_features, device=x.device)
-        ops.conv2d_fwd(x, w, y, 1, M, 1, 1, self.in_features, self.out_features, 1, 1, 0,
-                       bias=bias)
-        out = y[0].reshape(*shp[:-1], self.out_features)
+        """One MC sample (bayesian-torch LinearReparameterization.forward): w = mu +
+        softplus(rho) * eps, F.linear over the last dim, through the HIP GEMM (differentiable)."""
+        from .engine import run_layer
+        out = run_layer(self, x)
         if return_kl and not self.dnn_to_bnn_flag:
             return out, self.kl_loss()
         return out
-
-
-def _standalone_rng(layer):
-    if not hasattr(layer, "_mauv_seed"):
-        layer._mauv_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        layer._mauv_count = 0
-    layer._mauv_count += 1
-    return layer._mauv_seed, layer._mauv_count
 
 
 def is_bayesian(m):

@@ -51,17 +51,26 @@ class Identity(nn.Module):
 
 
 class AdditiveAttention(nn.Module):
-    """Parameter container; its math runs fused in the head schedule (engine.HeadRunner):
-    q|k|v as one 384-wide GEMM, tanh(q + k), Wm, softmax over the hidden dim, v * a."""
+    """base_models.py:35-52.  Inside MultiModalModel its maths runs fused in the head schedule
+    (engine.HeadRunner); called on its own, ``forward`` runs one stochastic pass through the
+    same kernels: q|k|v as ONE GEMM over [Wq;Wk;Wv], tanh(q + k), Wm, softmax over the
+    hidden dim, v * a (differentiable)."""
 
     def __init__(self, d_model, hidden_dim=128):
         super().__init__()
-        if d_model != 2048 or hidden_dim != 128:
-            raise NotImplementedError("mauv head kernels are specialised for 2048 -> 128")
         self.query_projection = nn.Linear(d_model, hidden_dim)
         self.key_projection = nn.Linear(d_model, hidden_dim)
         self.value_projection = nn.Linear(d_model, hidden_dim)
         self.attention_mechanism = nn.Linear(hidden_dim, hidden_dim)
+
+    def forward(self, query):
+        return self.mc_forward(query, 1)[0]
+
+    def mc_forward(self, query, num_mc):
+        if not is_bayesian(self.query_projection):
+            raise TypeError("AdditiveAttention must be converted with dnn_to_bnn "
+                            "(models/model_utils.py:35) before running")
+        return engine.run_attention_mc(self, query, num_mc)
 
 
 class MultiModalModel(nn.Module):

@@ -412,25 +412,26 @@ def pack_nchw(x, B, C, H, W, Cp, y):
 
 
 # ----------------------------------------------------------------------- head
-def attn_t(qkv, rows, t):
+def attn_t(qkv, rows, hid, t):
     _dev(torch.float32, qkv, t)
-    check(lib.mauv_attn_t(_p(qkv), rows, _p(t), stream()), "attn_t")
+    check(lib.mauv_attn_t(_p(qkv), rows, hid, _p(t), stream()), "attn_t")
 
 
-def attn_t_bwd(dt, t, rows, dqkv):
+def attn_t_bwd(dt, t, rows, hid, dqkv):
     _dev(torch.float32, dt, t, dqkv)
-    check(lib.mauv_attn_t_bwd(_p(dt), _p(t), rows, _p(dqkv), stream()), "attn_t_bwd")
+    check(lib.mauv_attn_t_bwd(_p(dt), _p(t), rows, hid, _p(dqkv), stream()), "attn_t_bwd")
 
 
-def attn_out(qkv, s, rows, comb, ld, off):
+def attn_out(qkv, s, rows, hid, comb, ld, off):
     _dev(torch.float32, qkv, s, comb)
-    check(lib.mauv_attn_out(_p(qkv), _p(s), rows, _p(comb), ld, off, stream()), "attn_out")
+    check(lib.mauv_attn_out(_p(qkv), _p(s), rows, hid, _p(comb), ld, off, stream()),
+          "attn_out")
 
 
-def attn_out_bwd(dcomb, ld, off, qkv, s, rows, dqkv, ds):
+def attn_out_bwd(dcomb, ld, off, qkv, s, rows, hid, dqkv, ds):
     _dev(torch.float32, dcomb, qkv, s, dqkv, ds)
-    check(lib.mauv_attn_out_bwd(_p(dcomb), ld, off, _p(qkv), _p(s), rows, _p(dqkv), _p(ds),
-                                stream()), "attn_out_bwd")
+    check(lib.mauv_attn_out_bwd(_p(dcomb), ld, off, _p(qkv), _p(s), rows, hid, _p(dqkv),
+                                _p(ds), stream()), "attn_out_bwd")
 
 
 def colsum(dy, G, rows, N, out, accumulate=False):

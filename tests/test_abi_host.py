@@ -49,7 +49,7 @@ def test_library_reports_gfx950_only():
 
 def test_abi_version_and_error_string():
     from mauv._lib import lib
-    assert lib.mauv_abi_version() == 2
+    assert lib.mauv_abi_version() == 3
     assert isinstance(lib.mauv_last_error(), bytes)
 
 

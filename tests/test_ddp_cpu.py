@@ -61,7 +61,7 @@ def test_distributed_mc_allreduce_and_broadcast(tmp_path):
         assert torch.equal(a, b)
         assert torch.allclose(a, torch.full_like(a, 1.5 * (i + 1)))  # mean of (1, 2) x (i+1)
     assert s0 != s1  # per-rank Philox streams (each replica samples its own epsilons)
-    assert n0 == n1 == 5 * 7 + 7 + 7 * 3 + 3
+    assert n0 == n1 == 36 + 8 + 24 + 4   # 5*7, 7, 7*3, 3 floats, each view padded to 4
 
 
 def _stats_worker(rank, world, port, q):
@@ -99,3 +99,97 @@ def test_mc_sharded_statistics_equal_single_process(tmp_path):
     np.testing.assert_allclose(alea.numpy(),
                                torch.mean(-torch.sum(P * torch.log(P + 1e-7), -1), 0).numpy(),
                                atol=1e-12)
+
+
+def _arena_worker(rank, world, port, q):
+    """The tri-modal model's real arena (696 tensors, 146.8 M floats) on CPU: the trunk
+    slices all-reduce from the engine's per-trunk hook (the first one before the KL backward
+    has been issued, so it is deferred), the rest in allreduce_grads."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "multimodal-auv_amd")]
+    _init(rank, world, port)
+    torch.set_num_threads(2)
+    from mauv.models import define_models, DEFAULT_PRIOR
+    from mauv.ddp import DistributedMC
+    from mauv.engine import root_state
+    torch.manual_seed(rank)
+    model = define_models(None, 7, DEFAULT_PRIOR)["multimodal_model"]
+    ddp = DistributedMC(model)
+    st = root_state(model)
+    arena = st.grads(torch.device("cpu"))
+    assert len(arena.params) == 696 and all(o % 4 == 0 for o in arena.offsets)
+    for i, p in enumerate(model.parameters()):
+        p.grad.fill_(float(rank + 1) * (i % 7 + 1))
+    with torch.enable_grad():
+        ddp._begin_step()
+    trunks = (model.image_model_feat, model.bathy_model_feat, model.sss_model_feat)
+    st.grad_ready_hook(trunks[0])          # before the KL backward: deferred
+    st.kl_bwd_count += 1                   # (what mauv.kl's backward does)
+    st.grad_ready_hook(trunks[1])
+    st.grad_ready_hook(trunks[2])
+    early = sorted(ddp._done)
+    ddp.allreduce_grads()
+    ok = all(torch.all(p.grad == 1.5 * (i % 7 + 1)).item()
+             for i, p in enumerate(model.parameters()))
+    head = sum(p.numel() for n, p in model.named_parameters()
+               if not n.split(".")[0].endswith("_feat"))
+    p0 = model.fc2.mu_weight.detach().clone()
+    torch.save((ok, early, arena.numel, head, p0), os.path.join(q, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_trimodal_arena_per_trunk_allreduce(tmp_path):
+    res = _run(_arena_worker, tmp_path)
+    for ok, early, numel, head, _ in res:
+        assert ok
+        assert len(early) == 2          # bathy and sss slices overlapped; image deferred
+        for a, b in early:
+            assert b - a >= 23_000_000 * 2   # one trunk's mu + rho
+        assert early[0][1] <= early[1][0]
+    assert torch.equal(res[0][4], res[1][4])   # rank 0's parameters broadcast
+
+
+def _nan_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "multimodal-auv_amd")]
+    _init(rank, world, port)
+    from mauv.ddp import DistributedMC
+    from mauv.train import mc_train_step
+    torch.manual_seed(0)
+
+    class Tri(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.f = torch.nn.Linear(12, 3)
+
+        def forward(self, x, b, s):
+            return self.f(torch.cat([x, b, s], 1))
+    net = Tri()
+    ddp = DistributedMC(net)
+    opt = torch.optim.SGD(net.parameters(), lr=0.1)
+    x = torch.randn(4, 4)
+    if rank == 1:
+        x[0, 0] = float("nan")          # only rank 1 sees a non-finite loss
+    before = [p.detach().clone() for p in net.parameters()]
+    r1 = mc_train_step(ddp, (x, torch.randn(4, 4), torch.randn(4, 4)), torch.tensor([0, 1, 2, 0]),
+                       torch.nn.CrossEntropyLoss(), opt, 2, 4, 0.5)
+    same = all(torch.equal(a, b) for a, b in zip(before, net.parameters()))
+    x2 = torch.full((4, 4), float(rank + 1))   # finite everywhere: both step, grads averaged
+    r2 = mc_train_step(ddp, (x2, torch.zeros(4, 4), torch.zeros(4, 4)), torch.tensor([0, 1, 2, 0]),
+                       torch.nn.CrossEntropyLoss(), opt, 2, 4, 0.5)
+    params = [p.detach().clone() for p in net.parameters()]
+    torch.save((r1 is None, same, r2 is not None and r2["stepped"], params),
+               os.path.join(q, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_nan_loss_on_one_rank_skips_on_all(tmp_path):
+    """A non-finite loss on one rank skips the batch on every rank (no unpaired all-reduce);
+    the next finite batch steps everywhere with averaged gradients (identical parameters)."""
+    res = _run(_nan_worker, tmp_path)
+    for skipped, same, stepped, _ in res:
+        assert skipped and same and stepped
+    for a, b in zip(res[0][3], res[1][3]):
+        assert torch.equal(a, b)

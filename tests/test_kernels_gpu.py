@@ -320,35 +320,38 @@ def test_philox_matches_oracle_restatement():
     assert abs(z.mean()) < 0.05 and abs(z.std() - 1) < 0.05
 
 
-def test_head_kernels():
+@pytest.mark.parametrize("hid", [128, 32, 100, 200])
+def test_head_kernels(hid):
+    """AdditiveAttention epilogues (base_models.py:43-52) at the model's hidden width (128)
+    and at widths that are not / are more than one wave of columns."""
     from mauv import ops
-    rows = 6
+    rows, H = 6, hid
     torch.manual_seed(6)
-    qkv = torch.randn(rows, 384)
-    s = torch.randn(rows, 128)
-    t = torch.empty(rows, 128, device=dev)
-    ops.attn_t(qkv.to(dev), rows, t)
-    close(t, torch.tanh(qkv[:, :128].double() + qkv[:, 128:256].double()))
-    comb = torch.zeros(rows, 384, device=dev)
-    ops.attn_out(qkv.to(dev), s.to(dev), rows, comb, 384, 128)
+    qkv = torch.randn(rows, 3 * H)
+    s = torch.randn(rows, H)
+    t = torch.empty(rows, H, device=dev)
+    ops.attn_t(qkv.to(dev), rows, H, t)
+    close(t, torch.tanh(qkv[:, :H].double() + qkv[:, H:2 * H].double()))
+    comb = torch.zeros(rows, 3 * H, device=dev)
+    ops.attn_out(qkv.to(dev), s.to(dev), rows, H, comb, 3 * H, H)
     sr = s.double().requires_grad_(True)
-    vr = qkv[:, 256:].double().requires_grad_(True)
+    vr = qkv[:, 2 * H:].double().requires_grad_(True)
     o = vr * torch.softmax(sr, 1)
-    close(comb[:, 128:256], o)
-    do = torch.randn(rows, 128)
+    close(comb[:, H:2 * H], o)
+    do = torch.randn(rows, H)
     o.backward(do.double())
-    dcomb = torch.zeros(rows, 384)
-    dcomb[:, 128:256] = do
-    dqkv = torch.zeros(rows, 384, device=dev)
-    ds = torch.empty(rows, 128, device=dev)
-    ops.attn_out_bwd(dcomb.to(dev), 384, 128, qkv.to(dev), s.to(dev), rows, dqkv, ds)
+    dcomb = torch.zeros(rows, 3 * H)
+    dcomb[:, H:2 * H] = do
+    dqkv = torch.zeros(rows, 3 * H, device=dev)
+    ds = torch.empty(rows, H, device=dev)
+    ops.attn_out_bwd(dcomb.to(dev), 3 * H, H, qkv.to(dev), s.to(dev), rows, H, dqkv, ds)
     close(ds, sr.grad)
-    close(dqkv[:, 256:], vr.grad)
-    dt = torch.randn(rows, 128)
-    ops.attn_t_bwd(dt.to(dev), t, rows, dqkv)
-    tt = torch.tanh(qkv[:, :128].double() + qkv[:, 128:256].double())
-    close(dqkv[:, :128], dt.double() * (1 - tt * tt))
-    close(dqkv[:, 128:256], dt.double() * (1 - tt * tt))
+    close(dqkv[:, 2 * H:], vr.grad)
+    dt = torch.randn(rows, H)
+    ops.attn_t_bwd(dt.to(dev), t, rows, H, dqkv)
+    tt = torch.tanh(qkv[:, :H].double() + qkv[:, H:2 * H].double())
+    close(dqkv[:, :H], dt.double() * (1 - tt * tt))
+    close(dqkv[:, H:2 * H], dt.double() * (1 - tt * tt))
 
 
 def test_mc_head_kernels():
