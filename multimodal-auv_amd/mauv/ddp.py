@@ -48,6 +48,7 @@ class DistributedMC(nn.Module):
         self._pending = []      # async works of the trunk slices issued during backward
         self._done = []         # [start, end) arena ranges they cover
         self._kl_mark = 0
+        self.n_overlapped = 0   # trunk slices all-reduced from the backward hook (cumulative)
         if overlap and self.world > 1:
             st.grad_ready_hook = self._trunk_ready
 
@@ -98,6 +99,7 @@ class DistributedMC(nn.Module):
             return
         self._pending += self._allreduce_range(st.arena.flat, *rng, async_op=True)
         self._done.append(rng)
+        self.n_overlapped += 1
 
     def all_ranks(self, flag):
         """Logical AND of a per-rank decision over the group (one tiny all-reduce): the
