@@ -309,6 +309,40 @@ int mauv_mc_finalize(const double* sums, int N, int B, int C, float eps_pred, fl
  * non-finite value) */
 int mauv_nonfinite_count(const float* p, long long n, int* out, hipStream_t stream);
 
+/* ---- input staging (staging.hip) ---------------------------------------------------------
+ * data/datasets.py:239-250 per-tile transforms on the device: uint8 HWC tiles [B][H][W][C] as
+ * PIL decodes them -> fp32 NCHW out = x / 255 (ToTensor), then (out - mean[c]) / std[c]
+ * (Normalize; mean/std nullable = ToTensor only), bit-exact with torchvision's fp32 ops.
+ * uifm_bt (nullable): also apply the underwater image formation model of
+ * Examples/"Example training with image noise.py":55-93 to the result:
+ *   t = exp(-bt[c] * (d * depth)); out = clamp(out * t + binf[c] * (1 - t), 0, 1)
+ * with bt[c] = beta_c * turbidity computed in fp32 as the reference does and d the
+ * [B][1][H][W] distance map (nullable = uniform 1, what the reference passes).
+ * mauv_uifm: the same degradation on fp32 NCHW tiles [B][C][H][W]. */
+int mauv_stage_u8(const unsigned char* x, int B, int H, int W, int C, const float* mean,
+                  const float* stdv, const float* uifm_bt, const float* uifm_binf,
+                  const float* dist, float depth, float* out, hipStream_t stream);
+int mauv_uifm(const float* x, int B, int C, int H, int W, const float* bt, const float* binf,
+              const float* dist, float depth, float* out, hipStream_t stream);
+
+/* ---- evaluation metrics (metrics.hip) ----------------------------------------------------
+ * train/multimodal.py:312-347 (confusion matrix) and Examples/"Example training with image
+ * noise.py":530-634 (uncertainty-error AUROC, macro F1, 15-bin ECE / Emax), accumulated on the
+ * device across an epoch instead of per-batch .cpu() copies:
+ * mauv_confusion_update: counts[y * C + p] += 1 (int32 [C*C + 1]; out-of-range labels or
+ *   predictions counted in counts[C*C]);
+ * mauv_calibration_update: per MC-mean probability row, conf = max, pred = argmax (first
+ *   maximum); the bin b with edges[b] < conf <= edges[b+1] (float64 edges, nbins + 1 of them)
+ *   gets bins[3b] += 1, bins[3b+1] += conf, bins[3b+2] += (pred == label);
+ * mauv_auroc_pairs: count2 += sum over (positive i, negative j) of 2 [s_i > s_j] + [s_i == s_j]
+ *   (AUROC = count2 / (2 n_pos n_neg)). */
+int mauv_confusion_update(const long long* labels, const long long* pred, int n, int C,
+                          int* counts, hipStream_t stream);
+int mauv_calibration_update(const float* probs, const long long* labels, int n, int C,
+                            int nbins, const double* edges, double* bins, hipStream_t stream);
+int mauv_auroc_pairs(const float* score, const unsigned char* positive, int n,
+                     unsigned long long* count2, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -83,6 +83,13 @@ SIGNATURES = {
     "mauv_mc_stats": [P, I, I, I, F, P, I, P],
     "mauv_mc_finalize": [P, I, I, I, F, P, P, P, P, P, P],
     "mauv_nonfinite_count": [P, LL, P, P],
+    # staging.hip
+    "mauv_stage_u8": [P, I, I, I, I, P, P, P, P, P, F, P, P],
+    "mauv_uifm": [P, I, I, I, I, P, P, P, F, P, P],
+    # metrics.hip
+    "mauv_confusion_update": [P, P, I, I, P, P],
+    "mauv_calibration_update": [P, P, I, I, I, P, P, P],
+    "mauv_auroc_pairs": [P, P, I, P, P],
 }
 _RESTYPES = {"mauv_last_error": ctypes.c_char_p, "mauv_bn_workspace_floats": LL,
              "mauv_bn_stats_workspace_floats": LL}

@@ -195,14 +195,14 @@ def train_multimodal_model(multimodal_model, dataloader, criterion, optimizer, e
     return train_loss, train_accuracy
 
 
-def _confusion_png(labels, predicted, csv_path, model_type, epoch):
+def _confusion_png(cm, csv_path, model_type, epoch):
+    """The reference's confusion-matrix PNG (multimodal.py:322-347) from a count matrix."""
     fig = None
     try:
         import matplotlib
         matplotlib.use("Agg")
         import matplotlib.pyplot as plt
-        from sklearn.metrics import confusion_matrix, ConfusionMatrixDisplay
-        cm = confusion_matrix(labels, predicted)
+        from sklearn.metrics import ConfusionMatrixDisplay
         fig, ax = plt.subplots(figsize=(8, 8))
         ConfusionMatrixDisplay(confusion_matrix=cm).plot(cmap="Blues", ax=ax)
         plt.title(f"Confusion Matrix for Epoch {epoch}")
@@ -215,6 +215,50 @@ def _confusion_png(labels, predicted, csv_path, model_type, epoch):
         if fig is not None:
             import matplotlib.pyplot as plt
             plt.close(fig)
+
+
+class _EvalEpoch:
+    """Per-epoch evaluation state with no per-batch device -> host copies: losses, correct
+    counts and uncertainties stay on the device (one copy each at the end, summed in the
+    reference's order), the confusion counts accumulate in mauv.metrics (metrics.hip).  A
+    foreign model's host tensors take the reference's host lists and sklearn."""
+
+    def __init__(self, C):
+        self.C, self.acc = C, None
+        self.losses, self.correct, self.vals = [], [], {}
+        self.labels, self.preds = [], []
+        self.total = 0
+
+    def add(self, loss, labels, predicted, **vals):
+        self.losses.append(loss.detach().reshape(()))
+        self.correct.append((predicted == labels).sum())
+        self.total += labels.size(0)
+        for k, v in vals.items():
+            self.vals.setdefault(k, []).append(v.detach().float().reshape(-1))
+        if labels.is_cuda:
+            if self.acc is None:
+                from .metrics import EvalAccumulator
+                self.acc = EvalAccumulator(self.C, labels.device)
+            self.acc.update(labels, predicted)
+        else:
+            self.labels.append(labels)
+            self.preds.append(predicted)
+
+    def loss_sum(self):
+        return sum(float(v) for v in torch.stack(self.losses).cpu().tolist())
+
+    def correct_count(self):
+        return int(torch.stack(self.correct).sum().item())
+
+    def values(self, k):
+        """float32 numpy vector of the epoch (the reference's list of np.float32)."""
+        return torch.cat(self.vals[k]).cpu().numpy() if k in self.vals else np.zeros(0, np.float32)
+
+    def confusion(self):
+        if self.acc is not None:
+            return self.acc.confusion_matrix()
+        from sklearn.metrics import confusion_matrix
+        return confusion_matrix(torch.cat(self.labels).numpy(), torch.cat(self.preds).numpy())
 
 
 def evaluate_multimodal_model(multimodal_model, dataloader, device, epoch, total_num_epochs,
@@ -232,8 +276,7 @@ def evaluate_multimodal_model(multimodal_model, dataloader, device, epoch, total
                             "Predictive Uncertainty", "Model Uncertainty", "Scaled KL",
                             "Cross Entropy Loss", "bathy Patch Type", "SSS Patch Type"])
             kl_w = kl_weight_for(epoch, total_num_epochs)
-            total_loss, correct, total = 0.0, 0, 0
-            all_pred, all_lab, all_pu, all_mu = [], [], [], []
+            ep = None
             with torch.no_grad():
                 for batch in dataloader:
                     inputs, labels, bathy, sss = _batch_to(batch, device, bathy_patch_type,
@@ -242,19 +285,14 @@ def evaluate_multimodal_model(multimodal_model, dataloader, device, epoch, total
                     kl = get_kl_loss(multimodal_model)
                     kl_scaled = kl / len(dataloader) * kl_w
                     ce, predicted, st = mc_eval_stats(logits, labels, 1e-8, 1e-8)
-                    total_loss += (ce + kl_scaled).item()
-                    correct += int((predicted == labels).sum().item())
-                    total += labels.size(0)
+                    ep = ep or _EvalEpoch(logits.shape[2])
                     pu = st["predictive_entropy"]
-                    all_pu.extend(pu.cpu().numpy())
-                    all_mu.extend((pu - st["aleatoric"]).cpu().numpy())
-                    all_pred.extend(predicted.cpu().numpy())
-                    all_lab.extend(labels.cpu().numpy())
-            test_accuracy = correct / total
-            test_loss = total_loss / len(dataloader)
-            _confusion_png(all_lab, all_pred, csv_path, model_type, epoch)
-            w.writerow([epoch + 1, model_type, test_loss, test_accuracy, np.mean(all_pu),
-                        np.mean(all_mu), kl_scaled.item(), ce.item(),
+                    ep.add(ce + kl_scaled, labels, predicted, pu=pu, mu=pu - st["aleatoric"])
+            test_accuracy = ep.correct_count() / ep.total
+            test_loss = ep.loss_sum() / len(dataloader)
+            _confusion_png(ep.confusion(), csv_path, model_type, epoch)
+            w.writerow([epoch + 1, model_type, test_loss, test_accuracy, np.mean(ep.values("pu")),
+                        np.mean(ep.values("mu")), kl_scaled.item(), ce.item(),
                         bathy_patch_type or "patch_30_bathy", sss_patch_type or "patch_30_sss"])
             logging.info(f"Epoch {epoch + 1}: Test Loss: {test_loss:.4f}, "
                          f"Accuracy: {test_accuracy:.4f}")
@@ -330,8 +368,7 @@ def evaluate_unimodal_model(model, dataloader, device, epoch, csv_path, total_nu
             if new_file:
                 w.writerow(["Epoch", "Model Type", "Test Loss", "Test Accuracy",
                             "predictive_uncertainty", "model_uncertainty"])
-            correct, total, total_loss = 0, 0, 0.0
-            all_ep, all_al, all_pred, all_lab = [], [], [], []
+            ep = None
             with torch.no_grad():
                 for batch in dataloader:
                     if model_type not in _UNI_SOURCES:
@@ -341,18 +378,16 @@ def evaluate_unimodal_model(model, dataloader, device, epoch, csv_path, total_nu
                     logits = mc_logits(model, num_mc, x)
                     kl = get_kl_loss(model)
                     ce, predicted, st = mc_eval_stats(logits, labels, 1e-7, 1e-7)
-                    total_loss += (ce + kl_w * (kl / dataloader.batch_size)).item()
-                    correct += int((predicted == labels).sum().item())
-                    total += labels.size(0)
-                    all_ep.extend(st["var"].cpu().numpy())
-                    all_al.extend(st["aleatoric"].cpu().numpy())
-                    all_pred.extend(predicted.cpu().numpy())
-                    all_lab.extend(labels.cpu().numpy())
-            accuracy = correct / total
-            avg_loss = total_loss / total
-            _confusion_png(all_lab, all_pred, csv_path, model_type, epoch)
+                    ep = ep or _EvalEpoch(logits.shape[2])
+                    ep.add(ce + kl_w * (kl / dataloader.batch_size), labels, predicted,
+                           ep_=st["var"], al=st["aleatoric"])
+            accuracy = ep.correct_count() / ep.total
+            avg_loss = ep.loss_sum() / ep.total
+            all_ep, all_al = ep.values("ep_"), ep.values("al")
+            _confusion_png(ep.confusion(), csv_path, model_type, epoch)
             w.writerow([epoch + 1, model_type, avg_loss, accuracy,
-                        np.mean(all_ep) if all_ep else 0.0, np.mean(all_al) if all_al else 0.0])
+                        np.mean(all_ep) if all_ep.size else 0.0,
+                        np.mean(all_al) if all_al.size else 0.0])
     except Exception:
         from .checkpointing import save_model
         save_model(model, csv_path, model_type)

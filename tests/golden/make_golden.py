@@ -17,6 +17,8 @@ drives the reference's OWN code:
   G8  train/loop_utils.py:train_and_evaluate_multimodal_model (epoch driver, 2 epochs)
   G9  train/loop_utils.py:train_and_evaluate_unimodal_model (epoch driver, range(1, 3))
       (``--loops``: writes golden_loops.json only)
+  G10 Examples/"Example training with image noise.py":simulate_underwater_degradation
+      (``--staging``: writes golden_staging.npz only)
 
 Epsilons come from one seeded torch.Generator consumed in forward order, so the oracle
 (``oracle/``) reproduces them by running the same module order.  Outputs land in
@@ -101,6 +103,13 @@ def main():
     out, arrays = {}, {}
     tmp = tempfile.mkdtemp()
     torch.set_num_threads(8)
+    here = os.path.dirname(os.path.abspath(__file__))
+    if "--staging" in sys.argv:   # G10 only (golden_staging.npz)
+        staging_golden(here)
+        return
+    if "--loops" in sys.argv:   # G8/G9 only (golden_loops.json); G3-G7 stay as committed
+        loops_golden(mu, SummaryWriter, prior, tmp, here)
+        return
 
     # ---------------- G3: reference define_models + MultiModalModel forward -------------
     torch.manual_seed(SEED_MODEL)
@@ -180,10 +189,6 @@ def main():
     out["g7_param_digest"] = param_digest(uni)
     bayes_ref.set_eps_source(None)
 
-    here = os.path.dirname(os.path.abspath(__file__))
-    if "--loops" in sys.argv:   # G8/G9 only (golden_loops.json); G3-G7 stay as committed
-        loops_golden(mu, SummaryWriter, prior, tmp, here)
-        return
     with open(os.path.join(here, "golden.json"), "w") as f:
         json.dump(out, f, indent=1)
     np.savez_compressed(os.path.join(here, "golden.npz"), **arrays)
@@ -231,6 +236,31 @@ def loops_golden(mu, SummaryWriter, prior, tmp, here):
     with open(os.path.join(here, "golden_loops.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1)[:3000])
+
+
+def staging_golden(here):
+    """G10: the reference's simulate_underwater_degradation
+    (Examples/"Example training with image noise.py":55-93) on seeded inputs: the function's
+    own definition is taken from the script (its module imports the whole training stack and
+    its file name has spaces) and run as written."""
+    import ast
+    path = os.path.join(REF_PKG, "Examples", "Example training with image noise.py")
+    tree = ast.parse(open(path).read())
+    fn = next(n for n in tree.body if isinstance(n, ast.FunctionDef)
+              and n.name == "simulate_underwater_degradation")
+    ns = {"torch": torch}
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), path, "exec"), ns)
+    sim = ns["simulate_underwater_degradation"]
+    g = torch.Generator().manual_seed(SEED_DATA + 10)
+    clean = torch.randn(2, 3, 8, 12, generator=g)            # a normalised optical batch
+    ones = torch.ones(2, 1, 8, 12)
+    dmap = torch.rand(2, 1, 8, 12, generator=g) * 3
+    arrays = {"clean": clean.numpy(), "dmap": dmap.numpy()}
+    for i, (turb, depth) in enumerate(((0.3, 1), (1.5, 1), (0.9, 2.5))):
+        arrays[f"uniform_{i}"] = sim(clean, ones, turb, depth).numpy()
+        arrays[f"map_{i}"] = sim(clean, dmap, turb, depth).numpy()
+    np.savez_compressed(os.path.join(here, "golden_staging.npz"), **arrays)
+    print("golden_staging.npz:", list(arrays))
 
 
 if __name__ == "__main__":

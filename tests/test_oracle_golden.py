@@ -153,3 +153,25 @@ def test_rho_gradient_uses_last_eps():
     sig = torch.sigmoid(layer.rho_kernel.detach())
     last = 3 * W.grad * eps[1] * sig
     assert torch.allclose(layer.rho_kernel.grad, last, atol=1e-5)
+
+
+def test_g10_uifm_degradation_matches_reference():
+    """oracle/staging_ref.simulate_underwater_degradation == the reference's own function
+    (golden_staging.npz, made by running it from the Examples script)."""
+    from oracle.staging_ref import simulate_underwater_degradation as sim
+    S = np.load(os.path.join(HERE, "golden_staging.npz"))
+    clean, dmap = torch.from_numpy(S["clean"]), torch.from_numpy(S["dmap"])
+    ones = torch.ones_like(dmap)
+    for i, (turb, depth) in enumerate(((0.3, 1), (1.5, 1), (0.9, 2.5))):
+        np.testing.assert_array_equal(sim(clean, ones, turb, depth).numpy(), S[f"uniform_{i}"])
+        np.testing.assert_array_equal(sim(clean, dmap, turb, depth).numpy(), S[f"map_{i}"])
+
+
+def test_to_tensor_normalize_known_answers():
+    """ToTensor is k / 255 in fp32 for every uint8 k; Normalize is (x - mean) / std."""
+    from oracle.staging_ref import to_tensor_normalize
+    t = torch.arange(256, dtype=torch.uint8).view(1, 16, 16, 1)
+    x = to_tensor_normalize(t)
+    assert torch.equal(x.flatten(), torch.arange(256, dtype=torch.float32) / 255)
+    y = to_tensor_normalize(t.expand(1, 16, 16, 3).contiguous(), (0.2, 0.3, 0.4), (0.5, 0.6, 0.7))
+    assert torch.equal(y[0, 1], (x[0, 0] - torch.tensor(0.3)) / torch.tensor(0.6))
