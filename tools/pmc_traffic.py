@@ -17,8 +17,8 @@ from collections import defaultdict
 def family(name):
     if "conv_gemm_f32" in name or "conv_split_f32" in name:
         return "conv_f32"        # the fp32 conv family: split kernels + stems on conv_gemm_f32
-    if "conv_gemm_h16" in name:
-        return "conv_h16"
+    if "conv_gemm_h16" in name or "conv_pipe16" in name:
+        return "conv_h16"        # the 16-bit conv family: pipelined kernels + fallback shapes
     return name.split("(")[0].replace("void ", "")
 
 
@@ -31,7 +31,7 @@ def load(d, counter):
     return out
 
 
-def main(fetch_dir, write_dir, out_json):
+def main(fetch_dir, write_dir, out_json, fam=None):
     fe, wr = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
     agg = defaultdict(lambda: [0, 0, 0.0, 0.0])
     for _, (n, v) in fe.items():
@@ -44,8 +44,10 @@ def main(fetch_dir, write_dir, out_json):
         a[3] += v * 1024.0
     rows = {k: {"launches": v[0], "read_bytes": v[2], "write_bytes": v[3],
                 "bytes_per_launch": (v[2] + v[3]) / max(v[0], 1)} for k, v in agg.items()}
-    conv = rows["conv_f32"]
-    res = {"kernel": "conv_f32 (conv_split_f32 + stem conv_gemm_f32)",
+    fam = fam or ("conv_f32" if "conv_f32" in rows else "conv_h16")
+    conv = rows[fam]
+    res = {"kernel": {"conv_f32": "conv_f32 (conv_split_f32 + stem conv_gemm_f32)",
+                      "conv_h16": "conv_h16 (conv_pipe16 + conv_gemm_h16)"}[fam],
            "bytes_per_launch": round(conv["bytes_per_launch"]),
            "launches": conv["launches"], "per_family": rows,
            "method": "2*FETCH_SIZE + WRITE_SIZE (rocprofv3 PMC, separate passes, KiB units)"}
@@ -56,4 +58,4 @@ def main(fetch_dir, write_dir, out_json):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
