@@ -275,6 +275,23 @@ int mauv_pack_nchw_h16(int dtype, const float* x, int B, int C, int H, int W, in
 int mauv_pack_nchw_f32(const float* x, int B, int C, int H, int W, int Cp, float* y,
                        hipStream_t stream);
 
+/* ---- stems over shared im2col rows (stem.hip) --------------------------------------------
+ * conv1 of each trunk (7x7 / 2, models/base_models.py:18, model_utils.py:58-59) sees the same
+ * images in every MC sample.  mauv_stem_im2col unrolls fp32 NCHW images once into rows
+ * cols[m][k] (m = (b, oh, ow), k = c*R*S + r*S + s: the OIHW parameter order), zero for
+ * k >= C*R*S up to Kp (Kp % 8 == 0); dtype -1 = fp32, 0 = bf16, 1 = f16 rows (RNE).
+ * mauv_stem_fwd_{f32,h16}: y[g][m][c] = sum_k cols[m][k] w[g][c][k] as ONE GEMM with the G
+ * weight sets stacked along N (w: [G][Cout][Kp], k >= C*R*S zero); per-m-tile BatchNorm
+ * partials as mauv_conv2d_fwd_f32 with nblk = mauv_conv2d_fwd_stat_blocks of the stem.
+ * fp32 needs Kp % 4 == 0, 16-bit Kp % 64 == 0 and Cout % 8 == 0.  The weight gradient is
+ * mauv_conv2d_bwd_weight_* of a 1x1 conv over the rows (group stride 0). */
+int mauv_stem_im2col(int dtype, const float* x, int B, int C, int H, int W, int R, int S,
+                     int stride, int pad, int Kp, void* out, hipStream_t stream);
+int mauv_stem_fwd_f32(const float* cols, const float* w, float* y, int G, int M, int Kp,
+                      int Cout, float* st_mean, float* st_m2, float* st_cnt, hipStream_t stream);
+int mauv_stem_fwd_h16(int dtype, const void* cols, const void* w, void* y, int G, int M, int Kp,
+                      int Cout, float* st_mean, float* st_m2, float* st_cnt, hipStream_t stream);
+
 /* ---- fusion head + MC head (head.hip) ----------------------------------------------------
  * AdditiveAttention.forward (models/base_models.py:43-52) epilogues around the q|k|v and
  * score GEMMs (qkv rows [q | k | v], each hid wide; the reference's model: hid = 128):

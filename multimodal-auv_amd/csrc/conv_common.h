@@ -46,7 +46,17 @@ struct ConvArgs {
   // (n * mg) >> sh for n < 2^31 (mauv::magic_div)
   unsigned long long mg_hw, mg_w;
   int sh_hw, sh_w;
+  // FWD with the MC groups stacked along N (the stems over shared im2col rows, stem.hip):
+  // column n belongs to group n / cpg, channel n % cpg; outputs and BN statistics go to that
+  // group's tensors ([G][M][cpg], [G][nblk][cpg]).  0 = off.
+  int cpg;
 };
+
+// output element (row, col) of a FWD/DGRAD epilogue, relative to the block's group base
+__device__ __forceinline__ long long conv_out_index(const ConvArgs& a, long long orow, int col) {
+  if (a.cpg) return (long long)(col / a.cpg) * a.out_sg + orow * a.cpg + col % a.cpg;
+  return orow * a.N + col;
+}
 
 // q = n / d as (n * m) >> s for every n < 2^31: s = 31 + ceil(log2 d), m = floor(2^s / d) + 1
 // (m*d - 2^s lies in (0, d], so the error term n*(m*d - 2^s)/(d*2^s) < 1/d never crosses an
@@ -136,7 +146,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx16 (&acc)
             orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
           }
         }
-        const long long o = orow * a.N + col;
+        const long long o = MODE == FWD ? conv_out_index(a, orow, col) : orow * a.N + col;
         float v = acc[mi][ni][r] + bias;
         if constexpr (MODE == DGRAD) {
           if (a.addend) v += a.addend[(long long)g * a.out_sg + o];
@@ -210,10 +220,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx16 (&acc)
       }
       const int mt = m0 / SR + sb;
       if (fst) {
-        const long long so = ((long long)g * a.st_nblk + a.st_base + mt) * a.N + n0 + col;
+        const int gc = a.cpg ? (n0 + col) / a.cpg : g, cc = a.cpg ? (n0 + col) % a.cpg : n0 + col;
+        const int nc = a.cpg ? a.cpg : a.N;
+        const long long so = ((long long)gc * a.st_nblk + a.st_base + mt) * nc + cc;
         a.st_mean[so] = t1 / (float)nv;
         a.st_m2[so] = t2;
-        if (n0 + col == 0) a.st_cnt[(long long)g * a.st_nblk + a.st_base + mt] = (float)nv;
+        if (cc == 0) a.st_cnt[(long long)gc * a.st_nblk + a.st_base + mt] = (float)nv;
       } else {
         const long long so = ((long long)g * a.bp_nblk + a.bp_base + mt) * a.N + n0 + col;
         a.bp_p1[so] = t1;

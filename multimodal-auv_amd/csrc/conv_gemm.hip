@@ -661,6 +661,27 @@ MAUV_API int mauv_conv2d_fwd_f32(const float* x, const long long* x_strides,
   return check_launch("conv2d_fwd");
 }
 
+// The stems as ONE GEMM over im2col rows shared by the G MC samples (stem.hip):
+// y[g][m][c] = sum_k cols[m][k] * w[g][c][k] with the G weight sets stacked along N
+// (N = G * Cout, ConvArgs::cpg = Cout): every row of the images is read once for all samples.
+MAUV_API int mauv_stem_fwd_f32(const float* cols, const float* w, float* y, int G, int M,
+                               int Kp, int Cout, float* st_mean, float* st_m2, float* st_cnt,
+                               hipStream_t stream) {
+  if (G <= 0 || M <= 0 || Kp <= 0 || Cout <= 0 || Kp % 4) { set_error("stem_fwd_f32: bad shape"); return kErrArg; }
+  ConvArgs a = make_args(1, 1, 1, M, Kp, G * Cout, 1, 1, 1, 0, nullptr);
+  a.x = cols; a.w = w; a.out = y;
+  a.M = M; a.N = G * Cout; a.K = Kp;
+  a.out_sg = (long long)M * Cout;
+  a.cpg = Cout;
+  a.st_mean = st_mean; a.st_m2 = st_m2; a.st_cnt = st_cnt;
+  a.st_nblk = stat_blocks(M, Cout, G); a.st_base = 0;
+  const int fm = f32_math();
+  if ((fm == 6 || fm == 5) && conv_split_launch(FWD, a, fm == 5, stream)) return check_launch("stem_fwd_f32");
+  if (Kp % 32 == 0) launch_tiles<FWD, true, true>(a, stream);
+  else launch_tiles<FWD, false, true>(a, stream);
+  return check_launch("stem_fwd_f32");
+}
+
 // Data gradient: dx[g] = conv_transpose(dy[g], W_g) (+ addend) (+ dx if accumulate).
 MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx,
                                       const float* addend, int accumulate, int G, int B, int H,

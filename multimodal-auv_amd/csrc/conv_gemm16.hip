@@ -550,6 +550,26 @@ MAUV_API int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_st
   return check_launch("conv2d_fwd_h16");
 }
 
+// 16-bit counterpart of mauv_stem_fwd_f32 (conv_gemm.hip): the pipelined kernel over the
+// shared im2col rows with the G weight sets stacked along N; Kp % 64 == 0.
+MAUV_API int mauv_stem_fwd_h16(int dtype, const void* cols, const void* w, void* y, int G,
+                               int M, int Kp, int Cout, float* st_mean, float* st_m2,
+                               float* st_cnt, hipStream_t stream) {
+  if (int e = check_shape16("stem_fwd_h16", dtype, G, 1, Kp, Cout, nullptr)) return e;
+  if (M <= 0 || Kp % 64) { set_error("stem_fwd_h16: needs M > 0 and Kp % 64 == 0"); return kErrArg; }
+  if (!aligned16(cols) || !aligned16(w)) { set_error("stem_fwd_h16: cols, w must be 16-B aligned"); return kErrArg; }
+  ConvArgs16 h = make_args16(1, 1, 1, M, Kp, G * Cout, 1, 1, 1, 0, nullptr);
+  h.x = (const u16*)cols; h.w = (const u16*)w; h.out = y;
+  h.M = M; h.N = G * Cout; h.K = Kp;
+  h.out_sg = (long long)M * Cout;
+  h.st_mean = st_mean; h.st_m2 = st_m2; h.st_cnt = st_cnt;
+  h.st_nblk = ceil_div(M, conv_tile_rows(M));
+  ConvArgs a = pipe_args(h);
+  a.cpg = Cout;
+  if (!conv_pipe16_launch(FWD, dtype, a, stream)) { set_error("stem_fwd_h16: shape outside the pipelined kernel"); return kErrArg; }
+  return check_launch("stem_fwd_h16");
+}
+
 MAUV_API int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, void* dx,
                                       const void* addend, int accumulate, int G, int B, int H,
                                       int W, int Cin, int Cout, int R, int S, int stride, int pad,

@@ -426,10 +426,12 @@ void conv_pipe16(const ConvArgs a) {
 #pragma unroll
       for (int w = 0; w < WGM; ++w) { t1 += red[w * BN + tid]; t2 += red[WGM * BN + w * BN + tid]; }
       const int mt = m0 / BM;
-      const long long so = ((long long)g * a.st_nblk + mt) * a.N + n0 + tid;
+      const int col = n0 + tid;
+      const int gc = a.cpg ? col / a.cpg : g, cc = a.cpg ? col % a.cpg : col;
+      const long long so = ((long long)gc * a.st_nblk + mt) * (a.cpg ? a.cpg : a.N) + cc;
       a.st_mean[so] = t1 / (float)nvalid;
       a.st_m2[so] = t2;
-      if (n0 + tid == 0) a.st_cnt[(long long)g * a.st_nblk + mt] = (float)nvalid;
+      if (cc == 0) a.st_cnt[(long long)gc * a.st_nblk + mt] = (float)nvalid;
     }
     __syncthreads();  // red is overwritten by the staged store below
   }
@@ -474,7 +476,8 @@ void conv_pipe16(const ConvArgs a) {
           orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
         }
       }
-      const long long o = (long long)g * a.out_sg + orow * a.N + col;
+      const long long o = (long long)g * a.out_sg +
+                          (MODE == FWD ? conv_out_index(a, orow, col) : orow * a.N + col);
       if constexpr (MODE == DGRAD) {
         if (addp) f += unpack8<DT>(*(const u32x4*)(addp + o));
         if (a.accumulate) f += unpack8<DT>(*(const u32x4*)(outp + o));
@@ -534,7 +537,8 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
   if (!on) return false;
   const long long lim = 0x7fff0000LL / 2;  // elements addressable by a 31-bit byte offset
   const long long nx = (long long)a0.B * a0.xs_b, ny = (long long)a0.B * a0.Ho * a0.Wo * a0.Cout;
-  if (nx > lim || ny > lim || a0.ws_g > lim) return false;
+  // (the FWD output is stored through plain pointers: only dgrad / wgrad read y by rsrc)
+  if (nx > lim || (mode != FWD && ny > lim) || a0.ws_g > lim) return false;
   const bool xs8 = a0.xs_w % 8 == 0 && a0.xs_h % 8 == 0 && a0.xs_b % 8 == 0 && a0.xs_g % 8 == 0;
   ConvArgs a = a0;
   if (mode == FWD) {

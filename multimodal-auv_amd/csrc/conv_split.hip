@@ -449,7 +449,8 @@ static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
 bool conv_split_launch(int mode, const ConvArgs& a0, int oneacc, hipStream_t st) {
   const long long lim = 0x7fff0000LL / 4;  // floats addressable by a 31-bit byte offset
   const long long nx = (long long)a0.B * a0.xs_b, ny = (long long)a0.B * a0.Ho * a0.Wo * a0.Cout;
-  if (nx > lim || ny > lim || a0.ws_g > lim) return false;
+  // (the FWD output is stored through plain pointers: only dgrad / wgrad read y by rsrc)
+  if (nx > lim || (mode != FWD && ny > lim) || a0.ws_g > lim) return false;
   ConvArgs a = a0;
   if (mode == FWD && a.Cin == 4 && a.S <= 8 && a.xs_c == 1 && a.xs_w == 4 && !a.xsc &&
       a.xs_h % 4 == 0 && a.xs_b % 4 == 0 && a.xs_g % 4 == 0 && a.N == 64) {

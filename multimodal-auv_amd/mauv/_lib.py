@@ -72,6 +72,10 @@ SIGNATURES = {
     "mauv_avgpool_bwd_h16": [I, P, I, I, I, P, P],
     "mauv_pack_nchw_h16": [I, P, I, I, I, I, I, P, P],
     "mauv_pack_nchw_f32": [P, I, I, I, I, I, P, P],
+    # stem.hip
+    "mauv_stem_im2col": [I, P] + [I] * 9 + [P, P],
+    "mauv_stem_fwd_f32": [P, P, P, I, I, I, I, P, P, P, P],
+    "mauv_stem_fwd_h16": [I, P, P, P, I, I, I, I, P, P, P, P],
     # head.hip
     "mauv_attn_t": [P, I, I, P, P],
     "mauv_attn_t_bwd": [P, P, I, I, P, P],

@@ -49,6 +49,9 @@ FUSED_STEM_POOL = os.environ.get("MAUV_FUSED_STEM_POOL", "1") == "1"
 # backward reads those instead of the 2-4 B stored output (MAUV_BN_RELU_MASK=0: read the output).
 # Not with the dgrad BN epilogue, which takes its mask from the output.
 BN_RELU_MASK = os.environ.get("MAUV_BN_RELU_MASK", "1") == "1" and not DGRAD_BN_EPILOGUE
+# The stems as ONE GEMM over im2col rows shared by the G samples, the G weight sets stacked
+# along N (stem.hip), instead of G implicit GEMMs over channel-padded pixels.
+STEM_GEMM = os.environ.get("MAUV_STEM_GEMM", "1") == "1"
 _STREAMS = {}
 
 
@@ -440,6 +443,45 @@ class TrunkRunner(_Runner):
                             accumulate=accumulate, bn=bn_args)
         return dx, pre
 
+    def _stem(self, conv, x, B, H, W):
+        """conv1 over im2col rows of the images, shared by the G samples: one GEMM
+        [M x Kp] . [Kp x G*Cout] (ops.stem_fwd); the sampled weights are the OIHW parameter
+        rows [Cout][Cin*R*S] zero-padded to Kp."""
+        G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
+        st, pd = conv.stride[0], conv.padding[0]
+        K = Cin * k * k
+        Kp = ops.stem_kp(self.dt, K)
+        Ho, Wo = ops.out_hw(H, k, st, pd), ops.out_hw(W, k, st, pd)
+        M = B * Ho * Wo
+        cols = torch.empty(M, Kp, device=x.device, dtype=self.dt)
+        ops.stem_im2col(x, B, Cin, H, W, k, st, pd, Kp, cols)
+        w = torch.zeros(G, Cout, Kp, device=x.device, dtype=self.dt)
+        self._sample(conv, conv.mu_kernel, conv.rho_kernel, "kernel", w, Cout, K, 1, cin_pad=Kp)
+        y = torch.empty(G, B, Ho, Wo, Cout, device=x.device, dtype=self.dt)
+        nblk = ops.fwd_stat_blocks(G, B, H, W, Cin, Cout, k, st, pd)
+        buf = torch.empty(2 * G * nblk * Cout + G * nblk, device=x.device)
+        part = (buf[:G * nblk * Cout], buf[G * nblk * Cout:2 * G * nblk * Cout],
+                buf[2 * G * nblk * Cout:], nblk)
+        ops.stem_fwd(cols, w, y, G, M, Kp, Cout, part[:3], K)
+        rec = ("stem", conv, cols, M, Kp) if self.save else None
+        return y, rec, part
+
+    def _stem_bwd(self, rec, dy):
+        """Weight gradient of _stem: a 1x1 weight-gradient GEMM over the shared rows (group
+        stride 0), then the reparameterisation backward over the [Cout][Kp] slabs."""
+        _, conv, cols, M, Kp = rec
+        if not conv.mu_kernel.requires_grad:
+            return
+        G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
+        K = Cin * k * k
+        xs = (0, Kp, Kp, Kp, 1)
+        splits = ops.wgrad_splits(G, M, 1, 1, Kp, Cout, 1, 1, 0)
+        ws = torch.empty(splits, G, Cout, Kp, device=dy.device)
+        ops.conv2d_bwd_weight(cols, dy, ws, splits, G, M, 1, 1, Kp, Cout, 1, 1, 0, x_strides=xs,
+                              alg_cin=K)
+        self._reparam_bwd(conv, conv.mu_kernel, conv.rho_kernel, ws, splits, Cout, K, 1,
+                          "kernel", dw_cin=Kp)
+
     def _bn(self, bn, y, part, relu, res=None, materialize=True, res_bn=None):
         """Statistics (from the conv epilogue partials) + optional materialised output."""
         G, C = self.G, y.shape[-1]
@@ -505,14 +547,17 @@ class TrunkRunner(_Runner):
             raise ValueError(f"trunk expects {t.conv1.in_channels} input channels, got {Cin}")
         self.B = B
         recs = self.recs = []
-        cp = self._cin_pad(Cin)
-        if self.dt == torch.float32 and cp == Cin:   # the stem reads the NCHW images in place
-            xs = (0, Cin * H * W, W, 1, H * W)
-        else:           # NHWC copy, channels zero-padded to 8 (16-bit) / 4 (fp32)
-            xh = torch.empty(B, H, W, cp, device=x.device, dtype=self.dt)
-            ops.pack_nchw(x, B, Cin, H, W, cp, xh)
-            x, xs = xh, (0, H * W * cp, W * cp, cp, 1)
-        y, rc, part = self._conv(t.conv1, x, B, H, W, x_strides=xs)
+        if STEM_GEMM:
+            y, rc, part = self._stem(t.conv1, x, B, H, W)
+        else:
+            cp = self._cin_pad(Cin)
+            if self.dt == torch.float32 and cp == Cin:   # the stem reads the NCHW images in place
+                xs = (0, Cin * H * W, W, 1, H * W)
+            else:           # NHWC copy, channels zero-padded to 8 (16-bit) / 4 (fp32)
+                xh = torch.empty(B, H, W, cp, device=x.device, dtype=self.dt)
+                ops.pack_nchw(x, B, Cin, H, W, cp, xh)
+                x, xs = xh, (0, H * W * cp, W * cp, cp, 1)
+            y, rc, part = self._conv(t.conv1, x, B, H, W, x_strides=xs)
         H, W = y.shape[2], y.shape[3]
         Hp, Wp = ops.out_hw(H, 3, 2, 1), ops.out_hw(W, 3, 2, 1)
         p = torch.empty(G, B, Hp, Wp, 64, device=x.device, dtype=self.dt)
@@ -609,7 +654,10 @@ class TrunkRunner(_Runner):
         del da, idx
         dy0, _ = self._bn_bwd(rb, da0)
         del da0
-        self._conv_bwd(rc, dy0, need_dx=False)
+        if rc[0] == "stem":
+            self._stem_bwd(rc, dy0)
+        else:
+            self._conv_bwd(rc, dy0, need_dx=False)
         if self.side is not None:
             torch.cuda.current_stream().wait_stream(self.side)
         if self.st.grad_ready_hook is not None:

@@ -411,6 +411,44 @@ def pack_nchw(x, B, C, H, W, Cp, y):
           "pack_nchw_h16")
 
 
+# ----------------------------------------------------------------------- stems (stem.hip)
+def stem_kp(dtype, K):
+    """Row width of the stem's im2col rows: K = Cin*R*S padded to the GEMM's K slice."""
+    q = 32 if dtype == torch.float32 else 64
+    return (K + q - 1) // q * q
+
+
+def stem_im2col(x, B, C, H, W, R, stride, pad, Kp, cols):
+    """cols[B*Ho*Wo][Kp] (fp32 / bf16 / f16) from fp32 NCHW images, k = c*R*R + r*R + s."""
+    _f32(x)
+    assert cols.is_cuda and cols.is_contiguous()
+    code = -1 if cols.dtype == torch.float32 else H16[cols.dtype]
+    Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
+    assert cols.numel() == B * Ho * Wo * Kp
+    check(lib.mauv_stem_im2col(code, _p(x), B, C, H, W, R, R, stride, pad, Kp, _p(cols),
+                               stream()), "stem_im2col")
+
+
+def stem_fwd(cols, w, y, G, M, Kp, Cout, stats, alg_k):
+    """y[G][M][Cout] = cols[M][Kp] . w[g][Cout][Kp]^T for every g as one GEMM (weights stacked
+    along N); stats = (mean, m2, cnt) partials as conv2d_fwd's.  alg_k: the stem's real
+    Cin*R*S (profiling counts algorithmic work, not the zero padding)."""
+    sm, s2, sn = stats
+    fl = 2.0 * G * M * Cout * alg_k
+    esz = w.element_size()
+    nb = esz * (M * Kp + G * Cout * Kp + G * M * Cout)
+    if w.dtype in H16:
+        _h16(w.dtype, cols, w, y)
+        with _Prof("fwd_" + str(w.dtype)[6:], fl, nb):
+            check(lib.mauv_stem_fwd_h16(H16[w.dtype], _p(cols), _p(w), _p(y), G, M, Kp, Cout,
+                                        _p(sm), _p(s2), _p(sn), stream()), "stem_fwd_h16")
+        return
+    _f32(cols, w, y)
+    with _Prof("fwd", fl, nb):
+        check(lib.mauv_stem_fwd_f32(_p(cols), _p(w), _p(y), G, M, Kp, Cout, _p(sm), _p(s2),
+                                    _p(sn), stream()), "stem_fwd_f32")
+
+
 # ----------------------------------------------------------------------- head
 def attn_t(qkv, rows, hid, t):
     _dev(torch.float32, qkv, t)

@@ -146,6 +146,73 @@ def test_stem_packed_nhwc4(cin, H, R):
     close(ws.sum(0).view(G, 64, R, R, 4)[..., :cin], torch.stack(ref))
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16],
+                         ids=["fp32", "bf16", "f16"])
+@pytest.mark.parametrize("cin,H,G", [(3, 20, 3), (1, 37, 4), (3, 33, 1), (1, 9, 5)])
+def test_stem_im2col_gemm(dt, cin, H, G):
+    """The stems as one GEMM over shared im2col rows (stem.hip): rows bit-exact against
+    F.unfold, outputs / BN partials / weight gradient against float64 convolutions of the
+    same (rounded) operands; G odd leaves a ragged 64-column tile of the stacked N."""
+    from mauv import ops
+    B, R, st, pd = 2, 7, 2, 3
+    torch.manual_seed(5)
+    x = torch.randn(B, cin, H, H)
+    K = cin * R * R
+    Kp = ops.stem_kp(dt, K)
+    Ho = ops.out_hw(H, R, st, pd)
+    M = B * Ho * Ho
+    cols = torch.empty(M, Kp, device=dev, dtype=dt)
+    ops.stem_im2col(x.to(dev), B, cin, H, H, R, st, pd, Kp, cols)
+    ref_cols = torch.zeros(M, Kp)
+    ref_cols[:, :K] = F.unfold(x, R, padding=pd, stride=st).transpose(1, 2).reshape(M, K)
+    assert torch.equal(cols.cpu(), ref_cols.to(dt)), "im2col rows differ"
+    mu = torch.randn(64, cin, R, R) * 0.1
+    rho = torch.full_like(mu, -4.0)
+    eps = torch.randn(G, mu.numel())
+    w = torch.zeros(G, 64, Kp, device=dev, dtype=dt)
+    ops.reparam_sample(mu.to(dev), rho.to(dev), w, G, 0, 0, 0, 64, K, 1, eps=eps.to(dev),
+                       cin_pad=Kp)
+    wref = (mu.view(1, 64, K) + F.softplus(rho).view(1, 64, K) * eps.view(G, 64, K))
+    close(w[..., :K].float(), wref, rtol=4e-3 if dt != torch.float32 else 1e-6, atol=1e-7)
+    assert torch.count_nonzero(w[..., K:]) == 0
+    nblk = ops.fwd_stat_blocks(G, B, H, H, cin, 64, R, st, pd)
+    stats = torch.empty(2 * G * nblk * 64 + G * nblk, device=dev)
+    sm, s2 = stats[:G * nblk * 64], stats[G * nblk * 64:2 * G * nblk * 64]
+    sn = stats[2 * G * nblk * 64:]
+    y = torch.empty(G, B, Ho, Ho, 64, device=dev, dtype=dt)
+    ops.stem_fwd(cols, w, y, G, M, Kp, 64, (sm, s2, sn), K)
+    wc = w.cpu().double()[..., :K].view(G, 64, cin, R, R)
+    xr = x.to(dt).double()
+    ref = torch.stack([F.conv2d(xr, wc[g], stride=st, padding=pd).permute(0, 2, 3, 1)
+                       for g in range(G)])
+    tol = 1e-4 if dt == torch.float32 else 8e-3
+    close(y.float(), ref, rtol=tol)
+    # per-m-tile partials merged -> the batch mean / variance of every group's channels
+    cnt = sn.view(G, nblk).double().cpu()
+    pm = sm.view(G, nblk, 64).double().cpu()
+    pm2 = s2.view(G, nblk, 64).double().cpu()
+    mean = (pm * cnt[..., None]).sum(1) / cnt.sum(1, keepdim=True)
+    m2 = (pm2 + cnt[..., None] * (pm - mean[:, None]) ** 2).sum(1)
+    assert torch.equal(cnt.sum(1), torch.full((G,), float(M), dtype=torch.float64))
+    rf = ref.view(G, M, 64)
+    close(mean, rf.mean(1), rtol=tol, atol=1e-5)
+    close(m2 / M, rf.var(1, unbiased=False), rtol=tol * 2)
+    # weight gradient: 1x1 weight-gradient GEMM over the shared rows
+    dy = torch.randn(G, B, Ho, Ho, 64).to(dt)
+    splits = ops.wgrad_splits(G, M, 1, 1, Kp, 64, 1, 1, 0)
+    ws = torch.empty(splits, G, 64, Kp, device=dev)
+    ops.conv2d_bwd_weight(cols, dy.to(dev), ws, splits, G, M, 1, 1, Kp, 64, 1, 1, 0,
+                          x_strides=(0, Kp, Kp, Kp, 1), alg_cin=K)
+    dref = []
+    for g in range(G):
+        wg = wc[g].clone().requires_grad_(True)
+        F.conv2d(xr, wg, stride=st, padding=pd).backward(dy[g].double().permute(0, 3, 1, 2))
+        dref.append(wg.grad.reshape(64, K))
+    dw = ws.sum(0)
+    close(dw[..., :K], torch.stack(dref), rtol=1e-4 if dt == torch.float32 else 2e-3)
+    assert torch.count_nonzero(dw[..., K:]) == 0
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
 @pytest.mark.parametrize("R,st,pd", [(1, 2, 0), (3, 2, 1), (1, 1, 0)])
 def test_dgrad_accumulate_into_dx(dt, R, st, pd):

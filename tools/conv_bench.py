@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--shape", default="", help="one shape Cin,Cout,R,stride,pad,H (profiling)")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "f16"])
+    ap.add_argument("--xpad", type=int, default=0,
+                    help="FWD: store x with a row pitch of Cin + xpad channels (strided loads)")
     ap.add_argument("--fused", action="store_true",
                     help="as in the model: BN+ReLU applied on load (fwd, wgrad) and BN "
                          "statistics partials from the fwd epilogue")
@@ -88,7 +90,12 @@ def main():
             res = []
             if dt != torch.float32 and Cin % 8:
                 Cin = 8   # the 16-bit path zero-pads the stems' input channels to 8
-            x = torch.randn(G, B, H, H, Cin, device=dev).to(dt)
+            xfull = torch.randn(G, B, H, H, Cin + a.xpad, device=dev).to(dt)
+            x = xfull[..., :Cin] if a.xpad else xfull
+            xstr = None
+            if a.xpad:
+                P = Cin + a.xpad
+                xstr = (B * H * H * P, H * H * P, H * P, P, 1)
             w = (torch.randn(G, Cout, R, R, Cin, device=dev) * 0.05).to(dt)
             y = torch.empty(G, B, Ho, Ho, Cout, device=dev, dtype=dt)
             xbn, stats = None, None
@@ -98,8 +105,9 @@ def main():
                 stats = (torch.empty(G, nblk, Cout, device=dev), torch.empty(G, nblk, Cout, device=dev),
                          torch.empty(G, nblk, device=dev))
             if "fwd" in kinds:
-                res.append(("fwd", timeit(lambda: ops.conv2d_fwd(x, w, y, G, B, H, H, Cin, Cout, R, st, pd,
-                                                                 x_bn=xbn, stats=stats))))
+                res.append(("fwd", timeit(lambda: ops.conv2d_fwd(xfull if a.xpad else x, w, y, G, B, H, H, Cin, Cout, R, st, pd,
+                                                                 x_bn=xbn, stats=stats,
+                                                                 x_strides=xstr))))
             if "dgrad" in kinds and name != "stem" and (dt == torch.float32 or Cout % 32 == 0):
                 dx = torch.empty_like(x)
                 res.append(("dgrad", timeit(lambda: ops.conv2d_bwd_data(y, w, dx, G, B, H, H, Cin, Cout, R, st, pd))))
