@@ -15,7 +15,6 @@
 // WGRAD A/B) as col images [64][rows+32] (ds_read_b64_tr_b16).  Epilogues: FWD statistics from
 // the fp32 accumulators and 16-bit rows staged through LDS (DGRAD: + addend / accumulate, parity
 // class row remap); WGRAD fp32 split-K slabs (conv_common.h).
-#include <stdlib.h>
 
 #include "conv_common.h"
 
@@ -84,15 +83,15 @@ struct Stage16 {
 
 // 2 x 2 waves (32 x 32 each) for 64 x 64 tiles; 4 x 2 / 2 x 4 waves of 32 x 64 / 64 x 32 for
 // 128 x 128, 4 x 2 / 2 x 4 of 32 x 32 for 128 x 64 / 64 x 128 (eight waves, four per SIMD:
-// two blocks per CU); 128 x 256 as 2 x 4 waves of 64 x 64 (one block per CU, two waves per
-// SIMD: half the loader / BN-on-load work and 2/3 of the LDS fragment reads per MAC).
+// two blocks per CU).  Measured and dropped: 128 x 256 tiles as 2 x 4 waves of 64 x 64 (one
+// block per CU: 5-25 % slower per shape) and 128 x 128 as 2 x 2 waves of 64 x 64 (neutral to
+// -2 %), DESIGN.md §2.7.
 template <int BM, int BN>
 struct Waves16 {
-  static constexpr bool WIDE = BN == 256;
-  static constexpr bool W8 = WIDE || BM + BN >= 192;
-  static constexpr int M = WIDE ? 2 : W8 ? (BM == 128 ? 4 : 2) : 2;
-  static constexpr int N = WIDE ? 4 : W8 ? (BM == 128 ? 2 : 4) : 2;
-  static constexpr int T = 64 * M * N, EU = WIDE ? 2 : 4;
+  static constexpr bool W8 = BM + BN >= 192;
+  static constexpr int M = W8 ? (BM == 128 ? 4 : 2) : 2;
+  static constexpr int N = W8 ? (BM == 128 ? 2 : 4) : 2;
+  static constexpr int T = 64 * M * N, EU = 4;
 };
 
 template <int MODE, int DT, int BM, int BN, bool XBN, bool STEM>
@@ -501,24 +500,9 @@ static void launch_pipe16(const ConvArgs& a, hipStream_t st) {
                      a);
 }
 
-// MAUV_P16_WIDE: bit m set -> mode m (FWD 0, DGRAD 1, WGRAD 2) takes 128 x 256 tiles when
-// N >= 256 and M > 64 (default off: one block per CU measured 5-25 % slower per shape than
-// two 128 x 128 blocks, tools/gpubatch_wide.sh)
-static int wide_modes() {
-  static int w = -1;
-  if (w < 0) { const char* e = getenv("MAUV_P16_WIDE"); w = e ? atoi(e) : 0; }
-  return w;
-}
-
 template <int MODE, int DT, bool XBN, bool STEM>
 static void pipe16_tiles(const ConvArgs& a, hipStream_t st) {
   const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
-  if constexpr (!STEM) {
-    if (bm == 128 && a.N >= 256 && ((wide_modes() >> MODE) & 1)) {
-      launch_pipe16<MODE, DT, 128, 256, XBN>(a, st);
-      return;
-    }
-  }
   if (bm == 64 && bn == 64) launch_pipe16<MODE, DT, 64, 64, XBN, STEM>(a, st);
   else if (bm == 64) launch_pipe16<MODE, DT, 64, 128, XBN, STEM>(a, st);
   else if (bn == 64) launch_pipe16<MODE, DT, 128, 64, XBN, STEM>(a, st);
@@ -532,9 +516,6 @@ static void pipe16_dt(int dt, const ConvArgs& a, hipStream_t st) {
 }
 
 bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
-  static int on = -1;  // MAUV_PIPE16=0 keeps conv_gemm16.hip's kernels (A/B measurements)
-  if (on < 0) { const char* e = getenv("MAUV_PIPE16"); on = e ? atoi(e) : 1; }
-  if (!on) return false;
   const long long lim = 0x7fff0000LL / 2;  // elements addressable by a 31-bit byte offset
   const long long nx = (long long)a0.B * a0.xs_b, ny = (long long)a0.B * a0.Ho * a0.Wo * a0.Cout;
   // (the FWD output is stored through plain pointers: only dgrad / wgrad read y by rsrc)

@@ -21,8 +21,6 @@
 // LDS images are conv_gemm16.hip's: k-contiguous operands (FWD A/B, DGRAD A) as row images
 // [rows][BK+8] (one ds_read_b128 per fragment), k-strided ones (DGRAD B, WGRAD A/B) as col images
 // [BK][rows+32] (two ds_read_b64_tr_b16).  Epilogue: conv_common.h (shared with conv_gemm.hip).
-// ABL_SPLIT_A / ABL_SPLIT_B (compile-time, never in the product build) store one plane of the
-// A / B operand instead of its exact split: timing ablation only (tools/gpubatch_ablsplit.sh).
 #include <stdlib.h>
 
 #include "conv_common.h"
@@ -294,11 +292,7 @@ void conv_split_f32(const ConvArgs a) {
       u16* dst = act ? As + off : dum;
       const int pst = act ? A_PL : 4;
       uint2 pl[3];
-#ifdef ABL_SPLIT_A
-      pl[0].x = pk_bf16(v[0], v[1]); pl[0].y = pk_bf16(v[2], v[3]); pl[1] = pl[2] = make_uint2(0, 0);
-#else
       split_bf16<3>(v, pl);
-#endif
 #pragma unroll
       for (int p = 0; p < 3; ++p) *(uint2*)(dst + p * pst) = pl[p];
     }
@@ -313,11 +307,7 @@ void conv_split_f32(const ConvArgs a) {
       u16* dst = act ? Bs + off : dum;
       const int pst = act ? B_PL : 4;
       uint2 pl[3];
-#ifdef ABL_SPLIT_B
-      pl[0].x = pk_bf16(v[0], v[1]); pl[0].y = pk_bf16(v[2], v[3]); pl[1] = pl[2] = make_uint2(0, 0);
-#else
       split_bf16<3>(v, pl);
-#endif
 #pragma unroll
       for (int p = 0; p < 3; ++p) *(uint2*)(dst + p * pst) = pl[p];
     }

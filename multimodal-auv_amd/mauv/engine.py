@@ -17,7 +17,6 @@ Activations are NHWC ``[G][B][H][W][C]`` fp32.  The stems read one NHWC copy of 
 NCHW images with the channels zero-padded to 4 (16-bit path: 8), shared by all MC samples
 (group stride 0).
 """
-import contextlib
 import os
 
 import torch
@@ -26,10 +25,6 @@ from . import ops
 from .layers import is_bayesian, LinearReparameterization
 
 
-# BN-backward partial sums (sum dz, sum dz*xhat) from the dgrad epilogue instead of a separate
-# pass over (y, dout).  Measured slower on MI355X (the LDS reduction lengthens every dgrad
-# tile more than the standalone partial kernel costs), so it is opt-in.
-DGRAD_BN_EPILOGUE = os.environ.get("MAUV_DGRAD_BN_EPILOGUE", "0") == "1"
 # fp32 stems on an NHWC copy of the images with 4 zero-padded channels (the pipelined split
 # kernel's STEM mode) instead of strided NCHW loads on the generic kernel
 F32_STEM_PACK = os.environ.get("MAUV_F32_STEM_PACK", "1") == "1"
@@ -37,18 +32,12 @@ F32_STEM_PACK = os.environ.get("MAUV_F32_STEM_PACK", "1") == "1"
 # forward and (autograd replays the forward's stream) its backward on a stream of its own, so
 # one trunk's memory-bound BN passes overlap another's MFMA-bound convs.
 TRUNK_STREAMS = os.environ.get("MAUV_TRUNK_STREAMS", "1") == "1"
-# Within a trunk's backward the weight gradient of each conv (+ its reparameterisation
-# backward) is off the critical dgrad -> BN-backward chain: MAUV_SIDE_WGRAD=1 runs it on a
-# side stream.  Off by default: with the three trunks already concurrent it measured neutral
-# (226-229 vs 228-230 triplets/s fp32, tools/gpubatch_streams.sh).
-SIDE_WGRAD = os.environ.get("MAUV_SIDE_WGRAD", "0") == "1"
 # The stem's bn1 + ReLU applied on load inside the max-pool (the 112x112 BN output, the largest
 # activation of the trunk, is never written; its backward recomputes the ReLU mask from y).
 FUSED_STEM_POOL = os.environ.get("MAUV_FUSED_STEM_POOL", "1") == "1"
 # Training block outputs (bn3 + residual + ReLU) also write 1-bit ReLU masks, and their
 # backward reads those instead of the 2-4 B stored output (MAUV_BN_RELU_MASK=0: read the output).
-# Not with the dgrad BN epilogue, which takes its mask from the output.
-BN_RELU_MASK = os.environ.get("MAUV_BN_RELU_MASK", "1") == "1" and not DGRAD_BN_EPILOGUE
+BN_RELU_MASK = os.environ.get("MAUV_BN_RELU_MASK", "1") == "1"
 # The stems as ONE GEMM over im2col rows shared by the G samples, the G weight sets stacked
 # along N (stem.hip), instead of G implicit GEMMs over channel-padded pixels.
 STEM_GEMM = os.environ.get("MAUV_STEM_GEMM", "1") == "1"
@@ -56,11 +45,10 @@ _STREAMS = {}
 
 
 def _trunk_streams(dev):
-    """(main, side) stream pairs of the three trunks."""
+    """The streams of the three trunks."""
     key = dev.index if dev.index is not None else torch.cuda.current_device()
     if key not in _STREAMS:
-        _STREAMS[key] = [(torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
-                         for _ in range(3)]
+        _STREAMS[key] = [torch.cuda.Stream(device=dev) for _ in range(3)]
     return _STREAMS[key]
 
 
@@ -349,16 +337,6 @@ class _BN:
         """(scale, shift, relu) for a consumer that applies this BN on load."""
         return (self.stats[2], self.stats[3], int(self.relu))
 
-    def epilogue_args(self, G, dgrad_shape):
-        """Arguments for a dgrad whose output is this BN's output gradient: the epilogue then
-        writes this BN's backward partial sums (returned as pre=(p1, p2, nblk))."""
-        nblk = ops.dgrad_stat_blocks(G, *dgrad_shape)
-        p = torch.empty(2, G, nblk, self.C, device=self.y.device)
-        args = dict(y=self.y, out=self.out, scale=self.stats[2], shift=self.stats[3],
-                    mean=self.stats[0], invstd=self.stats[1], relu=int(self.relu),
-                    p1=p[0], p2=p[1])
-        return args, (p[0], p[1], nblk)
-
 
 class TrunkRunner(_Runner):
     """torchvision ResNet-50 trunk (Bayesian convs, train-mode BN) for G MC samples.
@@ -367,17 +345,13 @@ class TrunkRunner(_Runner):
     * BN statistics come from the producing conv's epilogue (per-m-tile Welford partials);
     * bn1/bn2 of every bottleneck are never materialised: conv2/conv3 apply
       relu(y*scale + shift) while loading their input (forward and weight-gradient), and their
-      backward rebuilds the ReLU mask from y;
-    * the backward partial sums of each BN come from the epilogue of the dgrad that produces
-      its output gradient.
+      backward rebuilds the ReLU mask from y.
     """
 
-    def __init__(self, trunk, state, G, sample0, save, dtype=torch.float32, join=None,
-                 side=None):
+    def __init__(self, trunk, state, G, sample0, save, dtype=torch.float32, join=None):
         super().__init__(state, G, sample0, save)
         self.trunk = trunk
         self.join = join  # caller's stream when this trunk runs on a stream of its own
-        self.side = side  # stream for the weight gradients of the backward
         self.dt = dtype   # activation / sampled-weight storage (fp32, bf16 or f16)
 
     def _cin_pad(self, Cin):
@@ -410,38 +384,26 @@ class TrunkRunner(_Runner):
         rec = (conv, x, x_strides, x_bn, w, B, H, W) if self.save else None
         return y, rec, part
 
-    def _conv_bwd(self, rec, dy, need_dx=True, addend=None, dx=None, accumulate=False,
-                  bn_out=None):
-        """bn_out: the _BN whose output gradient dx is (its partials come back as `pre`)."""
+    def _conv_bwd(self, rec, dy, need_dx=True, addend=None, dx=None, accumulate=False):
         conv, x, xs, x_bn, w, B, H, W = rec
         G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
         st, pd = conv.stride[0], conv.padding[0]
         cp = self._cin_pad(Cin)
         if conv.mu_kernel.requires_grad:
-            side = self.side
-            if side is not None:
-                side.wait_stream(torch.cuda.current_stream())
-                for t in (x, dy) + (tuple(x_bn[:2]) if x_bn is not None else ()):
-                    t.record_stream(side)
-            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-                splits = ops.wgrad_splits(G, B, H, W, cp, Cout, k, st, pd)
-                ws = torch.empty(splits, G, Cout, k * k * cp, device=dy.device)
-                ops.conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, cp, Cout, k, st, pd,
-                                      x_strides=xs, x_bn=x_bn, alg_cin=Cin)
-                self._reparam_bwd(conv, conv.mu_kernel, conv.rho_kernel, ws, splits, Cout, Cin,
-                                  k * k, "kernel", dw_cin=cp)
-                del ws
+            splits = ops.wgrad_splits(G, B, H, W, cp, Cout, k, st, pd)
+            ws = torch.empty(splits, G, Cout, k * k * cp, device=dy.device)
+            ops.conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, cp, Cout, k, st, pd,
+                                  x_strides=xs, x_bn=x_bn, alg_cin=Cin)
+            self._reparam_bwd(conv, conv.mu_kernel, conv.rho_kernel, ws, splits, Cout, Cin,
+                              k * k, "kernel", dw_cin=cp)
+            del ws
         if not need_dx:
-            return None, None
+            return None
         if dx is None:
             dx = torch.empty(G, B, H, W, Cin, device=dy.device, dtype=self.dt)
-        bn_args, pre = (None, None)
-        if DGRAD_BN_EPILOGUE and self.dt == torch.float32 and bn_out is not None \
-                and bn_out.batch_stats:
-            bn_args, pre = bn_out.epilogue_args(G, (B, H, W, Cin, Cout, k, st, pd))
         ops.conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, k, st, pd, addend=addend,
-                            accumulate=accumulate, bn=bn_args)
-        return dx, pre
+                            accumulate=accumulate)
+        return dx
 
     def _stem(self, conv, x, B, H, W):
         """conv1 over im2col rows of the images, shared by the G samples: one GEMM
@@ -517,7 +479,7 @@ class TrunkRunner(_Runner):
         self.last_lazy = (scale, shift, int(relu))  # for a consumer applying it on load
         return out, rec
 
-    def _bn_bwd(self, rec, dout, want_dres=False, pre=None):
+    def _bn_bwd(self, rec, dout, want_dres=False):
         if not rec.batch_stats:
             raise NotImplementedError("mauv: backward through eval-mode BN is not on the path "
                                       "(the reference trains and predicts in .train())")
@@ -529,11 +491,10 @@ class TrunkRunner(_Runner):
         db = bn.bias.grad if bn.bias.requires_grad else None
         s = rec.stats
         if rec.mask is not None:
-            assert pre is None
             ops.bn_bwd_mask(rec.y, rec.mask, dout, s[0], s[1], s[2], G, M, C, ws, dy, dres, dg, db)
         else:
             ops.bn_bwd(rec.y, rec.out, dout, rec.relu, s[0], s[1], s[2], G, M, C, ws, dy, dres,
-                       dg, db, shift=s[3], pre=pre)
+                       dg, db, shift=s[3])
         return dy, dres
 
     # ---- schedule ----
@@ -622,28 +583,26 @@ class TrunkRunner(_Runner):
         da = torch.empty(G, B, H, W, 2048, device=dout.device, dtype=self.dt)
         ops.avgpool_bwd(dfeat, G * B, H * W, 2048, da)
         del dfeat
-        pre = None  # bn3 partials of the block being entered (from the previous dgrad epilogue)
         while self.recs:
             r1, s1, r2, s2, r3, s3, rd, sd = self.recs.pop()
-            prev_bn3 = self.recs[-1][5] if self.recs else None  # BN whose output is this input
-            dy3, dres = self._bn_bwd(s3, da, want_dres=True, pre=pre)
+            dy3, dres = self._bn_bwd(s3, da, want_dres=True)
             del da, s3
-            da2, pre2 = self._conv_bwd(r3, dy3, bn_out=s2)
+            da2 = self._conv_bwd(r3, dy3)
             del dy3, r3
-            dy2, _ = self._bn_bwd(s2, da2, pre=pre2)
+            dy2, _ = self._bn_bwd(s2, da2)
             del da2, s2
-            da1, pre1 = self._conv_bwd(r2, dy2, bn_out=s1)
+            da1 = self._conv_bwd(r2, dy2)
             del dy2, r2
-            dy1, _ = self._bn_bwd(s1, da1, pre=pre1)
+            dy1, _ = self._bn_bwd(s1, da1)
             del da1, s1
             if rd is not None:
                 dyd, _ = self._bn_bwd(sd, dres)
                 del dres, sd
-                dx, _ = self._conv_bwd(r1, dy1)
-                _, pre = self._conv_bwd(rd, dyd, dx=dx, accumulate=True, bn_out=prev_bn3)
+                dx = self._conv_bwd(r1, dy1)
+                self._conv_bwd(rd, dyd, dx=dx, accumulate=True)
                 del dyd, rd
             else:
-                dx, pre = self._conv_bwd(r1, dy1, addend=dres, bn_out=prev_bn3)
+                dx = self._conv_bwd(r1, dy1, addend=dres)
                 del dres
             del dy1, r1
             da = dx
@@ -658,8 +617,6 @@ class TrunkRunner(_Runner):
             self._stem_bwd(rc, dy0)
         else:
             self._conv_bwd(rc, dy0, need_dx=False)
-        if self.side is not None:
-            torch.cuda.current_stream().wait_stream(self.side)
         if self.st.grad_ready_hook is not None:
             self.st.grad_ready_hook(self.trunk)
         if self.join is not None:   # the caller's stream (optimizer, all-reduce) waits for us
@@ -825,7 +782,7 @@ def _to_device(x, dev):
     return x if x.device == dev else x.to(dev, non_blocking=True)
 
 
-def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None, join=None, side=None):
+def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None, join=None):
     """[num_mc, B, 2048|C] for one ResNet trunk (root = the trunk unless ``state`` given)."""
     _check_trunk(trunk)
     st = state or root_state(trunk)
@@ -835,7 +792,7 @@ def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None, join=None, side=Non
     s0 = st.next_samples(num_mc) if sample0 is None else sample0
     params = list(trunk.parameters())
     save = needs_grad(params)
-    runner = TrunkRunner(trunk, st, num_mc, s0, save, st.trunk_dtype(), join, side)
+    runner = TrunkRunner(trunk, st, num_mc, s0, save, st.trunk_dtype(), join)
     x = _to_device(x, dev)
     if x.dtype != torch.float32:   # autocast callers may hand 16-bit images; stems read fp32
         x = x.float()
@@ -861,14 +818,13 @@ def run_multimodal_mc(model, inputs, bathy, sss, num_mc):
             and needs_grad(head_params):
         cur = torch.cuda.current_stream(dev)
         feats = []
-        for trunk, x, (ts, side) in zip(trunks, xs, _trunk_streams(dev)):
+        for trunk, x, ts in zip(trunks, xs, _trunk_streams(dev)):
             ts.wait_stream(cur)
             if x.is_cuda:
                 x.record_stream(ts)
             with torch.cuda.stream(ts):
-                feats.append(run_trunk_mc(trunk, x, num_mc, st, s0, join=cur,
-                                          side=side if SIDE_WGRAD else None))
-        for f, (ts, _) in zip(feats, _trunk_streams(dev)):
+                feats.append(run_trunk_mc(trunk, x, num_mc, st, s0, join=cur))
+        for f, ts in zip(feats, _trunk_streams(dev)):
             cur.wait_stream(ts)
             f.record_stream(cur)
         f_img, f_bathy, f_sss = feats

@@ -169,6 +169,59 @@ def test_unimodal_resnet50custom_parity():
     _assert_grads_as_accurate(list(m.parameters()), list(o.parameters()), list(o64.parameters()))
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+def test_two_channel_input_trunk(dt):
+    """A ResNet50Custom over 2-channel tiles (image_processing.py:62-65 can build 2-channel
+    bathymetry): the stems' im2col rows take any channel count (K = 2*49 padded to the GEMM's
+    K slice), in fp32 training (gradients included) and 16-bit forward."""
+    from oracle import model_ref
+    from oracle.bayes_ref import dnn_to_bnn as o_dnn_to_bnn
+    from mauv.models import ResNet50Custom
+    from mauv.layers import dnn_to_bnn
+    from mauv.engine import root_state, set_precision
+    from mauv.kl import get_kl_loss
+    from mauv import mchead
+    from tests.helpers import DEFAULT_PRIOR
+    torch.manual_seed(3)
+    o = model_ref.ResNet50Custom(2, 7)
+    o_dnn_to_bnn(o, DEFAULT_PRIOR)
+    m = ResNet50Custom(2, 7)
+    dnn_to_bnn(m, DEFAULT_PRIOR)
+    m.load_state_dict(o.state_dict())
+    m = m.cuda()
+    torch.manual_seed(4)
+    x = torch.randn(2, 2, 64, 64)
+    y = torch.tensor([1, 5])
+
+    def oracle_loss(model, d=torch.float32):
+        lg = torch.stack([model(x.to(d)) for _ in range(2)])
+        loss = F.cross_entropy(lg.mean(0), y) + 0.25 * bayes_ref.get_kl_loss(model) / 2
+        loss.backward()
+        return lg, loss
+
+    o_pre = copy.deepcopy(o)
+    bridge = EpsBridge(o, m, 17)
+    with bridge:
+        o_logits, loss_o = oracle_loss(o)
+    bridge.collect()
+    root_state(m).eps_provider = bridge.provider
+    if dt != torch.float32:
+        set_precision(m, dt)
+        with torch.no_grad():
+            logits = m.mc_forward(x.cuda(), 2)
+        d = (logits.double().cpu() - o_logits.detach().double()).abs().max().item()
+        assert d <= 5e-2 * max(1.0, o_logits.abs().max().item()), d
+        return
+    o64, _ = oracle64(o_pre, bridge.store, lambda mm: oracle_loss(mm, torch.float64))
+    logits = m.mc_forward(x.cuda(), 2)
+    _assert_close(logits, o_logits)
+    ce, _, _ = mchead.mc_mean_ce(logits, y.cuda())
+    loss = ce + 0.25 * get_kl_loss(m) / 2
+    assert abs(loss.item() - loss_o.item()) <= 1e-4 * abs(loss_o.item())
+    loss.backward()
+    _assert_grads_as_accurate(list(m.parameters()), list(o.parameters()), list(o64.parameters()))
+
+
 @pytest.mark.parametrize("N,chunk", [(5, 5), (7, 3)])
 def test_predict_uncertainty_parity(N, chunk):
     """Fused MC statistics (HIP) vs predictors.py maths on the oracle (fp32, no autocast);
