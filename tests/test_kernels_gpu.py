@@ -148,7 +148,7 @@ def test_stem_packed_nhwc4(cin, H, R):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16],
                          ids=["fp32", "bf16", "f16"])
-@pytest.mark.parametrize("cin,H,G", [(3, 20, 3), (1, 37, 4), (3, 33, 1), (1, 9, 5)])
+@pytest.mark.parametrize("cin,H,G", [(3, 20, 3), (1, 37, 4), (3, 33, 1), (1, 9, 5), (2, 21, 2)])
 def test_stem_im2col_gemm(dt, cin, H, G):
     """The stems as one GEMM over shared im2col rows (stem.hip): rows bit-exact against
     F.unfold, outputs / BN partials / weight gradient against float64 convolutions of the

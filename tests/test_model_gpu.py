@@ -199,19 +199,41 @@ def test_two_channel_input_trunk(dt):
         loss.backward()
         return lg, loss
 
+    if dt != torch.float32:
+        # 16-bit forward.  The unimodal logits (no fusion head to damp the features) of this
+        # random-init trunk move by 10-35 % of their range with bf16 rounding alone — torch's
+        # own autocast run of the oracle model on the GPU (same weights, same epsilons) moves
+        # them as much (measured 0.17-0.42 vs the HIP path's 0.19-0.67, f16 0.07-0.29 vs
+        # 0.05-0.11, tools/diag_uni16.py) — so the bar is that reference precision scheme:
+        # the HIP deviation from the fp32 oracle within 2x torch-autocast's
+        x16 = torch.randn(4, 2, 160, 160)
+        og = copy.deepcopy(o).cuda()
+        bridge = EpsBridge(o, m, 17)
+        with bridge, torch.no_grad():
+            o_logits = torch.stack([o(x16) for _ in range(2)])
+        log = list(bridge.src.log)
+        bridge.collect()
+        it = iter(log)
+        bayes_ref.set_eps_source(lambda layer, name, shape: next(it)[2])
+        try:
+            with torch.no_grad(), torch.autocast("cuda", dtype=dt):
+                t_logits = torch.stack([og(x16.cuda()) for _ in range(2)]).float().cpu()
+        finally:
+            bayes_ref.set_eps_source(None)
+        root_state(m).eps_provider = bridge.provider
+        set_precision(m, dt)
+        with torch.no_grad():
+            logits = m.mc_forward(x16.cuda(), 2)
+        d = (logits.double().cpu() - o_logits.double()).abs().max().item()
+        dt_ = (t_logits.double() - o_logits.double()).abs().max().item()
+        assert d <= 2.0 * dt_ + 1e-3 * o_logits.abs().max().item(), (d, dt_)
+        return
     o_pre = copy.deepcopy(o)
     bridge = EpsBridge(o, m, 17)
     with bridge:
         o_logits, loss_o = oracle_loss(o)
     bridge.collect()
     root_state(m).eps_provider = bridge.provider
-    if dt != torch.float32:
-        set_precision(m, dt)
-        with torch.no_grad():
-            logits = m.mc_forward(x.cuda(), 2)
-        d = (logits.double().cpu() - o_logits.detach().double()).abs().max().item()
-        assert d <= 5e-2 * max(1.0, o_logits.abs().max().item()), d
-        return
     o64, _ = oracle64(o_pre, bridge.store, lambda mm: oracle_loss(mm, torch.float64))
     logits = m.mc_forward(x.cuda(), 2)
     _assert_close(logits, o_logits)

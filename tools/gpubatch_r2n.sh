@@ -1,5 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u tools/diag_g9.py > gpurun_out/r2n_c.log 2>&1 || { tail -20 gpurun_out/r2n_c.log; exit 1; }
-MAUV_STEM_GEMM=0 timeout -k 10 300 python -u tools/diag_g9.py > gpurun_out/r2n_d.log 2>&1 || { tail -20 gpurun_out/r2n_d.log; exit 1; }
-head -4 gpurun_out/r2n_c.log; tail -7 gpurun_out/r2n_c.log; head -4 gpurun_out/r2n_d.log
+timeout -k 10 300 python -u -m pytest tests/test_model_gpu.py -m gpu -q --timeout 240 --timeout-method thread -k "two_channel" > gpurun_out/r2n_m.log 2>&1 || { tail -20 gpurun_out/r2n_m.log; exit 1; }
+tail -2 gpurun_out/r2n_m.log
