@@ -143,13 +143,15 @@ def cpu_baseline(args):
     return out
 
 
-def pmc_traffic():
-    """HBM bytes per conv_gemm launch from the committed PMC summary of this same command
+def pmc_traffic(family="fp32"):
+    """HBM bytes per conv launch from the committed PMC summary of this same command
     (tools/pmc_traffic.py; separate FETCH_SIZE and WRITE_SIZE passes, FETCH_SIZE doubled per
     MI355X_MICROARCH.md's gfx950 correction).  PMC collection serialises kernels, so it runs
-    as its own profiled invocation; the newest profiles/round*_conv_traffic.json is used."""
+    as its own profiled invocation; the newest profiles/round*_conv_traffic.json (fp32 split
+    convs) or round*_bf16_conv_traffic.json (the 16-bit family) is used."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "round*_conv_traffic.json")))
+    files = [f for f in files if ("_bf16_" in os.path.basename(f)) == (family == "bf16")]
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -157,7 +159,7 @@ def pmc_traffic():
     return d["bytes_per_launch"], os.path.relpath(files[-1], REPO)
 
 
-def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic=True, suffix="",
+def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic="fp32", suffix="",
                   kernel="conv_gemm_f32 (implicit-GEMM fwd+dgrad+wgrad, all launches of one step)"):
     """Roofline of one step's implicit-GEMM launches of one precision (suffix "" = fp32,
     "_bfloat16" = the 16-bit trunks; the fp32 fusion-head GEMMs are then excluded).  The
@@ -188,7 +190,7 @@ def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic=True, suffix="",
     tot_ms = sum(v[2] for v in by.values())
     n = sum(v[0] for v in by.values())
     achieved = tot_fl / (tot_ms * 1e-3) / 1e12
-    traffic, tsrc = pmc_traffic() if traffic else (None, None)
+    traffic, tsrc = pmc_traffic(traffic) if traffic else (None, None)
     return {
         "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -331,8 +333,9 @@ def main():
                           f"statistics, master weights, head), num_mc={args.num_mc}"}
         if not args.no_roofline:
             bf16["roofline"] = roofline_step(
-                step, peak=BF16_MFMA_PEAK_TF, traffic=False, suffix="_bfloat16",
-                kernel="conv_pipe16<bf16> (pipelined implicit-GEMM fwd+dgrad+wgrad; stems conv_gemm_h16), one step")
+                step, peak=BF16_MFMA_PEAK_TF, traffic="bf16", suffix="_bfloat16",
+                kernel="conv_pipe16<bf16> (pipelined implicit-GEMM fwd+dgrad+wgrad; stems as one "
+                       "GEMM over shared im2col rows), one step")
         set_precision(model.module if world > 1 else model,
                       torch.bfloat16 if args.dtype == "bf16" else None)
 
