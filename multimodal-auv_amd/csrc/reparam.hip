@@ -24,22 +24,21 @@ __global__ __launch_bounds__(256) void reparam_sample_kernel(
     const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
     uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS, int cin_pad,
     typename S::T* __restrict__ out, long long out_gs) {
-  // 32-bit index arithmetic (the host checks numel < 2^31): the OIHW -> KRSC decomposition
-  // costs two 32-bit divisions per element instead of 64-bit ones
-  const unsigned numel = (unsigned)(Cout * Cin * RS);
-  const unsigned nq = (numel + 3) / 4, crs = (unsigned)(Cin * RS);
-  for (unsigned q = blockIdx.x * 256u + threadIdx.x; q < nq; q += gridDim.x * 256u) {
+  const long long numel = (long long)Cout * Cin * RS;
+  const long long nq = (numel + 3) / 4;
+  for (long long q = blockIdx.x * 256LL + threadIdx.x; q < nq; q += (long long)gridDim.x * 256) {
     float m[4], s[4];
     long long dst[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const unsigned i = 4 * q + e;
+      const long long i = 4 * q + e;
       if (i < numel) {
         m[e] = mu[i];
         s[e] = softplus(rho[i]);
-        const unsigned o = i / crs, rem = i - o * crs;
-        const unsigned c = rem / (unsigned)RS, rs = rem - c * (unsigned)RS;
-        dst[e] = ((long long)o * RS + rs) * cin_pad + c;
+        const long long o = i / ((long long)Cin * RS);
+        const long long rem = i - o * Cin * RS;
+        const int c = (int)(rem / RS), rs = (int)(rem - (long long)c * RS);
+        dst[e] = (o * RS + rs) * cin_pad + c;
       } else {
         m[e] = 0.f; s[e] = 0.f; dst[e] = -1;
       }
@@ -70,17 +69,15 @@ __global__ __launch_bounds__(256) void reparam_sample_kernel(
 //       dmu += sum,  drho += sum_g d_g * eps_g' * sigmoid(rho).
 // Reference mode (fixed >= 0): one epsilon for every g, so drho += (sum_g d_g) * eps * sig —
 // one pass.  Exact mode: one pass per g.
-// input channels per block: 256 for 1x1 (RS = 1), 64 otherwise (<= 64*49 parameters); wider
-// blocks than the first cut (64 / 16) — the small ones left most of each block's threads idle
-// in the chain-rule pass and were launch/latency-bound (34.6 us average per layer)
-__host__ __device__ inline int rb_cb(int RS) { return RS == 1 ? 256 : 64; }
+// input channels per block: 64 for 1x1 (RS = 1), 16 otherwise (<= 16*49 parameters)
+__host__ __device__ inline int rb_cb(int RS) { return RS == 1 ? 64 : 16; }
 
 __global__ __launch_bounds__(256) void reparam_bwd_kernel(
     const float* __restrict__ dw, int splits, long long dw_gs, long long dw_ss,
     const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
     uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS, int cin_pad,
     float* __restrict__ dmu, float* __restrict__ drho, long long fixed) {
-  __shared__ float sd[64 * 49];   // [cb][RS]
+  __shared__ float sd[16 * 49];   // [cb][RS]
   __shared__ float red[4][64];
   const int o = blockIdx.x, tid = threadIdx.x;
   const int CB = rb_cb(RS);
@@ -221,7 +218,6 @@ MAUV_API int mauv_reparam_sample(const float* mu, const float* rho, const float*
                                  float* out, long long out_gstride, hipStream_t stream) {
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
-  if (numel >= (1LL << 31)) { set_error("reparam_sample: tensor too large"); return kErrArg; }
   hipLaunchKernelGGL(reparam_sample_kernel<SF32>, dim3(grid_for(nq)), dim3(256), 0, stream, mu,
                      rho, eps, seed, sample0, layer, G, Cout, Cin, RS, Cin, out,
                      out_gstride ? out_gstride : numel);
@@ -238,7 +234,6 @@ MAUV_API int mauv_reparam_sample_padded(const float* mu, const float* rho, const
   if (cin_pad < Cin) { set_error("reparam_sample_padded: cin_pad < Cin"); return kErrArg; }
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
-  if (numel >= (1LL << 31)) { set_error("reparam_sample: tensor too large"); return kErrArg; }
   hipLaunchKernelGGL(reparam_sample_kernel<SF32>, dim3(grid_for(nq)), dim3(256), 0, stream, mu,
                      rho, eps, seed, sample0, layer, G, Cout, Cin, RS, cin_pad, out,
                      out_gstride ? out_gstride : (long long)Cout * RS * cin_pad);
@@ -257,7 +252,6 @@ MAUV_API int mauv_reparam_sample_h16(int dtype, const float* mu, const float* rh
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
   const long long gs = out_gstride ? out_gstride : (long long)Cout * RS * cin_pad;
-  if (numel >= (1LL << 31)) { set_error("reparam_sample_h16: tensor too large"); return kErrArg; }
 #define L(D) hipLaunchKernelGGL(reparam_sample_kernel<S16<D>>, dim3(grid_for(nq)), dim3(256), 0, \
                                 stream, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS,   \
                                 cin_pad, (u16*)out, gs);
