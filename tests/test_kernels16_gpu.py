@@ -44,8 +44,8 @@ CASES = [
     (1, 4, 20, 64, 128, 3, 1, 1),   # 128 x 128 eight-wave tiles, ragged last m tile
     (2, 2, 15, 128, 64, 3, 2, 1),   # strided dgrad with Cout = 64, odd extents
     (1, 2, 6, 96, 64, 3, 1, 1),     # Cin % 64 != 0: the pipelined FWD declines, DGRAD/WGRAD run
-    (1, 2, 12, 256, 256, 3, 1, 1),  # N >= 256, M > 64: 128 x 256 tiles (fwd, dgrad)
-    (2, 3, 9, 64, 512, 1, 1, 0),    # 128 x 256 fwd tiles, ragged m, two n tiles
+    (1, 2, 12, 256, 256, 3, 1, 1),  # N >= 256, M > 64: two 128-wide n tiles (fwd, dgrad)
+    (2, 3, 9, 64, 512, 1, 1, 0),    # 128 x 128 fwd tiles, ragged m, four n tiles
 ]
 
 
