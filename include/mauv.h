@@ -92,8 +92,9 @@ int mauv_set_f32_math(int mode);
  * Same three GEMM views on v_mfma_f32_32x32x16_{bf16,f16}: dtype 0 = bf16 (BASELINE configs[2]
  * training), 1 = f16 (the reference predictor's torch.amp.autocast on a GPU,
  * inference/predictors.py:55).  x / w / y / dy / dx / addend are 16-bit words, statistics
- * partials and weight-gradient slabs fp32.  Cin and Cout must be multiples of 8 (the stems'
- * 1/3-channel inputs are zero-padded to 8 channels), dgrad needs Cout % 32 == 0; x strides
+ * partials and weight-gradient slabs fp32.  Cin and Cout must be multiples of 8 (the stems
+ * run as GEMMs over im2col rows, mauv_stem_*; their former 8-channel padded form remains
+ * valid), dgrad needs Cout % 32 == 0; x strides
  * are channel-contiguous multiples of 8.  Statistics partials: mauv_conv2d_fwd_stat_blocks. */
 int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_strides,
                         const float* x_scale, const float* x_shift, int x_relu, const void* w,
