@@ -65,6 +65,28 @@ def test_forward16_logits(dt):
 
 
 @pytest.mark.parametrize("dt", DTS, ids=["bf16", "f16"])
+def test_forward16_ragged_nonsquare(dt):
+    """16-bit forward on non-square tiles with sides off the 32 grid (ragged tiles in every
+    kernel and in the stems' im2col GEMM) vs the fp32 oracle, SURVEY §8c's bf16 row."""
+    from mauv.engine import root_state, set_precision
+    o, m = build_pair()
+    set_precision(m, dt)
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(3, 3, 100, 150, generator=g)
+    b = torch.rand(3, 3, 120, 90, generator=g)
+    b[:, 2] = 0
+    s = torch.rand(3, 1, 77, 131, generator=g)
+    bridge = EpsBridge(o, m, 23)
+    with bridge, torch.no_grad():
+        o_logits = torch.stack([o(x, b, s) for _ in range(2)])
+    bridge.collect()
+    root_state(m).eps_provider = bridge.provider
+    with torch.no_grad():
+        logits = m.mc_forward(*_cuda(x, b, s), 2)
+    _close16(logits, o_logits)
+
+
+@pytest.mark.parametrize("dt", DTS, ids=["bf16", "f16"])
 def test_train_step16(dt):
     """One 16-bit training step vs the fp32 oracle: logits / loss within the bf16 row; the
     fusion head's gradients (fp32 layers fed by 16-bit features) point the same way as the

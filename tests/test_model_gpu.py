@@ -96,6 +96,44 @@ def test_multimodal_train_step_parity(S_opt, S_son, B, N):
             assert int(bm) == int(obuf[n]) == N
 
 
+def test_ragged_nonsquare_train_step():
+    """Non-square tiles whose sides are no multiple of 32 (every layer's M and the stems'
+    output grids ragged against the 128 / 64-row tiles, odd stride-2 extents), B=3, N=2:
+    logits, loss and gradients against the oracle as in the square cases."""
+    from mauv.engine import root_state
+    from mauv.kl import get_kl_loss
+    from mauv import mchead
+    o, m = build_pair()
+    o_pre = copy.deepcopy(o)
+    g = torch.Generator().manual_seed(11)
+    B, N = 3, 2
+    x = torch.randn(B, 3, 100, 150, generator=g)
+    b = torch.rand(B, 3, 120, 90, generator=g)
+    b[:, 2] = 0
+    s = torch.rand(B, 1, 77, 131, generator=g)
+    y = torch.tensor([0, 3, 6])
+
+    def oracle_loss(model, dt=torch.float32):
+        lg = torch.stack([model(x.to(dt), b.to(dt), s.to(dt)) for _ in range(N)])
+        loss = F.cross_entropy(lg.mean(0), y) + bayes_ref.get_kl_loss(model) / B * 0.5
+        loss.backward()
+        return lg, loss
+
+    bridge = EpsBridge(o, m, 5)
+    with bridge:
+        o_logits, loss_o = oracle_loss(o)
+    bridge.collect()
+    o64, _ = oracle64(o_pre, bridge.store, lambda mm: oracle_loss(mm, torch.float64))
+    root_state(m).eps_provider = bridge.provider
+    logits = m.mc_forward(*_cuda(x, b, s), N)
+    _assert_close(logits, o_logits)
+    ce, _, _ = mchead.mc_mean_ce(logits, y.cuda())
+    loss = ce + get_kl_loss(m) / B * 0.5
+    assert abs(loss.item() - loss_o.item()) <= 1e-4 * abs(loss_o.item())
+    loss.backward()
+    _assert_grads_as_accurate(list(m.parameters()), list(o.parameters()), list(o64.parameters()))
+
+
 def test_exact_rho_gradient_mode():
     """rho_grad="exact" (per-sample eps) vs the oracle with non-aliased epsilons."""
     from mauv.engine import root_state, set_rho_grad_mode
