@@ -16,6 +16,8 @@
 // the fp32 accumulators and 16-bit rows staged through LDS (DGRAD: + addend / accumulate, parity
 // class row remap); WGRAD fp32 split-K slabs (conv_common.h).
 
+#include <stdlib.h>
+
 #include "conv_common.h"
 
 namespace mauv {
@@ -94,9 +96,15 @@ struct Waves16 {
   static constexpr int T = 64 * M * N, EU = 4;
 };
 
-template <int MODE, int DT, int BM, int BN, bool XBN, bool STEM>
+// ONE: short K (a few 64-deep stages, the 1x1 convs over 64-128 channels): one LDS buffer, one
+// register stage, stages run one after another, and a register budget low enough for three to
+// four blocks per CU instead of two — with one or two stages there is little of a next tile to
+// overlap inside a block, so more resident blocks are the cover for load and store latency
+// SHORT: 0 = the two-stage pipeline; 1 = exactly one stage (nt == 1, straight-line: 62 VGPRs,
+// up to four blocks per CU); 2 = short K through one buffer, stages one after another.
+template <int MODE, int DT, int BM, int BN, bool XBN, bool STEM, int SHORT = 0>
 __global__ __launch_bounds__((Waves16<BM, BN>::T))
-__attribute__((amdgpu_waves_per_eu(Waves16<BM, BN>::EU)))
+__attribute__((amdgpu_waves_per_eu(SHORT ? 6 : Waves16<BM, BN>::EU)))
 void conv_pipe16(const ConvArgs a) {
   constexpr int BK = 64, EPC = 8, KQ = BK / EPC;
   constexpr int WGM = Waves16<BM, BN>::M, WGN = Waves16<BM, BN>::N, NT = Waves16<BM, BN>::T;
@@ -113,10 +121,12 @@ void conv_pipe16(const ConvArgs a) {
   constexpr int STG = A_SZ + B_SZ;
   constexpr int XS = (XBN && MODE == FWD) ? 2 * kMaxXbn16 : 0;  // floats
   constexpr int DUM = (PA || PB) ? 8 * NT : 0;                 // dummy chunk slots (16-bit)
-  static_assert(2 * STG >= 2 * WM * (BN + 4) && 2 * STG >= 8 * WGM * BN, "epilogue scratch");
-  __shared__ __attribute__((aligned(16))) u16 smem[2 * STG + 2 * XS + DUM];
-  float* xbn = (float*)(smem + 2 * STG);
-  u16* dum = smem + 2 * STG + 2 * XS + 8 * threadIdx.x;
+  constexpr bool ONE = SHORT != 0;
+  constexpr int NBUF = ONE ? 1 : 2;
+  static_assert(NBUF * STG >= 2 * WM * (BN + 4) && NBUF * STG >= 8 * WGM * BN, "epilogue scratch");
+  __shared__ __attribute__((aligned(16))) u16 smem[NBUF * STG + 2 * XS + DUM];
+  float* xbn = (float*)(smem + NBUF * STG);
+  u16* dum = smem + NBUF * STG + 2 * XS + 8 * threadIdx.x;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
@@ -341,6 +351,25 @@ void conv_pipe16(const ConvArgs a) {
     }
   };
 
+  if constexpr (SHORT == 1) {  // nt == 1 (host-checked)
+    St S0;
+    load(S0, 0);
+    if constexpr (XBN && MODE == FWD) __syncthreads();  // xbn staged
+    store(S0, 0);
+    __syncthreads();
+    compute(0);
+    __syncthreads();  // the epilogue reuses the operand buffer
+  } else if constexpr (SHORT == 2) {  // short K: stages one after another through one buffer
+    St S0;
+    if constexpr (XBN && MODE == FWD) __syncthreads();  // xbn staged
+    for (int t = 0; t < nt; ++t) {
+      load(S0, t);
+      store(S0, 0);
+      __syncthreads();
+      compute(0);
+      __syncthreads();  // the next stage / the epilogue reuses the operand buffer
+    }
+  } else {
   // ---- pipeline: buffer 0 <- tile 0, registers S1 <- tile 1 ----
   St S0, S1;
   load(S0, 0);
@@ -363,6 +392,7 @@ void conv_pipe16(const ConvArgs a) {
   if (nt & 1) {
     compute(0);
     __syncthreads();  // the epilogue reuses the operand buffers
+  }
   }
 
   // ---------------- epilogue ----------------
@@ -439,7 +469,7 @@ void conv_pipe16(const ConvArgs a) {
   // one wave row wm per pass — then every thread writes 16-byte rows of 8 channels (residual
   // addend / previous dx added in fp32, one rounding)
   constexpr int SLD = BN + 4, CPR = BN / 8;
-  constexpr int PASSES = BM * SLD * 4 <= 2 * STG * 2 ? 1 : WGM, PR = BM / PASSES;
+  constexpr int PASSES = BM * SLD * 4 <= NBUF * STG * 2 ? 1 : WGM, PR = BM / PASSES;
   constexpr int NCH = PR * CPR;
   float* stile = (float*)smem;
   u16* outp = (u16*)a.out;
@@ -493,11 +523,20 @@ void conv_pipe16(const ConvArgs a) {
   }
 }
 
-template <int MODE, int DT, int BM, int BN, bool XBN, bool STEM = false>
+template <int MODE, int DT, int BM, int BN, bool XBN, bool STEM = false, int SHORT = 0>
 static void launch_pipe16(const ConvArgs& a, hipStream_t st) {
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
-  hipLaunchKernelGGL((conv_pipe16<MODE, DT, BM, BN, XBN, STEM>), grid, dim3(Waves16<BM, BN>::T), 0, st,
+  hipLaunchKernelGGL((conv_pipe16<MODE, DT, BM, BN, XBN, STEM, SHORT>), grid, dim3(Waves16<BM, BN>::T), 0, st,
                      a);
+}
+
+// forward launches with K <= MAUV_P16_SHORT_K (default 256; 0 = off) take the short-K kernels
+// (measured, tools/gpubatch_r2y.sh: f16 inference 11.03k -> 11.52k MC-samples/s, bf16
+// training 563 -> 582 triplets/s; K <= 64 alone: 11.30k / 585)
+static int short_k() {
+  static int k = -1;
+  if (k < 0) { const char* e = getenv("MAUV_P16_SHORT_K"); k = e ? atoi(e) : 256; }
+  return k;
 }
 
 template <int MODE, int DT, bool XBN, bool STEM>
@@ -506,6 +545,10 @@ static void pipe16_tiles(const ConvArgs& a, hipStream_t st) {
   if (bm == 64 && bn == 64) launch_pipe16<MODE, DT, 64, 64, XBN, STEM>(a, st);
   else if (bm == 64) launch_pipe16<MODE, DT, 64, 128, XBN, STEM>(a, st);
   else if (bn == 64) launch_pipe16<MODE, DT, 128, 64, XBN, STEM>(a, st);
+  else if (MODE == FWD && !STEM && a.K == 64 && short_k() >= 64)
+    launch_pipe16<MODE, DT, 128, 128, XBN, STEM, (MODE == FWD && !STEM) ? 1 : 0>(a, st);
+  else if (MODE == FWD && !STEM && a.K <= short_k())
+    launch_pipe16<MODE, DT, 128, 128, XBN, STEM, (MODE == FWD && !STEM) ? 2 : 0>(a, st);
   else launch_pipe16<MODE, DT, 128, 128, XBN, STEM>(a, st);
 }
 

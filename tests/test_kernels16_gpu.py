@@ -45,7 +45,10 @@ CASES = [
     (2, 2, 15, 128, 64, 3, 2, 1),   # strided dgrad with Cout = 64, odd extents
     (1, 2, 6, 96, 64, 3, 1, 1),     # Cin % 64 != 0: the pipelined FWD declines, DGRAD/WGRAD run
     (1, 2, 12, 256, 256, 3, 1, 1),  # N >= 256, M > 64: two 128-wide n tiles (fwd, dgrad)
-    (2, 3, 9, 64, 512, 1, 1, 0),    # 128 x 128 fwd tiles, ragged m, four n tiles
+    (2, 3, 9, 64, 512, 1, 1, 0),    # 128 x 128 fwd tiles, ragged m, four n tiles; K = 64:
+                                    # the one-stage forward kernel
+    (2, 3, 9, 128, 256, 1, 1, 0),   # K = 128 / 256: the short-K sequential forward kernel
+    (1, 3, 10, 256, 256, 1, 1, 0),
 ]
 
 
@@ -116,23 +119,27 @@ def test_conv16_stem_shared_padded_input(dt):
 
 @pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
 @pytest.mark.parametrize("Cout", [128, 256])
-def test_conv16_lazy_bn_input_and_stats(dt, Cout):
-    """x' = relu(x*scale + shift) applied on load (FWD and WGRAD) + epilogue statistics."""
+@pytest.mark.parametrize("Cin,R", [(64, 3), (64, 1), (128, 1)])
+def test_conv16_lazy_bn_input_and_stats(dt, Cout, Cin, R):
+    """x' = relu(x*scale + shift) applied on load (FWD and WGRAD) + epilogue statistics
+    (3x3: the two-stage pipeline; 1x1 over 64 / 128 channels: the one-stage and short-K
+    forward kernels)."""
     from mauv import ops
-    G, B, H, Cin = 2, 3, 8, 64
+    G, B, H = 2, 3, 8
     torch.manual_seed(3)
     x = torch.randn(G, B, H, H, Cin).to(dt)
     sc = torch.rand(G, Cin) + 0.5
     sh = torch.randn(G, Cin) * 0.3
-    w = (torch.randn(G, Cout, 3, 3, Cin) / 24).to(dt)
+    pd = R // 2
+    w = (torch.randn(G, Cout, R, R, Cin) / (8 * R)).to(dt)
     xt = torch.relu(x.float() * sc[:, None, None, None] + sh[:, None, None, None]).to(dt)
-    ref = ref_conv(xt, w, 1, 1)
-    nblk = ops.fwd_stat_blocks(G, B, H, H, Cin, Cout, 3, 1, 1)
+    ref = ref_conv(xt, w, 1, pd)
+    nblk = ops.fwd_stat_blocks(G, B, H, H, Cin, Cout, R, 1, pd)
     pm = torch.empty(G, nblk, Cout, device=dev)
     pm2 = torch.empty_like(pm)
     pc = torch.empty(G, nblk, device=dev)
     y = torch.empty(G, B, H, H, Cout, device=dev, dtype=dt)
-    ops.conv2d_fwd(x.to(dev), w.to(dev), y, G, B, H, H, Cin, Cout, 3, 1, 1,
+    ops.conv2d_fwd(x.to(dev), w.to(dev), y, G, B, H, H, Cin, Cout, R, 1, pd,
                    x_bn=(sc.to(dev), sh.to(dev), 1), stats=(pm, pm2, pc))
     close(y, ref, 2 * ULP[dt])
     # merged partials = mean / M2 of the fp32 (pre-rounding) output
@@ -143,17 +150,17 @@ def test_conv16_lazy_bn_input_and_stats(dt, Cout):
     close(mu, r.mean(1), 1e-4)
     close(m2 / r.shape[1], r.var(1, unbiased=False), 1e-3)
     dy = torch.randn(G, B, H, H, Cout).to(dt)
-    splits = ops.wgrad_splits(G, B, H, H, Cin, Cout, 3, 1, 1)
-    ws = torch.empty(splits, G, Cout, 9 * Cin, device=dev)
-    ops.conv2d_bwd_weight(x.to(dev), dy.to(dev), ws, splits, G, B, H, H, Cin, Cout, 3, 1, 1,
+    splits = ops.wgrad_splits(G, B, H, H, Cin, Cout, R, 1, pd)
+    ws = torch.empty(splits, G, Cout, R * R * Cin, device=dev)
+    ops.conv2d_bwd_weight(x.to(dev), dy.to(dev), ws, splits, G, B, H, H, Cin, Cout, R, 1, pd,
                           x_bn=(sc.to(dev), sh.to(dev), 1))
     dw = []
     for g in range(G):
         wg = w[g].permute(0, 3, 1, 2).double().requires_grad_(True)
-        F.conv2d(xt[g].permute(0, 3, 1, 2).double(), wg, padding=1).backward(
+        F.conv2d(xt[g].permute(0, 3, 1, 2).double(), wg, padding=pd).backward(
             dy[g].permute(0, 3, 1, 2).double())
         dw.append(wg.grad.permute(0, 2, 3, 1))
-    close(ws.sum(0).view(G, Cout, 3, 3, Cin), torch.stack(dw), 1e-3)
+    close(ws.sum(0).view(G, Cout, R, R, Cin), torch.stack(dw), 1e-3)
 
 
 @pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
