@@ -78,9 +78,13 @@ __device__ __forceinline__ int row_of(int idx) {
   return (idx >> 6) * 16 + 8 * (l >> 5) + 2 * ((l >> 2) & 3) + ((l >> 4) & 1);
 }
 
-template <int MODE, int BM, int BN, bool XBN, bool ONEACC, int WV, bool STEM = false>
+// SEQ: short K (the 1x1 forwards over <= 256 channels): one register stage and one LDS buffer,
+// stages one after another, a register budget for three blocks per CU instead of two (the
+// 16-bit kernel's short-K variant, conv_pipe16.hip)
+template <int MODE, int BM, int BN, bool XBN, bool ONEACC, int WV, bool STEM = false,
+          bool SEQ = false>
 __global__ __launch_bounds__((SplitWaves<BM, BN, WV>::T))
-__attribute__((amdgpu_waves_per_eu(SplitWaves<BM, BN, WV>::EU)))
+__attribute__((amdgpu_waves_per_eu(SEQ ? 6 : SplitWaves<BM, BN, WV>::EU)))
 void conv_split_f32(const ConvArgs a) {
   constexpr int BK = 16;
   constexpr int WGM = SplitWaves<BM, BN, WV>::M, WGN = SplitWaves<BM, BN, WV>::N;
@@ -99,10 +103,11 @@ void conv_split_f32(const ConvArgs a) {
   constexpr int STG = 3 * (A_PL + B_PL);
   constexpr int XS = (XBN && MODE == FWD) ? 2 * kMaxXbn : 0;  // floats
   constexpr int DUM = (PA || PB) ? 12 * NT : 0;                // dummy plane slots (16-bit)
-  static_assert(2 * STG >= 8 * BN, "epilogue scratch");
-  __shared__ __attribute__((aligned(16))) u16 smem[2 * STG + 2 * XS + DUM];
-  float* xbn = (float*)(smem + 2 * STG);
-  u16* dum = smem + 2 * STG + 2 * XS + 12 * threadIdx.x;
+  constexpr int NBUF = SEQ ? 1 : 2;
+  static_assert(NBUF * STG >= 8 * BN, "epilogue scratch");
+  __shared__ __attribute__((aligned(16))) u16 smem[NBUF * STG + 2 * XS + DUM];
+  float* xbn = (float*)(smem + NBUF * STG);
+  u16* dum = smem + NBUF * STG + 2 * XS + 12 * threadIdx.x;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
@@ -357,6 +362,17 @@ void conv_split_f32(const ConvArgs a) {
       }
   };
 
+  if constexpr (SEQ) {
+    St S0;
+    if constexpr (XBN && MODE == FWD) __syncthreads();  // xbn staged
+    for (int t = 0; t < nt; ++t) {
+      load(S0, t);
+      split_store(S0, 0);
+      __syncthreads();
+      compute(0);
+      __syncthreads();  // the next stage / the epilogue scratch reuses the buffer
+    }
+  } else {
   // ---- pipeline: buffer 0 <- tile 0, registers S1 <- tile 1 ----
   St S0, S1;
   load(S0, 0);
@@ -376,6 +392,7 @@ void conv_split_f32(const ConvArgs a) {
     split_store(S0, 0);
     __syncthreads();
   }
+  }
 
   if constexpr (!ONEACC) {
 #pragma unroll
@@ -386,12 +403,12 @@ void conv_split_f32(const ConvArgs a) {
   conv_epilogue<MODE, BM, BN, MI, NI, WGM, WGN>(a, acc, (float*)smem, tid, m0, n0, g, sp);
 }
 
-template <int MODE, int BM, int BN, bool XBN, int WV = 4, bool STEM = false>
+template <int MODE, int BM, int BN, bool XBN, int WV = 4, bool STEM = false, bool SEQ = false>
 static void launch_split(const ConvArgs& a, int oneacc, hipStream_t st) {
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
   const dim3 block(SplitWaves<BM, BN, WV>::T);
   if constexpr (WV == 8) {  // one accumulator set (128-VGPR budget)
-    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV, STEM>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV, STEM, SEQ>), grid, block, 0, st, a);
   } else {
     if (oneacc)
       hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV, STEM>), grid, block, 0, st, a);
@@ -399,6 +416,13 @@ static void launch_split(const ConvArgs& a, int oneacc, hipStream_t st) {
       hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, false, WV, STEM>), grid, block, 0, st,
                          a);
   }
+}
+
+// forward launches with K <= MAUV_SPLIT_SHORT_K (default 256; 0 = off) take the SEQ kernel
+static int split_short_k() {
+  static int k = -1;
+  if (k < 0) { const char* e = getenv("MAUV_SPLIT_SHORT_K"); k = e ? atoi(e) : 256; }
+  return k;
 }
 
 template <int MODE, bool XBN>
@@ -427,6 +451,12 @@ static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
   // waves (MAUV_SPLIT_W8=0 restores those, 1 keeps four waves on the 64-wide tiles)
   static int w8 = -1;
   if (w8 < 0) { const char* e8 = getenv("MAUV_SPLIT_W8"); w8 = e8 ? atoi(e8) : 2; }
+  if constexpr (MODE == FWD) {
+    if (w8 && bm == 128 && bn == 128 && a.K <= split_short_k()) {
+      launch_split<MODE, 128, 128, XBN, 8, false, true>(a, oneacc, st);
+      return;
+    }
+  }
   if (w8 && bm == 128 && bn == 128) { launch_split<MODE, 128, 128, XBN, 8>(a, oneacc, st); return; }
   if (w8 == 2 && bm == 128 && bn == 64) { launch_split<MODE, 128, 64, XBN, 8>(a, oneacc, st); return; }
   if (w8 == 2 && bm == 64 && bn == 128) { launch_split<MODE, 64, 128, XBN, 8>(a, oneacc, st); return; }

@@ -29,6 +29,8 @@ CONV_CASES = [
     (1, 2, 8, 256, 512, 1, 2, 0),
     (2, 2, 4, 512, 2048, 1, 1, 0),
     (3, 2, 5, 64, 256, 1, 1, 0),
+    (2, 3, 9, 64, 256, 1, 1, 0),     # 1x1 forwards with K <= 256 on 128 x 128 tiles: the
+    (1, 3, 10, 256, 128, 1, 1, 0),   # split kernel's short-K (SEQ) variant
 ]
 
 
@@ -73,6 +75,49 @@ def test_conv_fwd_dgrad_wgrad(case):
     ws = torch.empty(splits, G, Cout, R * R * Cin, device=dev)
     ops.conv2d_bwd_weight(x.to(dev), dy.to(dev), ws, splits, G, B, H, H, Cin, Cout, R, st, pad)
     close(ws.sum(0).view(G, Cout, R, R, Cin), torch.stack(dw_ref))
+
+
+@pytest.mark.parametrize("Cin,R", [(64, 3), (64, 1), (128, 1), (256, 1)])
+def test_conv_lazy_bn_input_and_stats(Cin, R):
+    """fp32 convs with the producing BN + ReLU applied on load (FWD and WGRAD) and the
+    epilogue statistics: the two-stage split kernel (3x3) and its short-K variant (1x1)."""
+    from mauv import ops
+    G, B, H, Cout = 2, 3, 8, 128
+    pd = R // 2
+    torch.manual_seed(4)
+    x = torch.randn(G, B, H, H, Cin)
+    sc = torch.rand(G, Cin) + 0.5
+    sh = torch.randn(G, Cin) * 0.3
+    w = torch.randn(G, Cout, R, R, Cin) / (8 * R)
+    xt = torch.relu(x * sc[:, None, None, None] + sh[:, None, None, None])
+    ref = _ref_conv(xt, w, 1, pd)
+    nblk = ops.fwd_stat_blocks(G, B, H, H, Cin, Cout, R, 1, pd)
+    pm = torch.empty(G, nblk, Cout, device=dev)
+    pm2 = torch.empty_like(pm)
+    pc = torch.empty(G, nblk, device=dev)
+    y = torch.empty(G, B, H, H, Cout, device=dev)
+    xbn = (sc.to(dev), sh.to(dev), 1)
+    ops.conv2d_fwd(x.to(dev), w.to(dev), y, G, B, H, H, Cin, Cout, R, 1, pd, x_bn=xbn,
+                   stats=(pm, pm2, pc))
+    close(y, ref)
+    n = pc.double().cpu()
+    mu = (pm.double().cpu() * n[..., None]).sum(1) / n.sum(1, keepdim=True)
+    m2 = (pm2.double().cpu() + n[..., None] * (pm.double().cpu() - mu[:, None]) ** 2).sum(1)
+    r = ref.reshape(G, -1, Cout)
+    close(mu, r.mean(1))
+    close(m2 / r.shape[1], r.var(1, unbiased=False), rtol=1e-4)
+    dy = torch.randn(G, B, H, H, Cout)
+    splits = ops.wgrad_splits(G, B, H, H, Cin, Cout, R, 1, pd)
+    ws = torch.empty(splits, G, Cout, R * R * Cin, device=dev)
+    ops.conv2d_bwd_weight(x.to(dev), dy.to(dev), ws, splits, G, B, H, H, Cin, Cout, R, 1, pd,
+                          x_bn=xbn)
+    dw = []
+    for g in range(G):
+        wg = w[g].permute(0, 3, 1, 2).double().requires_grad_(True)
+        F.conv2d(xt[g].permute(0, 3, 1, 2).double(), wg, padding=pd).backward(
+            dy[g].permute(0, 3, 1, 2).double())
+        dw.append(wg.grad.permute(0, 2, 3, 1))
+    close(ws.sum(0).view(G, Cout, R, R, Cin), torch.stack(dw))
 
 
 @pytest.mark.parametrize("cin", [3, 1])
