@@ -83,9 +83,16 @@ def main():
             key = (Cin, Cout, R, st, pd, H)
             Ho = ops.out_hw(H, R, st, pd)
             fl = 2.0 * G * B * Ho * Ho * Cout * R * R * Cin
+            esz = 4 if a.dtype == "fp32" else 2
+            # algorithmic HBM bytes of one launch: each operand read once, the output written once
+            # (wgrad: its fp32 split-K slabs are written once)
+            nx, ny, nw = G * B * H * H * Cin, G * B * Ho * Ho * Cout, G * Cout * R * R * Cin
+            sp_ = ops.wgrad_splits(G, B, H, H, Cin, Cout, R, st, pd)
+            byt = {"fwd": esz * (nx + nw + ny), "dgrad": esz * (ny + nw + nx),
+                   "wgrad": esz * (nx + ny) + 4 * sp_ * nw}
             if key in cache:
                 for kind, ms in cache[key]:
-                    rows.append((trunk, name, kind, key, ms, fl))
+                    rows.append((trunk, name, kind, key, ms, fl, byt[kind]))
                 continue
             res = []
             if dt != torch.float32 and Cin % 8:
@@ -122,16 +129,22 @@ def main():
             torch.cuda.empty_cache()
             cache[key] = res
             for kind, ms in res:
-                rows.append((trunk, name, kind, key, ms, fl))
-    tot = defaultdict(lambda: [0.0, 0.0])
+                rows.append((trunk, name, kind, key, ms, fl, byt[kind]))
+    # per-launch roofline time: max(flops / MFMA peak, algorithmic bytes / HBM peak)
+    peak = 2.5e15 / 6 if a.dtype == "fp32" else 2.5e15
+    tot = defaultdict(lambda: [0.0, 0.0, 0.0])
     for r in rows:
         tot[r[2]][0] += r[4]
         tot[r[2]][1] += r[5]
-    print(f"{'trunk':6s} {'layer':10s} {'pass':6s} {'Cin,Cout,R,s,p,H':28s} {'ms':>8s} {'TF/s':>7s}")
+        tot[r[2]][2] += max(r[5] / peak, r[6] / 8e12) * 1e3
+    print(f"{'trunk':6s} {'layer':10s} {'pass':6s} {'Cin,Cout,R,s,p,H':28s} {'ms':>8s} {'TF/s':>7s} {'GB/s':>7s} {'roof':>5s}")
     for r in sorted(rows, key=lambda r: -r[4])[:a.top]:
-        print(f"{r[0]:6s} {r[1]:10s} {r[2]:6s} {str(r[3]):28s} {r[4]:8.3f} {r[5] / r[4] / 1e9:7.1f}")
-    for k, (ms, fl) in tot.items():
-        print(f"TOTAL {k:6s}: {ms:8.2f} ms  {fl / 1e12:8.2f} TFLOP  {fl / ms / 1e9:6.1f} TF/s")
+        rt = max(r[5] / peak, r[6] / 8e12) * 1e3
+        print(f"{r[0]:6s} {r[1]:10s} {r[2]:6s} {str(r[3]):28s} {r[4]:8.3f} {r[5] / r[4] / 1e9:7.1f} "
+              f"{r[6] / r[4] / 1e6:7.0f} {rt / r[4]:5.2f}")
+    for k, (ms, fl, rt) in tot.items():
+        print(f"TOTAL {k:6s}: {ms:8.2f} ms  {fl / 1e12:8.2f} TFLOP  {fl / ms / 1e9:6.1f} TF/s  "
+              f"roofline {rt:7.2f} ms ({rt / ms:.2f})")
     allms = sum(v[0] for v in tot.values())
     allfl = sum(v[1] for v in tot.values())
     print(f"TOTAL all   : {allms:8.2f} ms  {allfl / allms / 1e9:6.1f} TF/s")
