@@ -50,7 +50,39 @@ struct ConvArgs {
   // column n belongs to group n / cpg, channel n % cpg; outputs and BN statistics go to that
   // group's tensors ([G][M][cpg], [G][nblk][cpg]).  0 = off.
   int cpg;
+  // block order over the whole grid (1, default) or over blockIdx.x only (0): see conv_block_tile
+  int xcd_grid;
 };
+
+// XCD-aware block -> (tile, group / split-K slice) map.  Blocks are dealt round-robin over the 8
+// XCDs by their LINEAR id (blockIdx.x + gridDim.x * blockIdx.y; MI355X_MICROARCH.md, workgroup
+// dispatch), so blocks l and l + 8 share an L2.  The linear ids of one XCD are given one
+// contiguous range of the logical order (tiles m-major within a group / split-K slice, then the
+// next slice): the column tiles of one row tile, and all tiles of one weight-gradient slice,
+// share an XCD and its L2 instead of being dealt to eight.  xcd_grid = 0 restores the round-1
+// order over blockIdx.x only (which puts every group's / slice's tiles on all eight XCDs
+// whenever gridDim.x is a multiple of 8, and scatters them when it is not).
+template <int BM, int BN>
+__device__ __forceinline__ void conv_block_tile(const ConvArgs& a, int& m0, int& n0, int& by) {
+  const int nN = (a.N + BN - 1) / BN;
+  int L;
+  if (a.xcd_grid) {
+    const int nx = gridDim.x, tot = nx * gridDim.y;
+    const int lin = blockIdx.x + nx * blockIdx.y, xcd = lin & 7, q = tot >> 3, r = tot & 7;
+    const int Lg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (lin >> 3);
+    by = Lg / nx;
+    L = Lg - by * nx;
+  } else {
+    const int b = blockIdx.x, nwg = gridDim.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    by = blockIdx.y;
+  }
+  m0 = (L / nN) * BM;
+  n0 = (L - (L / nN) * nN) * BN;
+}
+
+// MAUV_XCD_GRID (default 1): conv_block_tile's order
+int conv_xcd_grid();
 
 // output element (row, col) of a FWD/DGRAD epilogue, relative to the block's group base
 __device__ __forceinline__ long long conv_out_index(const ConvArgs& a, long long orow, int col) {

@@ -758,13 +758,35 @@ MAUV_API int mauv_conv2d_wgrad_splits(int G, int B, int H, int W, int Cin, int C
   const int N = R * S * Cin;
   const long long tiles = (long long)ceil_div(Cout, Cout <= 64 ? 64 : 128) *
                           ceil_div(N, N <= 64 ? 64 : 128) * G;
-  // target >= ~1024 workgroups, but keep >= 256 pixels per split
-  long long splits = (1024 + tiles - 1) / tiles;
-  const long long maxs = (P + 255) / 256;
-  if (splits > maxs) splits = maxs;
-  if (splits < 1) splits = 1;
-  if (splits > 256) splits = 256;
-  return (int)splits;
+  // keep >= 256 pixels per split; at most 256 splits
+  long long maxs = (P + 255) / 256;
+  if (maxs > 256) maxs = 256;
+  if (maxs < 1) maxs = 1;
+  // The weight-gradient kernels run two blocks per CU: 512 resident blocks on the 256 CUs.  The
+  // round-1 rule (the fewest splits giving >= 1024 blocks) landed every trunk launch at
+  // 1025-1440 blocks, i.e. a third block round holding 0.2-40 % of a round.  Take, among the
+  // split counts giving one to three rounds (>= one full round where the pixels allow it), the
+  // fewest splits whose last round is filled within 5 % of the best fill (fewer splits: fewer
+  // fp32 slab bytes).  MAUV_WGRAD_SPLITS=0 restores the round-1 rule.
+  static int mode = -1;
+  if (mode < 0) { const char* e = getenv("MAUV_WGRAD_SPLITS"); mode = e ? atoi(e) : 1; }
+  if (mode == 0) {
+    long long splits = (1024 + tiles - 1) / tiles;
+    if (splits > maxs) splits = maxs;
+    return (int)(splits < 1 ? 1 : splits);
+  }
+  const long long slots = 512;
+  const long long lo = tiles * maxs < slots ? maxs : (slots + tiles - 1) / tiles;
+  auto fill = [&](long long s) {
+    const long long nb = tiles * s, rounds = (nb + slots - 1) / slots;
+    return (double)nb / (double)(rounds * slots);
+  };
+  double top = 0.0;
+  for (long long s = lo; s <= maxs && (s == lo || tiles * s <= 3 * slots); ++s) top = fmax(top, fill(s));
+  long long best = lo;
+  for (long long s = lo; s <= maxs && (s == lo || tiles * s <= 3 * slots); ++s)
+    if (fill(s) >= top - 0.05) { best = s; break; }
+  return (int)best;
 }
 
 // Weight gradient partial slabs: ws[split][g][Cout][R*S*Cin] (reduced by mauv_reparam_bwd).

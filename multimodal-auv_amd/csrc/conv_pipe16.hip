@@ -130,17 +130,11 @@ void conv_pipe16(const ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
-  int m0, n0;
-  {  // XCD-aware tile order (conv_gemm.hip)
-    const int nN = (a.N + BN - 1) / BN;
-    const int b = blockIdx.x, nwg = gridDim.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
-    const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-    m0 = (L / nN) * BM;
-    n0 = (L - (L / nN) * nN) * BN;
-  }
+  int m0, n0, by;
+  conv_block_tile<BM, BN>(a, m0, n0, by);  // XCD-aware order over the whole grid
   int g, sp = 0;
-  if constexpr (MODE == WGRAD) { g = blockIdx.y / a.splits; sp = blockIdx.y % a.splits; }
-  else g = blockIdx.y;
+  if constexpr (MODE == WGRAD) { g = by / a.splits; sp = by % a.splits; }
+  else g = by;
   int kbeg = 0, kend = a.K;
   if constexpr (MODE == WGRAD) { kbeg = sp * a.kchunk; kend = min(a.K, kbeg + a.kchunk); }
   // STEM (FWD, Cin = 8, S <= 8): stage r holds the S taps of filter row r as 8 pixel chunks
@@ -569,6 +563,7 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
   if (nx > lim || (mode != FWD && ny > lim) || a0.ws_g > lim) return false;
   const bool xs8 = a0.xs_w % 8 == 0 && a0.xs_h % 8 == 0 && a0.xs_b % 8 == 0 && a0.xs_g % 8 == 0;
   ConvArgs a = a0;
+  a.xcd_grid = conv_xcd_grid();
   if (mode == FWD) {
     if (a.Cin == 8 && a.S <= 8 && a.xs_w == 8 && !a.xsc && a.xs_h % 8 == 0 && a.xs_b % 8 == 0 &&
         a.xs_g % 8 == 0) {  // the stems: 7x7 taps over 8 zero-padded input channels

@@ -111,17 +111,11 @@ void conv_split_f32(const ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
-  int m0, n0;
-  {  // XCD-aware tile order (conv_gemm.hip)
-    const int nN = (a.N + BN - 1) / BN;
-    const int b = blockIdx.x, nwg = gridDim.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
-    const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-    m0 = (L / nN) * BM;
-    n0 = (L - (L / nN) * nN) * BN;
-  }
+  int m0, n0, by;
+  conv_block_tile<BM, BN>(a, m0, n0, by);  // XCD-aware order over the whole grid
   int g, sp = 0;
-  if constexpr (MODE == WGRAD) { g = blockIdx.y / a.splits; sp = blockIdx.y % a.splits; }
-  else g = blockIdx.y;
+  if constexpr (MODE == WGRAD) { g = by / a.splits; sp = by % a.splits; }
+  else g = by;
   int kbeg = 0, kend = a.K;
   if constexpr (MODE == WGRAD) { kbeg = sp * a.kchunk; kend = min(a.K, kbeg + a.kchunk); }
   // STEM (FWD, Cin = 4 zero-padded channels, xs_w = 4): the taps of one filter row as pixel
@@ -418,6 +412,12 @@ static void launch_split(const ConvArgs& a, int oneacc, hipStream_t st) {
   }
 }
 
+int conv_xcd_grid() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("MAUV_XCD_GRID"); v = e ? atoi(e) : 1; }
+  return v;
+}
+
 // forward launches with K <= MAUV_SPLIT_SHORT_K (default 256; 0 = off) take the SEQ kernel
 static int split_short_k() {
   static int k = -1;
@@ -472,6 +472,7 @@ bool conv_split_launch(int mode, const ConvArgs& a0, int oneacc, hipStream_t st)
   // (the FWD output is stored through plain pointers: only dgrad / wgrad read y by rsrc)
   if (nx > lim || (mode != FWD && ny > lim) || a0.ws_g > lim) return false;
   ConvArgs a = a0;
+  a.xcd_grid = conv_xcd_grid();
   if (mode == FWD && a.Cin == 4 && a.S <= 8 && a.xs_c == 1 && a.xs_w == 4 && !a.xsc &&
       a.xs_h % 4 == 0 && a.xs_b % 4 == 0 && a.xs_g % 4 == 0 && a.N == 64) {
     // the stems over 4 zero-padded input channels (mauv_pack_nchw_f32)

@@ -62,6 +62,9 @@ def main():
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "f16"])
     ap.add_argument("--xpad", type=int, default=0,
                     help="FWD: store x with a row pitch of Cin + xpad channels (strided loads)")
+    ap.add_argument("--mark", action="store_true",
+                    help="launch a torch.flip marker kernel before each timed pass and print "
+                         "'MARK' lines (per-shape PMC traffic: tools/shape_traffic.py)")
     ap.add_argument("--fused", action="store_true",
                     help="as in the model: BN+ReLU applied on load (fwd, wgrad) and BN "
                          "statistics partials from the fwd epilogue")
@@ -73,6 +76,17 @@ def main():
     kinds = a.only.split(",")
     rows = []
     cache = {}
+    marker = torch.zeros(2, device=dev)
+    nmark = [0]
+
+    def mark(trunk, name, kind, key, nbytes):
+        if a.mark:
+            torch.cuda.synchronize()
+            torch.flip(marker, [0])
+            torch.cuda.synchronize()
+            print(f"MARK {nmark[0]} {trunk} {name} {kind} {','.join(map(str, key))} {nbytes} "
+                  f"{REPS + 1}", flush=True)
+            nmark[0] += 1
     for trunk, cin, S in (("opt", 3, 224), ("bathy", 3, 256), ("sss", 1, 256)):
         if trunk not in a.trunks:
             continue
@@ -112,16 +126,19 @@ def main():
                 stats = (torch.empty(G, nblk, Cout, device=dev), torch.empty(G, nblk, Cout, device=dev),
                          torch.empty(G, nblk, device=dev))
             if "fwd" in kinds:
+                mark(trunk, name, "fwd", key, byt["fwd"])
                 res.append(("fwd", timeit(lambda: ops.conv2d_fwd(xfull if a.xpad else x, w, y, G, B, H, H, Cin, Cout, R, st, pd,
                                                                  x_bn=xbn, stats=stats,
                                                                  x_strides=xstr))))
             if "dgrad" in kinds and name != "stem" and (dt == torch.float32 or Cout % 32 == 0):
                 dx = torch.empty_like(x)
+                mark(trunk, name, "dgrad", key, byt["dgrad"])
                 res.append(("dgrad", timeit(lambda: ops.conv2d_bwd_data(y, w, dx, G, B, H, H, Cin, Cout, R, st, pd))))
                 del dx
             if "wgrad" in kinds:
                 sp = ops.wgrad_splits(G, B, H, H, Cin, Cout, R, st, pd)
                 ws = torch.empty(sp, G, Cout, R * R * Cin, device=dev)
+                mark(trunk, name, "wgrad", key, byt["wgrad"])
                 res.append(("wgrad", timeit(lambda: ops.conv2d_bwd_weight(x, y, ws, sp, G, B, H, H, Cin, Cout, R, st, pd,
                                                                           x_bn=xbn))))
                 del ws
