@@ -35,6 +35,7 @@ for _p in (REPO, os.path.join(REPO, "multimodal-auv_amd")):
 METRIC = "triplets/sec training + MC-samples/sec inference, 7-class BNN, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md: f32-in MFMA = vector peak (spec)
 BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: dense bf16/f16 MFMA (no sparsity)
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E
 # fp32 GEMM arithmetic of the convs (include/mauv.h mauv_set_f32_math): "split" issues six
 # bf16 MFMA plane products per fp32 product, "exact" one f32 MFMA
 F32_PEAK_TF = {"split": BF16_MFMA_PEAK_TF / 6, "split1": BF16_MFMA_PEAK_TF / 6,
@@ -177,10 +178,16 @@ def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic="fp32", suffix="",
     rows, ops.PROFILE = ops.PROFILE, None
     by = {}
     nbytes = 0.0
+    roof_ms, n_hbm = 0.0, 0
     for kind, fl, nb, nl, e0, e1 in rows:
         if (suffix and not kind.endswith(suffix)) or (not suffix and "_" in kind):
             continue
         ms = e0.elapsed_time(e1)
+        # this launch's own roofline time: its FLOPs at the MFMA peak or its algorithmic bytes
+        # at the HBM peak, whichever is longer
+        t_fl, t_hbm = fl / (peak * 1e12) * 1e3, nb / (HBM_PEAK_GBS * 1e9) * 1e3
+        roof_ms += max(t_fl, t_hbm)
+        n_hbm += nl if t_hbm > t_fl else 0
         d = by.setdefault(kind, [0, 0.0, 0.0])
         d[0] += nl
         d[1] += fl
@@ -201,6 +208,11 @@ def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic="fp32", suffix="",
         "launches": n, "avg_launch_us": round(tot_ms * 1e3 / max(n, 1), 2),
         "algorithmic_gflop_per_launch": round(tot_fl / max(n, 1) / 1e9, 3),
         "conv_ms_per_step": round(tot_ms, 2),
+        "per_launch_roofline": {
+            "ms": round(roof_ms, 2), "frac": round(roof_ms / tot_ms, 4),
+            "hbm_bound_launches": n_hbm,
+            "note": "sum over launches of max(FLOPs / MFMA peak, algorithmic bytes / HBM peak) "
+                    "against the summed measured durations"},
         "breakdown": {k: {"launches": v[0], "gflop": round(v[1] / 1e9, 1),
                           "ms": round(v[2], 2), "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 1)}
                       for k, v in by.items()},

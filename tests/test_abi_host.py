@@ -151,3 +151,43 @@ def test_mc_shard_counts():
         for w in (1, 2, 3, 8):
             counts = [local_mc_count(n, r, w) for r in range(w)]
             assert sum(counts) == n and max(counts) - min(counts) <= 1
+
+
+def _trunk_convs(S, B=64):
+    """(H, Cin, Cout, R, stride) of every ResNet-50 conv after the stem, at input size S."""
+    H, inp, out = S // 4, 64, []
+    for planes, blocks, st in ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)):
+        for bi in range(blocks):
+            s = st if bi == 0 else 1
+            out += [(H, inp, planes, 1, 1), (H, planes, planes, 3, s), (H // s, planes, planes * 4, 1, 1)]
+            if bi == 0:
+                out.append((H, inp, planes * 4, 1, s))
+            H, inp = H // s, planes * 4
+    return out
+
+
+def test_wgrad_split_count_fills_block_rounds():
+    """mauv_conv2d_wgrad_splits (host helper, conv_gemm.hip): at the bench workload every
+    weight-gradient launch of the three trunks fills its last round of 512 resident blocks
+    (two per CU) to >= 80 %, within one to three rounds; the round-1 rule (MAUV_WGRAD_SPLITS=0,
+    the fewest splits giving >= 1024 blocks) is restored in a fresh process."""
+    import subprocess
+    import sys
+    from mauv import ops
+
+    def tiles(Cin, Cout, R):
+        N = R * R * Cin
+        return -(-Cout // (64 if Cout <= 64 else 128)) * -(-N // (64 if N <= 64 else 128)) * 5
+    for S in (224, 256):
+        for H, Cin, Cout, R, st in _trunk_convs(S):
+            sp = ops.wgrad_splits(5, 64, H, H, Cin, Cout, R, st, R // 2)
+            nb = tiles(Cin, Cout, R) * sp
+            rounds = -(-nb // 512)
+            assert 1 <= rounds <= 3, (S, H, Cin, Cout, R, st, sp, nb)
+            assert nb / (rounds * 512) >= 0.8, (S, H, Cin, Cout, R, st, sp, nb)
+    code = ("import sys; sys.path[:0] = [%r, %r]; from mauv import ops; "
+            "print(ops.wgrad_splits(5, 64, 64, 64, 64, 64, 3, 1, 1))"
+            % (REPO, os.path.join(REPO, "multimodal-auv_amd")))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True,
+                         env=dict(os.environ, MAUV_WGRAD_SPLITS="0")).stdout.split()[-1]
+    assert int(out) == 41   # ceil(1024 / 25 tiles)
