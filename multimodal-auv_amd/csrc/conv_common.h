@@ -46,6 +46,8 @@ struct ConvArgs {
   // (n * mg) >> sh for n < 2^31 (mauv::magic_div)
   unsigned long long mg_hw, mg_w;
   int sh_hw, sh_w;
+  // WGRAD: n / Wo and n / Ho for n < 2^17 as umulhi(n, m16) (m16 = 0: divisor 1; m16_div)
+  unsigned m16_w, m16_h;
   // FWD with the MC groups stacked along N (the stems over shared im2col rows, stem.hip):
   // column n belongs to group n / cpg, channel n % cpg; outputs and BN statistics go to that
   // group's tensors ([G][M][cpg], [G][nblk][cpg]).  0 = off.
@@ -77,8 +79,11 @@ __device__ __forceinline__ void conv_block_tile(const ConvArgs& a, int& m0, int&
     L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
     by = blockIdx.y;
   }
-  m0 = (L / nN) * BM;
-  n0 = (L - (L / nN) * nN) * BN;
+  // block-uniform: keep them in SGPRs (the divisions above expand to VALU code, and a buffer
+  // descriptor derived from a VGPR value costs a waterfall loop at every load)
+  by = __builtin_amdgcn_readfirstlane(by);
+  m0 = __builtin_amdgcn_readfirstlane((L / nN) * BM);
+  n0 = __builtin_amdgcn_readfirstlane((L - (L / nN) * nN) * BN);
 }
 
 // MAUV_XCD_GRID (default 1): conv_block_tile's order
@@ -98,6 +103,20 @@ inline void magic_div(unsigned d, unsigned long long& m, int& s) {
   while ((1ull << l) < d) ++l;
   s = 31 + l;
   m = (unsigned long long)(((unsigned __int128)1 << s) / d) + 1;
+}
+
+// q = n / d as umulhi(n, m) with m = floor((2^32 - 1) / d) + 1, exact for n < 2^17 and
+// 2 <= d <= 4096 (checked exhaustively, tests/test_abi_host.py); d = 1 -> m = 0 (q = n)
+inline unsigned m16_div(unsigned d) { return d <= 1 ? 0u : (unsigned)(0xFFFFFFFFull / d + 1); }
+// buffer offset `off` when `ok`, else `oob` (past the descriptor: the load returns 0), as one
+// v_cndmask: the empty asm pins `off` to a VGPR computed before the select, so the compiler
+// does not move the offset arithmetic under a branch around the load
+__device__ __forceinline__ unsigned sel_off(bool ok, unsigned off, unsigned oob) {
+  asm("" : "+v"(off));
+  return ok ? off : oob;
+}
+__device__ __forceinline__ unsigned udiv16(unsigned n, unsigned m) {
+  return m ? __umulhi(n, m) : n;
 }
 
 // Launch the pipelined split-fp32 kernel (conv_split.hip) for an fp32 conv; false when the

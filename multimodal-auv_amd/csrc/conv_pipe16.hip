@@ -235,9 +235,9 @@ void conv_pipe16(const ConvArgs a) {
       S.tc = t_c;
 #pragma unroll
       for (int j = 0; j < NVA; ++j) {
-        const bool ok = sok && (unsigned)(aq0[j] + t_r) < (unsigned)a.H &&
-                        (unsigned)(aq1[j] + t_s) < (unsigned)a.W;
-        S.a[j] = bload16(ra, ok ? abase[j] + soff : kOOB16);
+        const bool ok = sok & ((unsigned)(aq0[j] + t_r) < (unsigned)a.H) &
+                        ((unsigned)(aq1[j] + t_s) < (unsigned)a.W);
+        S.a[j] = bload16(ra, sel_off(ok, abase[j] + soff, kOOB16));
         S.ok |= (unsigned)ok << j;
       }
 #pragma unroll
@@ -253,9 +253,9 @@ void conv_pipe16(const ConvArgs a) {
       const unsigned soff = (unsigned)((t_c - (t_r * a.Wo + t_s) * a.Cout) * 2);
 #pragma unroll
       for (int j = 0; j < NVA; ++j) {
-        const bool ok = sok && (unsigned)(aq0[j] - t_r) < (unsigned)a.Ho &&
-                        (unsigned)(aq1[j] - t_s) < (unsigned)a.Wo;
-        S.a[j] = bload16(ra, ok ? abase[j] + soff : kOOB16);
+        const bool ok = sok & ((unsigned)(aq0[j] - t_r) < (unsigned)a.Ho) &
+                        ((unsigned)(aq1[j] - t_s) < (unsigned)a.Wo);
+        S.a[j] = bload16(ra, sel_off(ok, abase[j] + soff, kOOB16));
       }
       const int r = a.r0 + a.stride * t_r, s = a.s0 + a.stride * t_s;
       const unsigned woff = (unsigned)(((t_c * a.R + r) * a.S + s) * a.Cin * 2);
@@ -269,17 +269,24 @@ void conv_pipe16(const ConvArgs a) {
         const bool ok = k0 + aq0[j] < kend;
         S.a[j] = bload16(ra, ok ? abase[j] + (unsigned)(k0 * a.Cout * 2) : kOOB16);
       }
+      // pixel k0 + d of this stage (d = the chunk's pixel row < 64): k0 decomposed once per
+      // stage (uniform), then d carried through the row and image with two 32-bit magic
+      // divisions; branch-free (one select per load)
       const unsigned HW = (unsigned)(a.Ho * a.Wo);
+      const unsigned b0 = mdiv16((unsigned)k0, a.mg_hw, a.sh_hw), p0 = (unsigned)k0 - b0 * HW;
+      const unsigned oh0 = mdiv16(p0, a.mg_w, a.sh_w), ow0 = p0 - oh0 * (unsigned)a.Wo;
+      const int lim = kend - k0;
       S.ok = 0;
 #pragma unroll
       for (int j = 0; j < NVB; ++j) {
-        const unsigned p = (unsigned)(k0 + bq0[j]);
-        const unsigned b = mdiv16(p, a.mg_hw, a.sh_hw), rem = p - b * HW;
-        const unsigned oh = mdiv16(rem, a.mg_w, a.sh_w), ow = rem - oh * (unsigned)a.Wo;
-        const int ih = (int)oh * a.stride + bq1[j], iw = (int)ow * a.stride + bq2[j];
-        const bool ok = (int)p < kend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        S.b[j] = bload16(rb, ok ? bbase[j] + (unsigned)(((int)b * xs_b + ih * xs_h + iw * xs_w) * 2)
-                                : kOOB16);
+        const unsigned tw = ow0 + (unsigned)bq0[j], q1 = udiv16(tw, a.m16_w);
+        const unsigned th = oh0 + q1, q2 = udiv16(th, a.m16_h);
+        const int ow = (int)(tw - q1 * (unsigned)a.Wo), oh = (int)(th - q2 * (unsigned)a.Ho);
+        const int b = (int)(b0 + q2);
+        const int ih = oh * a.stride + bq1[j], iw = ow * a.stride + bq2[j];
+        const bool ok = (bq0[j] < lim) & ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
+        S.b[j] = bload16(rb, sel_off(ok, bbase[j] + (unsigned)((b * xs_b + ih * xs_h + iw * xs_w) * 2),
+                                     kOOB16));
         S.ok |= (unsigned)ok << (8 + j);
       }
     }
@@ -578,8 +585,11 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
     pipe16_dt<DGRAD, false>(dt, a, st);
   } else {
     if (a.Cout % 8 || a.Cin % 8 || !xs8 || a.kchunk % 64) return false;
+    if (a.Wo > 4096 || a.Ho > 4096) return false;
     magic_div((unsigned)(a.Ho * a.Wo), a.mg_hw, a.sh_hw);
     magic_div((unsigned)a.Wo, a.mg_w, a.sh_w);
+    a.m16_w = m16_div((unsigned)a.Wo);
+    a.m16_h = m16_div((unsigned)a.Ho);
     if (a.xsc) pipe16_dt<WGRAD, true>(dt, a, st);
     else pipe16_dt<WGRAD, false>(dt, a, st);
   }

@@ -215,10 +215,10 @@ void conv_split_f32(const ConvArgs a) {
       S.tc = t_c;
 #pragma unroll
       for (int j = 0; j < NVA; ++j) {
-        const bool ok = sok && tap && (unsigned)(aq0[j] + t_r) < (unsigned)a.H &&
-                        (unsigned)(aq1[j] + t_s) < (unsigned)a.W;
+        const bool ok = sok & tap & ((unsigned)(aq0[j] + t_r) < (unsigned)a.H) &
+                        ((unsigned)(aq1[j] + t_s) < (unsigned)a.W);
         const bool act = !PA || tid + NT * j < LA;
-        S.a[j] = bload(ra, ok && act ? abase[j] + soff : kOOB);
+        S.a[j] = bload(ra, sel_off(ok & act, abase[j] + soff, kOOB));
         S.ok |= (unsigned)ok << j;
       }
 #pragma unroll
@@ -239,9 +239,9 @@ void conv_split_f32(const ConvArgs a) {
       const unsigned soff = (unsigned)((t_c - (t_r * a.Wo + t_s) * a.Cout) * 4);
 #pragma unroll
       for (int j = 0; j < NVA; ++j) {
-        const bool ok = sok && (unsigned)(aq0[j] - t_r) < (unsigned)a.Ho &&
-                        (unsigned)(aq1[j] - t_s) < (unsigned)a.Wo && (!PA || tid + NT * j < LA);
-        S.a[j] = bload(ra, ok ? abase[j] + soff : kOOB);
+        const bool ok = sok & ((unsigned)(aq0[j] - t_r) < (unsigned)a.Ho) &
+                        ((unsigned)(aq1[j] - t_s) < (unsigned)a.Wo) & (!PA || tid + NT * j < LA);
+        S.a[j] = bload(ra, sel_off(ok, abase[j] + soff, kOOB));
       }
       const int r = a.r0 + a.stride * t_r, s = a.s0 + a.stride * t_s;
       const unsigned woff = (unsigned)(((t_c * a.R + r) * a.S + s) * a.Cin * 4);
@@ -256,18 +256,23 @@ void conv_split_f32(const ConvArgs a) {
         const bool ok = k0 + aq0[j] < kend && (!PA || tid + NT * j < LA);
         S.a[j] = bload(ra, ok ? abase[j] + (unsigned)(k0 * a.Cout * 4) : kOOB);
       }
+      // pixel k0 + d (d = the float4's pixel row < 16): conv_pipe16.hip's branch-free form
       const unsigned HW = (unsigned)(a.Ho * a.Wo);
+      const unsigned b0 = mdiv((unsigned)k0, a.mg_hw, a.sh_hw), p0 = (unsigned)k0 - b0 * HW;
+      const unsigned oh0 = mdiv(p0, a.mg_w, a.sh_w), ow0 = p0 - oh0 * (unsigned)a.Wo;
+      const int lim = kend - k0;
       S.ok = 0;
 #pragma unroll
       for (int j = 0; j < NVB; ++j) {
-        const unsigned p = (unsigned)(k0 + bq0[j]);
-        const unsigned b = mdiv(p, a.mg_hw, a.sh_hw), rem = p - b * HW;
-        const unsigned oh = mdiv(rem, a.mg_w, a.sh_w), ow = rem - oh * (unsigned)a.Wo;
-        const int ih = (int)oh * a.stride + bq1[j], iw = (int)ow * a.stride + bq2[j];
-        const bool ok = (int)p < kend && (unsigned)ih < (unsigned)a.H &&
-                        (unsigned)iw < (unsigned)a.W && (!PB || tid + NT * j < LB);
-        S.b[j] = bload(rb, ok ? bbase[j] + (unsigned)(((int)b * xs_b + ih * xs_h + iw * xs_w) * 4)
-                              : kOOB);
+        const unsigned tw = ow0 + (unsigned)bq0[j], q1 = udiv16(tw, a.m16_w);
+        const unsigned th = oh0 + q1, q2 = udiv16(th, a.m16_h);
+        const int ow = (int)(tw - q1 * (unsigned)a.Wo), oh = (int)(th - q2 * (unsigned)a.Ho);
+        const int b = (int)(b0 + q2);
+        const int ih = oh * a.stride + bq1[j], iw = ow * a.stride + bq2[j];
+        const bool ok = (bq0[j] < lim) & ((unsigned)ih < (unsigned)a.H) &
+                        ((unsigned)iw < (unsigned)a.W) & (!PB || tid + NT * j < LB);
+        S.b[j] = bload(rb, sel_off(ok, bbase[j] + (unsigned)((b * xs_b + ih * xs_h + iw * xs_w) * 4),
+                                   kOOB));
         S.ok |= (unsigned)ok << (8 + j);
       }
     }
@@ -425,6 +430,13 @@ static int split_short_k() {
   return k;
 }
 
+// data-gradient launches with K <= MAUV_SPLIT_SHORT_K_DGRAD (default 0 = off) take the SEQ kernel
+static int split_short_k_dgrad() {
+  static int k = -1;
+  if (k < 0) { const char* e = getenv("MAUV_SPLIT_SHORT_K_DGRAD"); k = e ? atoi(e) : 0; }
+  return k;
+}
+
 template <int MODE, bool XBN>
 static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
   const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
@@ -453,6 +465,12 @@ static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
   if (w8 < 0) { const char* e8 = getenv("MAUV_SPLIT_W8"); w8 = e8 ? atoi(e8) : 2; }
   if constexpr (MODE == FWD) {
     if (w8 && bm == 128 && bn == 128 && a.K <= split_short_k()) {
+      launch_split<MODE, 128, 128, XBN, 8, false, true>(a, oneacc, st);
+      return;
+    }
+  }
+  if constexpr (MODE == DGRAD) {  // the data gradients with K = taps x Cout <= the threshold
+    if (w8 && bm == 128 && bn == 128 && a.K > 0 && a.K <= split_short_k_dgrad()) {
       launch_split<MODE, 128, 128, XBN, 8, false, true>(a, oneacc, st);
       return;
     }
@@ -493,8 +511,11 @@ bool conv_split_launch(int mode, const ConvArgs& a0, int oneacc, hipStream_t st)
     const bool vb = (a.Cin % 4 == 0) && a.xs_c == 1 && a.xs_w % 4 == 0 && a.xs_h % 4 == 0 &&
                     a.xs_b % 4 == 0 && a.xs_g % 4 == 0;
     if (a.Cout % 4 || !vb) return false;
+    if (a.Wo > 4096 || a.Ho > 4096) return false;
     magic_div((unsigned)(a.Ho * a.Wo), a.mg_hw, a.sh_hw);
     magic_div((unsigned)a.Wo, a.mg_w, a.sh_w);
+    a.m16_w = m16_div((unsigned)a.Wo);
+    a.m16_h = m16_div((unsigned)a.Ho);
     if (a.xsc) split_tiles<WGRAD, true>(a, oneacc, st);
     else split_tiles<WGRAD, false>(a, oneacc, st);
   }

@@ -191,3 +191,13 @@ def test_wgrad_split_count_fills_block_rounds():
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True,
                          env=dict(os.environ, MAUV_WGRAD_SPLITS="0")).stdout.split()[-1]
     assert int(out) == 41   # ceil(1024 / 25 tiles)
+
+
+def test_m16_magic_division_exact():
+    """conv_common.h m16_div / udiv16 (the weight-gradient loaders' pixel -> (row, image)
+    carry): q = umulhi(n, floor((2^32 - 1) / d) + 1) equals n // d for every n < 2^17 and
+    2 <= d <= 4096 (d = 1 takes the m = 0 path, q = n)."""
+    n = np.arange(1 << 17, dtype=np.uint64)
+    for d in range(2, 4097):
+        m = np.uint64((0xFFFFFFFF // d) + 1)
+        assert np.array_equal((n * m) >> np.uint64(32), n // np.uint64(d)), d
