@@ -1,3 +1,5 @@
+# RECORD ONLY: the switch MAUV_SPLIT_DEEP and the variant it selected were measured (DESIGN.md cites the result)
+# and removed from the code; this script no longer reproduces that A/B.
 # A/B: three register stages (loads three tiles ahead) in the eight-wave 128x128 split kernel
 # (record of a measured experiment whose code was removed: see DESIGN.md; the variable it sets is no longer read)
 set -o pipefail

@@ -1,3 +1,5 @@
+# RECORD ONLY: the switch MAUV_P16_PERSIST and the variant it selected were measured (DESIGN.md cites the result)
+# and removed from the code; this script no longer reproduces that A/B.
 # A/B: persistent 16-bit conv blocks for short-K launches (MAUV_P16_PERSIST = max stages)
 # (record of a measured experiment whose code was removed: see DESIGN.md; the variable it sets is no longer read)
 set -o pipefail

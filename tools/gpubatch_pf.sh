@@ -1,3 +1,5 @@
+# RECORD ONLY: the switch MAUV_SPLIT_PF and the variant it selected were measured (DESIGN.md cites the result)
+# and removed from the code; this script no longer reproduces that A/B.
 # A/B: L2 prefetch touches in the split kernel (MAUV_SPLIT_PF)
 # (record of a measured experiment whose code was removed: see DESIGN.md; the variable it sets is no longer read)
 set -o pipefail

@@ -1,3 +1,5 @@
+# RECORD ONLY: the switch MAUV_LAZY_BN_INFER and the variant it selected were measured (DESIGN.md cites the result)
+# and removed from the code; this script no longer reproduces that A/B.
 # A/B: inference with bn1/bn2 applied on load (default) vs materialised (MAUV_LAZY_BN_INFER=0)
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,3 +1,5 @@
+# RECORD ONLY: the switch MAUV_P16_SHORT_DGRAD and the variant it selected were measured (DESIGN.md cites the result)
+# and removed from the code; this script no longer reproduces that A/B.
 # short-K kernels: parity; bench A/B of the data-gradient variants and of the threshold
 set -o pipefail
 mkdir -p gpurun_out

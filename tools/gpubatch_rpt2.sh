@@ -1,3 +1,5 @@
+# RECORD ONLY: the switch MAUV_SIDE_WGRAD and the variant it selected were measured (DESIGN.md cites the result)
+# and removed from the code; this script no longer reproduces that A/B.
 # BN backward partial rows-per-thread with the ReLU masks (8/16/32), and the side wgrad stream
 set -o pipefail
 mkdir -p gpurun_out

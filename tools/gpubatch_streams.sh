@@ -1,3 +1,5 @@
+# RECORD ONLY: the switch MAUV_SIDE_WGRAD and the variant it selected were measured (DESIGN.md cites the result)
+# and removed from the code; this script no longer reproduces that A/B.
 # concurrent trunk streams: model parity + A/B bench (fp32, bf16, inference)
 set -o pipefail
 mkdir -p gpurun_out
