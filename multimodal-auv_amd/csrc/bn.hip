@@ -562,17 +562,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rows(const typename S::T* __
   }
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  const int v = e ? atoi(e) : 0;
-  return v > 0 ? v : dflt;
-}
-
-// Row-walk geometry: <= 2 rows per thread (MAUV_BN_APPLY_RPT overrides, for measurement;
-// 2 vs 4 vs 8 vs 16: inference 10.40-10.43k vs 10.32-10.35k vs 10.16-10.19k vs 10.12k
+// Row-walk geometry: <= 2 rows per thread (measured 2 vs 4 vs 8 vs 16: inference 10.40-10.43k vs 10.32-10.35k vs 10.16-10.19k vs 10.12k
 // MC-samples/s on one box; training flat).
 static void rows_geometry(long long M, int C, int& nblk, int& rpb) {
-  static const int rpt = env_int("MAUV_BN_APPLY_RPT", 2);
+  constexpr int rpt = 2;
   const int rp = 256 / (C / 8);
   const long long r = (long long)rp * rpt;
   rpb = (int)r;
@@ -604,7 +597,7 @@ static void launch_apply(const typename S::T* y, const float* scale, const float
 }
 
 static void bwd_geometry(long long M, int C, int& nblk, int& rpb) {
-  static const int rpt = env_int("MAUV_BN_PARTIAL_RPT", 32);
+  constexpr int rpt = 32;  // rows per thread of the backward partial pass
   const int rp = 256 / (C / 8);
   long long r = (long long)rp * rpt;
   long long n = (M + r - 1) / r;

@@ -543,10 +543,8 @@ void conv_gemm_f32(const ConvArgs a) {
   conv_epilogue<MODE, BM, BN>(a, acc, smem, tid, m0, n0, g, sp);
 }
 
-static int g_bk = 0;  // tile depth: 16 or 32 (MAUV_CONV_BK; default 16)
-// MAUV_CONV_ROW: row images + b128 operand reads for FWD (bit 0) / DGRAD (bit 1); measured
-// on the bench workload: DGRAD +3.5 %, FWD -2 % -> default DGRAD only (2)
-static int g_row = -1;
+// exact mode: DGRAD uses row images + b128 operand reads (measured on the bench workload:
+// DGRAD +3.5 %, FWD -2 %); a 32-deep tile measured slower (2 vs 3 blocks per CU) and was removed
 
 // fp32 product arithmetic (file header): 6 = split (default), 3 = split3, 0 = exact.
 // Initial value from MAUV_F32_MATH=split|split3|exact; mauv_set_f32_math changes it.
@@ -561,14 +559,6 @@ static int f32_math() {
 
 template <int MODE, int BM, int BN, bool VA, bool VB>
 static void launch(const ConvArgs& a, hipStream_t st) {
-  if (!g_bk) {
-    const char* e = getenv("MAUV_CONV_BK");
-    g_bk = (e && atoi(e) == 32) ? 32 : 16;  // measured: 16 wins (3 vs 2 blocks/CU)
-  }
-  if (g_row < 0) {
-    const char* e = getenv("MAUV_CONV_ROW");
-    g_row = e ? atoi(e) : 2;
-  }
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
   const int fm = f32_math();
   if (fm == 6) {
@@ -577,13 +567,8 @@ static void launch(const ConvArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, false, 5>), grid, dim3(256), 0, st, a);
   } else if (fm == 3) {
     hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, false, 3>), grid, dim3(256), 0, st, a);
-  } else if (g_bk == 16) {
-    if ((MODE == FWD && (g_row & 1)) || (MODE == DGRAD && (g_row & 2)))
-      hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, true, 0>), grid, dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, false, 0>), grid, dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 32, VA, VB, false, 0>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_gemm_f32<MODE, BM, BN, 16, VA, VB, MODE == DGRAD, 0>), grid, dim3(256), 0, st, a);
   }
 }
 

@@ -57,9 +57,8 @@ struct Stage {
 
 }  // namespace
 
-// Waves: 2 x 2 for tiles up to 128 x 128 (256 threads, two blocks per CU), 4 x 2 / 2 x 4 for
-// 256 x 128 / 128 x 256 (512 threads, one block per CU) — the 256-wide tiles halve the L2
-// re-reads of the other operand per MFMA, which the fp32 operand traffic makes the limit.
+// Waves: 2 x 2 for tiles up to 128 x 128 (256 threads, two blocks per CU); the launcher
+// instantiates 64 x 64 with these.
 // WV = 8 on a 128 x 128 tile: 4 x 2 waves of 32 x 64 (one accumulator set, <= 128 VGPRs, two
 // blocks = four waves per SIMD for latency hiding)
 // (128 x 64 / 64 x 128 with WV = 8: waves of 32 x 32; the 64-wide operand is then loaded by
@@ -430,58 +429,24 @@ static int split_short_k() {
   return k;
 }
 
-// data-gradient launches with K <= MAUV_SPLIT_SHORT_K_DGRAD (default 0 = off) take the SEQ kernel
-static int split_short_k_dgrad() {
-  static int k = -1;
-  if (k < 0) { const char* e = getenv("MAUV_SPLIT_SHORT_K_DGRAD"); k = e ? atoi(e) : 0; }
-  return k;
-}
-
 template <int MODE, bool XBN>
 static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
   const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
-  // MAUV_SPLIT_BIG: 1 = 256-wide tiles while they keep >= 2 blocks per CU-round, 2 = whenever
-  // both extents exceed 64 (tests); default 0 — measured on the bench workload, they do not beat
-  // two co-resident 128 x 128 blocks (225 vs 229 ms of convs per step)
-  const char* e = getenv("MAUV_SPLIT_BIG");
-  const int big = e ? atoi(e) : 0;
-  const long long minb = big == 2 ? 1 : 512;
-  if (big && bm == 128 && bn == 128) {
-    // a 256-wide side along the larger extent
-    const long long gz = (long long)a.G * (MODE == WGRAD ? a.splits : 1);
-    if (a.M >= a.N && (long long)ceil_div(a.M, 256) * ceil_div(a.N, 128) * gz >= minb) {
-      launch_split<MODE, 256, 128, XBN>(a, oneacc, st);
-      return;
-    }
-    if (a.N > a.M && a.N >= 256 && (long long)ceil_div(a.M, 128) * ceil_div(a.N, 256) * gz >= minb) {
-      launch_split<MODE, 128, 256, XBN>(a, oneacc, st);
-      return;
-    }
-  }
   // eight-wave blocks (four waves per SIMD): 128 x 128 tiles as waves of 32 x 64, 128 x 64 and
   // 64 x 128 as waves of 32 x 32 — measured 200 vs 235 ms of convs per bench step over four
-  // waves (MAUV_SPLIT_W8=0 restores those, 1 keeps four waves on the 64-wide tiles)
-  static int w8 = -1;
-  if (w8 < 0) { const char* e8 = getenv("MAUV_SPLIT_W8"); w8 = e8 ? atoi(e8) : 2; }
+  // waves.  256-wide tiles (225 vs 229 ms of convs per step against two co-resident 128 x 128
+  // blocks) and a short-K data-gradient variant (neutral) were measured and
+  // removed.
   if constexpr (MODE == FWD) {
-    if (w8 && bm == 128 && bn == 128 && a.K <= split_short_k()) {
+    if (bm == 128 && bn == 128 && a.K <= split_short_k()) {
       launch_split<MODE, 128, 128, XBN, 8, false, true>(a, oneacc, st);
       return;
     }
   }
-  if constexpr (MODE == DGRAD) {  // the data gradients with K = taps x Cout <= the threshold
-    if (w8 && bm == 128 && bn == 128 && a.K > 0 && a.K <= split_short_k_dgrad()) {
-      launch_split<MODE, 128, 128, XBN, 8, false, true>(a, oneacc, st);
-      return;
-    }
-  }
-  if (w8 && bm == 128 && bn == 128) { launch_split<MODE, 128, 128, XBN, 8>(a, oneacc, st); return; }
-  if (w8 == 2 && bm == 128 && bn == 64) { launch_split<MODE, 128, 64, XBN, 8>(a, oneacc, st); return; }
-  if (w8 == 2 && bm == 64 && bn == 128) { launch_split<MODE, 64, 128, XBN, 8>(a, oneacc, st); return; }
-  if (bm == 64 && bn == 64) launch_split<MODE, 64, 64, XBN>(a, oneacc, st);
-  else if (bm == 64) launch_split<MODE, 64, 128, XBN>(a, oneacc, st);
-  else if (bn == 64) launch_split<MODE, 128, 64, XBN>(a, oneacc, st);
-  else launch_split<MODE, 128, 128, XBN>(a, oneacc, st);
+  if (bm == 128 && bn == 128) launch_split<MODE, 128, 128, XBN, 8>(a, oneacc, st);
+  else if (bm == 128 && bn == 64) launch_split<MODE, 128, 64, XBN, 8>(a, oneacc, st);
+  else if (bm == 64 && bn == 128) launch_split<MODE, 64, 128, XBN, 8>(a, oneacc, st);
+  else launch_split<MODE, 64, 64, XBN>(a, oneacc, st);
 }
 
 bool conv_split_launch(int mode, const ConvArgs& a0, int oneacc, hipStream_t st) {

@@ -94,13 +94,13 @@ def test_split_as_accurate_as_exact(case, f32_math):
 
 
 @pytest.mark.parametrize("case", [
-    (2, 2, 8, 128, 256, 3, 1, 1),      # FWD 128x256, DGRAD 256x128, WGRAD 128x256
-    (1, 3, 9, 128, 512, 1, 2, 0),      # strided 1x1: FWD 128x256 (N > M), DGRAD parity classes
-    (2, 2, 5, 256, 384, 3, 2, 1),      # ragged M and N edges inside the 256-wide tiles
+    (2, 2, 8, 128, 256, 3, 1, 1),      # 128 x 128 eight-wave tiles, K > 256
+    (1, 3, 9, 128, 512, 1, 2, 0),      # strided 1x1: short-K forward, DGRAD parity classes
+    (2, 2, 5, 256, 384, 3, 2, 1),      # ragged M and N edges
 ])
-def test_split_wide_tiles(case, f32_math, monkeypatch):
-    """The 8-wave 256 x 128 / 128 x 256 tiles (forced on small shapes) vs float64, including
-    their two-partials-per-tile BN statistics epilogue."""
+def test_split_tiles_vs_exact(case, f32_math):
+    """The eight-wave split tiles vs float64, as accurate as exact f32 MFMA (within 2x its
+    error), and their per-128-row BN statistics partials from the forward epilogue."""
     from mauv import ops
     G, B, H, Cin, Cout, R, st, pad = case
     torch.manual_seed(5)
@@ -109,12 +109,11 @@ def test_split_wide_tiles(case, f32_math, monkeypatch):
     Ho = (H + 2 * pad - R) // st + 1
     dy = torch.randn(G, B, Ho, Ho, Cout)
     refs = _ref_all(x, w, dy, st, pad)
+    f32_math("exact")
+    exact = _run_all(x, w, dy, G, B, H, Cin, Cout, R, st, pad)
     f32_math("split")
-    monkeypatch.setenv("MAUV_SPLIT_BIG", "0")
-    small = _run_all(x, w, dy, G, B, H, Cin, Cout, R, st, pad)
-    monkeypatch.setenv("MAUV_SPLIT_BIG", "2")
-    wide = _run_all(x, w, dy, G, B, H, Cin, Cout, R, st, pad)
-    for what, o, s_, r in zip(("y", "dx", "dW"), wide, small, refs):
+    split = _run_all(x, w, dy, G, B, H, Cin, Cout, R, st, pad)
+    for what, o, s_, r in zip(("y", "dx", "dW"), split, exact, refs):
         scale = r.abs().max().item()
         e_w, e_s = (o.double() - r).abs().max().item(), (s_.double() - r).abs().max().item()
         assert e_w <= 2.0 * e_s + ULP32 * scale, (what, e_w, e_s)
@@ -122,22 +121,20 @@ def test_split_wide_tiles(case, f32_math, monkeypatch):
     M = B * Ho * Ho
     nblk = ops.fwd_stat_blocks(G, B, H, H, Cin, Cout, R, st, pad)
     xd, wd = x.cuda(), w.cuda()
-    for big in ("0", "2"):
-        monkeypatch.setenv("MAUV_SPLIT_BIG", big)
-        y = torch.empty(G, B, Ho, Ho, Cout, device=dev)
-        pm = torch.full((G, nblk, Cout), float("nan"), device=dev)
-        p2 = torch.full((G, nblk, Cout), float("nan"), device=dev)
-        pc = torch.full((G, nblk), float("nan"), device=dev)
-        ops.conv2d_fwd(xd, wd, y, G, B, H, H, Cin, Cout, R, st, pad, stats=(pm, p2, pc))
-        cnt = pc.double().cpu()
-        assert torch.isfinite(cnt).all() and cnt.sum(1).eq(M).all(), cnt
-        mean = (pm.double().cpu() * cnt[..., None]).sum(1) / M
-        yr = refs[0].reshape(G, M, Cout)
-        assert (mean - yr.mean(1)).abs().max().item() <= 1e-5 * yr.abs().max().item()
-        dev_ = pm.double().cpu() - mean[:, None]
-        m2 = (p2.double().cpu() + cnt[..., None] * dev_ ** 2).sum(1)
-        var_ref = ((yr - yr.mean(1, keepdim=True)) ** 2).sum(1)
-        assert ((m2 - var_ref).abs() / var_ref).max().item() <= 1e-4
+    y = torch.empty(G, B, Ho, Ho, Cout, device=dev)
+    pm = torch.full((G, nblk, Cout), float("nan"), device=dev)
+    p2 = torch.full((G, nblk, Cout), float("nan"), device=dev)
+    pc = torch.full((G, nblk), float("nan"), device=dev)
+    ops.conv2d_fwd(xd, wd, y, G, B, H, H, Cin, Cout, R, st, pad, stats=(pm, p2, pc))
+    cnt = pc.double().cpu()
+    assert torch.isfinite(cnt).all() and cnt.sum(1).eq(M).all(), cnt
+    mean = (pm.double().cpu() * cnt[..., None]).sum(1) / M
+    yr = refs[0].reshape(G, M, Cout)
+    assert (mean - yr.mean(1)).abs().max().item() <= 1e-5 * yr.abs().max().item()
+    dev_ = pm.double().cpu() - mean[:, None]
+    m2 = (p2.double().cpu() + cnt[..., None] * dev_ ** 2).sum(1)
+    var_ref = ((yr - yr.mean(1, keepdim=True)) ** 2).sum(1)
+    assert ((m2 - var_ref).abs() / var_ref).max().item() <= 1e-4
 
 
 def test_split_keeps_fp32_range(f32_math):

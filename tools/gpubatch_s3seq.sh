@@ -1,3 +1,5 @@
+# RECORD ONLY: the switch MAUV_SPLIT_SHORT_K_DGRAD and the variant it selected were measured (DESIGN.md cites the result)
+# and removed from the code; this script no longer reproduces that A/B.
 # short-K (SEQ) split-fp32 kernels for the data gradient (MAUV_SPLIT_SHORT_K_DGRAD) and a
 # forward threshold of 512 (MAUV_SPLIT_SHORT_K): conv totals and fp32 training A/B
 set -o pipefail
