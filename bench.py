@@ -241,6 +241,9 @@ def main():
     ap.add_argument("--bf16-steps", type=int, default=5)
     ap.add_argument("--no-infer-fp32", action="store_true",
                     help="skip MC inference with fp32 trunks (autocast off)")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="skip the per-GPU slices of configs[4] (S=128/512, B=32) and the "
+                         "num_mc=12 step of main.py:310")
     ap.add_argument("--exact-steps", type=int, default=2,
                     help="also time the fp32 step with exact f32 MFMA products (0 = skip)")
     args = ap.parse_args()
@@ -351,6 +354,41 @@ def main():
         set_precision(model.module if world > 1 else model,
                       torch.bfloat16 if args.dtype == "bf16" else None)
 
+    sweep = None
+    if not args.no_sweep:
+        # configs[4] per-GPU slice (B=256 over 8 GPUs = 32/GPU) at the sonar sizes the
+        # headline does not cover, and main.py:310's num_mc=12 at the headline shape; same
+        # model, optimiser and trunk precision as the headline.  Each leg reports its peak
+        # HBM; a leg that does not fit is reported, not fatal.
+        sweep = {}
+        legs = [(f"sonar{S}", 32, S, args.num_mc) for S in (128, 512)]
+        legs.append(("num_mc12", args.batch, args.sonar, 12))
+        for name, Bs, S, nmc in legs:
+            opt.zero_grad(set_to_none=True)
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            torch.cuda.reset_peak_memory_stats(dev)
+            try:
+                xs_, bs_, ss_, ys_ = synthetic_batch(Bs, args.optical, S, dev, 4321 + rank)
+
+                def sstep():
+                    return mc_train_step(model, (xs_, bs_, ss_), ys_, crit, opt, nmc, Bs, kl_w)
+
+                sstep()
+                ts = timed(sstep, 2)
+                sweep[name] = {"value": round(Bs * world * 2 / ts, 3), "unit": "triplets/s",
+                               "ms_per_step": round(ts / 2 * 1e3, 2), "steps": 2,
+                               "batch_per_gpu": Bs, "sonar_px": S, "optical_px": args.optical,
+                               "num_mc": nmc, "dtype": args.dtype,
+                               "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)}
+            except torch.OutOfMemoryError as e:
+                sweep[name] = {"error": "out of memory", "detail": str(e)[:200]}
+            finally:
+                xs_ = bs_ = ss_ = ys_ = None
+        opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
     infer = None
     if not args.no_infer:
         from mauv.predict import multimodal_predict_and_save
@@ -417,7 +455,8 @@ def main():
                        "parallelism": f"dp{world}"},
             "f32_math": f32_math if args.dtype == "fp32" else None,
             "fp32_exact_mfma": exact,
-            "inference": infer, "bf16_train": bf16, "roofline": roof, "cpu_baseline": cpu,
+            "inference": infer, "bf16_train": bf16, "train_sweep": sweep, "roofline": roof,
+            "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
