@@ -12,6 +12,11 @@ namespace mauv {
 // Tie-break as torch's max_pool2d: first maximum in (kh, kw) scan order; NaN wins.
 // One thread per 8 channels of one output pixel (C % 8 == 0, the stem has C = 64; one 16-B
 // load per tap for 16-bit storage); pixel decomposition in 32-bit when the output fits.
+// Branch-free taps: the nine loads are issued together from clamped in-image addresses and the
+// taps outside the image (padding) become -inf after the load, which never wins the scan —
+// the same maxima and indices as skipping them.  Block order: with gridDim.x % 8 == 0 each XCD
+// (blocks are dealt round-robin to the 8 XCDs) walks a contiguous eighth of every grid-stride
+// sweep, so the input row shared by two neighbouring output rows is read through one L2.
 template <class S, class I>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const typename S::T* __restrict__ x,
                                                           int N, int H, int W, int C, int Ho,
@@ -22,50 +27,65 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const typename S::T* _
                                                           int npg) {
   const I C8 = (I)(C / 8);
   const I total = (I)N * Ho * Wo * C8;
-  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
+  const unsigned nb = gridDim.x, b = blockIdx.x;
+  const unsigned bid = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  for (I i = (I)bid * 256 + threadIdx.x; i < total; i += (I)nb * 256) {
     const int c = 8 * (int)(i % C8);
     I p = i / C8;
     const int ow = (int)(p % (I)Wo); p /= (I)Wo;
     const int oh = (int)(p % (I)Ho);
     const int n = (int)(p / (I)Ho);
-    floatx8 best;
-    int bi[8];
+    floatx8 v[9];
+    unsigned ok = 0;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int r = 0; r < 3; ++r) {
+      const int ih = oh * 2 - 1 + r;
+      const bool vr = (unsigned)ih < (unsigned)H;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int iw = ow * 2 - 1 + s;
+        const bool vt = vr & ((unsigned)iw < (unsigned)W);
+        ok |= (vt ? 1u : 0u) << (r * 3 + s);
+        const int ihc = vr ? ih : 0, iwc = ((unsigned)iw < (unsigned)W) ? iw : 0;
+        v[r * 3 + s] = S::ld8(x + (((long long)n * H + ihc) * W + iwc) * C + c);
+      }
+    }
     floatx8 sc, sh;
     if (scale) {  // pending BN + ReLU of the stem, applied on load (group g = n / npg)
       const int gc = (n / npg) * C + c;
       sc = ldf8(scale + gc);
       sh = ldf8(shift + gc);
     }
-    for (int r = 0; r < 3; ++r) {
-      const int ih = oh * 2 - 1 + r;
-      if (ih < 0 || ih >= H) continue;
-      for (int s = 0; s < 3; ++s) {
-        const int iw = ow * 2 - 1 + s;
-        if (iw < 0 || iw >= W) continue;
-        floatx8 v = S::ld8(x + (((long long)n * H + ih) * W + iw) * C + c);
-        if (scale) {
-          // exactly what bn_apply would have stored: relu(y*scale + shift) in fp32, rounded to
-          // the storage type — so maxima and tie-breaks match the materialised path
-          v = v * sc + sh;
+    floatx8 best;
+    int bi[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
-          alignas(16) typename S::T tmp[8];
-          S::st8(tmp, v);
-          v = S::ld8(tmp);
-        }
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (v[e] > best[e] || isnan(v[e])) { best[e] = v[e]; bi[e] = r * 3 + s; }
+    for (int t = 0; t < 9; ++t) {
+      floatx8 u = v[t];
+      if (scale) {
+        // exactly what bn_apply would have stored: relu(y*scale + shift) in fp32, rounded to
+        // the storage type — so maxima and tie-breaks match the materialised path
+        u = u * sc + sh;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) u[e] = u[e] > 0.f ? u[e] : 0.f;
+        alignas(16) typename S::T tmp[8];
+        S::st8(tmp, u);
+        u = S::ld8(tmp);
+      }
+      const bool vt = (ok >> t) & 1u;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float q = vt ? u[e] : -INFINITY;
+        if (q > best[e] || isnan(q)) { best[e] = q; bi[e] = t; }
       }
     }
     S::st8(y + 8 * (long long)i, best);
     if (idx) {
-      uint2 b;
-      b.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
-      b.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
-      *(uint2*)(idx + 8 * (long long)i) = b;
+      uint2 bb;
+      bb.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+      bb.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+      *(uint2*)(idx + 8 * (long long)i) = bb;
     }
   }
 }
