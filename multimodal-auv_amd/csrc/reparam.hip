@@ -43,7 +43,9 @@ __global__ __launch_bounds__(256) void reparam_sample_kernel(
         m[e] = 0.f; s[e] = 0.f; dst[e] = -1;
       }
     }
-    for (int g = 0; g < G; ++g) {
+    // blockIdx.y takes groups g = blockIdx.y, blockIdx.y + gridDim.y, ... (the Philox counter
+    // is (sample, layer, quad): the same normals whichever block draws them)
+    for (int g = blockIdx.y; g < G; g += gridDim.y) {
       floatx4 ep;
       if (eps) {
 #pragma unroll
@@ -69,18 +71,24 @@ __global__ __launch_bounds__(256) void reparam_sample_kernel(
 //       dmu += sum,  drho += sum_g d_g * eps_g' * sigmoid(rho).
 // Reference mode (fixed >= 0): one epsilon for every g, so drho += (sum_g d_g) * eps * sig —
 // one pass.  Exact mode: one pass per g.
-// input channels per block: 64 for 1x1 (RS = 1), 16 otherwise (<= 16*49 parameters)
-__host__ __device__ inline int rb_cb(int RS) { return RS == 1 ? 64 : 16; }
+// input channels per block: 64 for 1x1 (RS = 1) and for the 3x3 layers whose Cout x Cin/64
+// blocks still number >= 1024 (then each (o, tap) run of the slab is one 256-B line instead of
+// four 64-B pieces), 16 otherwise (<= 16*49 parameters; a small layer keeps its block count).
+// The per-element sum order does not depend on it.
+inline int rb_cb(int Cout, int Cin, int RS) {
+  if (RS == 1) return 64;
+  if (RS * 64 <= 16 * 49 && (long long)Cout * ((Cin + 63) / 64) >= 1024) return 64;
+  return 16;
+}
 
 __global__ __launch_bounds__(256) void reparam_bwd_kernel(
     const float* __restrict__ dw, int splits, long long dw_gs, long long dw_ss,
     const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
     uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS, int cin_pad,
-    float* __restrict__ dmu, float* __restrict__ drho, long long fixed) {
+    float* __restrict__ dmu, float* __restrict__ drho, long long fixed, int CB) {
   __shared__ float sd[16 * 49];   // [cb][RS]
   __shared__ float red[4][64];
   const int o = blockIdx.x, tid = threadIdx.x;
-  const int CB = rb_cb(RS);
   const int c0 = blockIdx.y * CB, cb = min(CB, Cin - c0);
   const int len = cb * RS;
   const long long numel = (long long)Cout * Cin * RS;
@@ -205,6 +213,14 @@ static int grid_for(long long nq) {
   if (b > 65536) b = 65536;
   return (int)(b < 1 ? 1 : b);
 }
+// reparam_sample grid: quads along x; the MC groups split along y until ~2048 blocks (eight
+// per CU) — a small layer's few quad blocks otherwise walk all G groups one after another
+static dim3 sample_grid(long long nq, int G) {
+  const int bx = grid_for(nq);
+  long long gy = (2048 + bx - 1) / bx;
+  if (gy > G) gy = G;
+  return dim3(bx, (unsigned)(gy < 1 ? 1 : gy));
+}
 
 }  // namespace mauv
 
@@ -218,7 +234,7 @@ MAUV_API int mauv_reparam_sample(const float* mu, const float* rho, const float*
                                  float* out, long long out_gstride, hipStream_t stream) {
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
-  hipLaunchKernelGGL(reparam_sample_kernel<SF32>, dim3(grid_for(nq)), dim3(256), 0, stream, mu,
+  hipLaunchKernelGGL(reparam_sample_kernel<SF32>, sample_grid(nq, G), dim3(256), 0, stream, mu,
                      rho, eps, seed, sample0, layer, G, Cout, Cin, RS, Cin, out,
                      out_gstride ? out_gstride : numel);
   return check_launch("reparam_sample");
@@ -234,7 +250,7 @@ MAUV_API int mauv_reparam_sample_padded(const float* mu, const float* rho, const
   if (cin_pad < Cin) { set_error("reparam_sample_padded: cin_pad < Cin"); return kErrArg; }
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
-  hipLaunchKernelGGL(reparam_sample_kernel<SF32>, dim3(grid_for(nq)), dim3(256), 0, stream, mu,
+  hipLaunchKernelGGL(reparam_sample_kernel<SF32>, sample_grid(nq, G), dim3(256), 0, stream, mu,
                      rho, eps, seed, sample0, layer, G, Cout, Cin, RS, cin_pad, out,
                      out_gstride ? out_gstride : (long long)Cout * RS * cin_pad);
   return check_launch("reparam_sample_padded");
@@ -252,7 +268,7 @@ MAUV_API int mauv_reparam_sample_h16(int dtype, const float* mu, const float* rh
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
   const long long gs = out_gstride ? out_gstride : (long long)Cout * RS * cin_pad;
-#define L(D) hipLaunchKernelGGL(reparam_sample_kernel<S16<D>>, dim3(grid_for(nq)), dim3(256), 0, \
+#define L(D) hipLaunchKernelGGL(reparam_sample_kernel<S16<D>>, sample_grid(nq, G), dim3(256), 0, \
                                 stream, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS,   \
                                 cin_pad, (u16*)out, gs);
   MAUV_DT_DISPATCH(dtype, "reparam_sample_h16", L)
@@ -281,9 +297,10 @@ MAUV_API int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride,
   const long long ss = dw_sstride ? dw_sstride : gs * G;
   if (RS > 49) { set_error("reparam_bwd: R*S > 49"); return kErrArg; }
   (void)nq;
-  hipLaunchKernelGGL(reparam_bwd_kernel, dim3(Cout, ceil_div(Cin, rb_cb(RS))), dim3(256), 0, stream, dw, splits,
+  const int cb = rb_cb(Cout, Cin, RS);
+  hipLaunchKernelGGL(reparam_bwd_kernel, dim3(Cout, ceil_div(Cin, cb)), dim3(256), 0, stream, dw, splits,
                      gs, ss, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS, dw_cin, dmu, drho,
-                     fixed_sample >= 0 ? (long long)(fixed_sample - (long long)sample0) : -1LL);
+                     fixed_sample >= 0 ? (long long)(fixed_sample - (long long)sample0) : -1LL, cb);
   return check_launch("reparam_bwd");
 }
 
