@@ -462,7 +462,11 @@ class TrunkRunner(_Runner):
                                   bn.running_var if track else None, bn.momentum, bn.eps, ws,
                                   mean, invstd, scale, shift)
             if track:
-                bn.num_batches_tracked.add_(G)
+                pending = getattr(self, "_nbt", None)
+                if pending is None:
+                    bn.num_batches_tracked.add_(G)
+                else:   # one multi-tensor add per trunk forward (run_forward)
+                    pending.append(bn.num_batches_tracked)
         else:
             ops.bn_eval_params(G, C, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                bn.eps, scale, shift)
@@ -499,6 +503,15 @@ class TrunkRunner(_Runner):
 
     # ---- schedule ----
     def run_forward(self, x):
+        self._nbt = []
+        try:
+            return self._run_forward(x)
+        finally:
+            nbt, self._nbt = self._nbt, None
+            if nbt:
+                torch._foreach_add_(nbt, self.G)
+
+    def _run_forward(self, x):
         t, G = self.trunk, self.G
         x = x.contiguous()
         if x.dtype != torch.float32:
