@@ -73,11 +73,24 @@ def _host_cpu():
     except OSError:
         pass
     try:
-        usable = len(os.sched_getaffinity(0))
+        aff = sorted(os.sched_getaffinity(0))
     except AttributeError:
-        usable = os.cpu_count()
+        aff = list(range(os.cpu_count() or 1))
+    # physical cores among the CPUs this process may run on (SMT siblings counted once)
+    phys = set()
+    for c in aff:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            with open(base + "physical_package_id") as f:
+                pk = f.read().strip()
+            with open(base + "core_id") as f:
+                phys.add((pk, f.read().strip()))
+        except OSError:
+            phys.add(("?", c))
     return {"cpu_model": model, "host_physical_cores": len(cores) or None,
-            "host_logical_cpus": os.cpu_count(), "usable_cpus": usable}
+            "host_logical_cpus": os.cpu_count(), "usable_cpus": len(aff),
+            "usable_physical_cores": len(phys),
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_baseline(args):
@@ -92,8 +105,11 @@ def cpu_baseline(args):
         CPU autocast crashes at predictors.py:74), per MC-sample triplet."""
     from oracle.model_ref import define_models, DEFAULT_PRIOR
     from oracle import loops_ref
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    host = _host_cpu()
+    # torch.set_num_threads(<physical cores>) (SURVEY.md §8d): the physical cores of the CPUs
+    # this process may run on, whatever OMP_NUM_THREADS the box exports
+    threads = max(1, host["usable_physical_cores"])
+    prev_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     models = define_models(None, 7, DEFAULT_PRIOR)
@@ -114,7 +130,7 @@ def cpu_baseline(args):
            "sample": f"oracle train step, B={Bc}, num_mc={Nc} (scaled x{args.num_mc}/{Nc} to "
                      f"num_mc={args.num_mc}), {args.optical}/{args.sonar} px, torch-CPU fp32, "
                      f"{reps} timed steps of {dt:.2f} s"}
-    out.update(_host_cpu())
+    out.update(host)
     # configs[0]: the unimodal CPU path, timed in full
     uni = models["image_model"]
     uopt = torch.optim.Adam(uni.parameters(), lr=5e-5)
@@ -141,6 +157,7 @@ def cpu_baseline(args):
         "sample": f"predictors.py MC loop, B={Bi}, num_mc={Ni}, {args.optical}/{args.sonar} px, "
                   f"fp32, {reps} timed batches of {di:.2f} s (per MC-sample triplet; the "
                   f"GPU number is B=256, num_mc=100)"}
+    torch.set_num_threads(prev_threads)
     return out
 
 
@@ -154,10 +171,19 @@ def pmc_traffic(family="fp32"):
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "round*_conv_traffic.json")))
     files = [f for f in files if ("_bf16_" in os.path.basename(f)) == (family == "bf16")]
     if not files:
-        return None, None
+        return None, None, None
     with open(files[-1]) as f:
         d = json.load(f)
-    return d["bytes_per_launch"], os.path.relpath(files[-1], REPO)
+    return d["bytes_per_launch"], os.path.relpath(files[-1], REPO), d.get("library_sha16")
+
+
+def library_sha16():
+    """sha256 prefix of the libmauv_hip.so this process loaded (the PMC traffic summary records
+    the library it profiled, so the line says whether the two match)."""
+    import hashlib
+    from mauv import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic="fp32", suffix="",
@@ -197,12 +223,14 @@ def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic="fp32", suffix="",
     tot_ms = sum(v[2] for v in by.values())
     n = sum(v[0] for v in by.values())
     achieved = tot_fl / (tot_ms * 1e-3) / 1e12
-    traffic, tsrc = pmc_traffic(traffic) if traffic else (None, None)
+    traffic, tsrc, tsha = pmc_traffic(traffic) if traffic else (None, None, None)
+    lsha = library_sha16()
     return {
         "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
         "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC)",
-        "traffic_source": tsrc,
+        "traffic_source": tsrc, "traffic_library_sha16": tsha, "library_sha16": lsha,
+        "traffic_matches_library": tsha == lsha,
         "algorithmic_bytes_per_launch": round(nbytes / max(n, 1)),
         "kernel": kernel,
         "launches": n, "avg_launch_us": round(tot_ms * 1e3 / max(n, 1), 2),
@@ -244,17 +272,34 @@ def main():
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the per-GPU slices of configs[4] (S=128/512, B=32) and the "
                          "num_mc=12 step of main.py:310")
-    ap.add_argument("--exact-steps", type=int, default=2,
+    ap.add_argument("--exact-steps", type=int, default=5,
                     help="also time the fp32 step with exact f32 MFMA products (0 = skip)")
+    ap.add_argument("--leg-steps", type=int, default=5,
+                    help="timed steps of each train_sweep leg")
+    ap.add_argument("--no-infer-sweep", action="store_true",
+                    help="skip configs[4]'s MC-inference legs (sonar 128 / 512 px, B=256, "
+                         "N=100) and main.py's predictor call shape (B=8, num_mc=12)")
+    ap.add_argument("--sweep-batch", type=int, default=32,
+                    help="triplets per GPU of the configs[4] training legs (256 over 8 GPUs)")
+    ap.add_argument("--infer-sweep-batch", type=int, default=256)
+    ap.add_argument("--infer-sweep-mc", type=int, default=100)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for world > 1 (nccl = RCCL over xGMI; gloo "
+                         "rehearses the multi-rank harness, e.g. two ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU; a rehearsal with more ranks than GPUs (gloo) shares them round-robin
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from mauv.models import define_models, DEFAULT_PRIOR
     from mauv.train import mc_train_step
@@ -361,7 +406,7 @@ def main():
         # model, optimiser and trunk precision as the headline.  Each leg reports its peak
         # HBM; a leg that does not fit is reported, not fatal.
         sweep = {}
-        legs = [(f"sonar{S}", 32, S, args.num_mc) for S in (128, 512)]
+        legs = [(f"sonar{S}", args.sweep_batch, S, args.num_mc) for S in (128, 512)]
         legs.append(("num_mc12", args.batch, args.sonar, 12))
         for name, Bs, S, nmc in legs:
             opt.zero_grad(set_to_none=True)
@@ -375,9 +420,11 @@ def main():
                     return mc_train_step(model, (xs_, bs_, ss_), ys_, crit, opt, nmc, Bs, kl_w)
 
                 sstep()
-                ts = timed(sstep, 2)
-                sweep[name] = {"value": round(Bs * world * 2 / ts, 3), "unit": "triplets/s",
-                               "ms_per_step": round(ts / 2 * 1e3, 2), "steps": 2,
+                ts = timed(sstep, args.leg_steps)
+                sweep[name] = {"value": round(Bs * world * args.leg_steps / ts, 3),
+                               "unit": "triplets/s",
+                               "ms_per_step": round(ts / args.leg_steps * 1e3, 2),
+                               "steps": args.leg_steps,
                                "batch_per_gpu": Bs, "sonar_px": S, "optical_px": args.optical,
                                "num_mc": nmc, "dtype": args.dtype,
                                "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)}
@@ -436,6 +483,45 @@ def main():
                              "dtype": "fp32 trunks (split-fp32 convs), autocast off",
                              "path": "mauv.predict.mc_statistics"}
 
+    infer_sweep = None
+    if not args.no_infer and not args.no_infer_sweep:
+        # configs[4]'s MC-sharded inference at the sonar sizes the headline does not cover
+        # (B=256, N=100, 224 px optical; MC samples sharded over the ranks), and the reference's
+        # own predictor call shape (main.py:261-271: batch_size_unimodal=8 :315, num_mc=12
+        # :310) over 32 batches — both through the drop-in multimodal_predict_and_save under
+        # its own f16 autocast
+        infer_sweep = {}
+        legs = [(f"sonar{S}", args.infer_sweep_batch, S, args.infer_sweep_mc, 1)
+                for S in (128, 512)]
+        legs.append(("main_py_b8_mc12", 8, args.sonar, 12, 32))
+        for name, Bi, S, Ni, nb in legs:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            torch.cuda.reset_peak_memory_stats(dev)
+            try:
+                batches = []
+                for j in range(nb):
+                    xi_, bi_, si_, _ = synthetic_batch(Bi, args.optical, S, dev, 500 + j)
+                    batches.append((xi_, bi_, si_, [f"t{j}_{i}" for i in range(Bi)]))
+                pcsv = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mauv_bench_{name}_r{rank}.csv")
+                # warm-up: one MC chunk per rank (allocator blocks of the timed batch)
+                ck = mc_chunk(model, Bi, Ni, dtype=torch.float16, device=dev,
+                              hw=[(args.optical, args.optical), (S, S), (S, S)])
+                multimodal_predict_and_save(model, batches[:1], dev, pcsv,
+                                            num_mc_samples=min(Ni, max(world, 2) * ck))
+                d = timed(lambda: multimodal_predict_and_save(model, batches, dev, pcsv,
+                                                              num_mc_samples=Ni), 1)
+                infer_sweep[name] = {
+                    "value": round(Ni * Bi * nb / d, 2), "unit": "MC-samples/s",
+                    "batch": Bi, "num_mc": Ni, "batches": nb, "sonar_px": S,
+                    "optical_px": args.optical, "ms_per_batch": round(d / nb * 1e3, 2),
+                    "sharding": "mc" if world > 1 else "none", "mc_chunk": ck,
+                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)}
+            except torch.OutOfMemoryError as e:
+                infer_sweep[name] = {"error": "out of memory", "detail": str(e)[:200]}
+            finally:
+                batches = None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -455,7 +541,8 @@ def main():
                        "parallelism": f"dp{world}"},
             "f32_math": f32_math if args.dtype == "fp32" else None,
             "fp32_exact_mfma": exact,
-            "inference": infer, "bf16_train": bf16, "train_sweep": sweep, "roofline": roof,
+            "inference": infer, "infer_sweep": infer_sweep, "bf16_train": bf16,
+            "train_sweep": sweep, "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

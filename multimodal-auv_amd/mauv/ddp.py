@@ -97,6 +97,10 @@ class DistributedMC(nn.Module):
         rng = self._slice_of(trunk)
         if rng is None:
             return
+        # the KL backward was issued on the caller's stream and adds into this slice: order
+        # the all-reduce after it explicitly (not by autograd's node order)
+        if st.kl_bwd_event is not None:
+            torch.cuda.current_stream().wait_event(st.kl_bwd_event)
         self._pending += self._allreduce_range(st.arena.flat, *rng, async_op=True)
         self._done.append(rng)
         self.n_overlapped += 1
@@ -111,6 +115,29 @@ class DistributedMC(nn.Module):
         t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
         return bool(t.item())
+
+    def sum_ranks(self, values):
+        """Element-wise sum of a list of floats over the ranks (one float64 all-reduce)."""
+        if self.world == 1:
+            return list(values)
+        dev = next(self.module.parameters()).device
+        t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, group=self.group)
+        return t.cpu().tolist()
+
+    def check_same_batch(self, B):
+        """MC-sharded prediction all-reduces per-item statistics: every rank must hold the same
+        batch.  One MAX all-reduce of (B, -B) checks that the batch sizes agree."""
+        if self.world == 1:
+            return
+        dev = next(self.module.parameters()).device
+        t = torch.tensor([B, -B], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        lo, hi = -int(t[1]), int(t[0])
+        if lo != hi:
+            raise RuntimeError(f"mauv MC-sharded prediction: ranks hold batches of different "
+                               f"sizes ({lo}..{hi}); every rank must iterate the same loader in "
+                               "the same order (the MC samples, not the images, are sharded)")
 
     def allreduce_grads(self):
         """Average the flat gradient arena across ranks: wait for the trunk slices issued

@@ -114,6 +114,7 @@ class RootState:
         # kl_bwd_count counts issued KL backwards (they write into every trunk's slice)
         self.grad_ready_hook = None
         self.kl_bwd_count = 0
+        self.kl_bwd_event = None   # recorded after the last KL backward (mauv.kl)
 
     def trunk_dtype(self):
         if self.precision is not None:

@@ -31,6 +31,7 @@ class KLTable:
         self.entries = _entries(modules)
         self.n = len(self.entries)
         self._fwd = None
+        self._fwd_key = None
         self._bwd = None
         self._bwd_key = None
 
@@ -46,15 +47,21 @@ class KLTable:
             rows[i, 5] = np.array([pm, ps], dtype=np.float32).view(np.int64)[0]
         return torch.from_numpy(rows).to(device)
 
+    def _ptr_key(self):
+        """Every mu / rho storage pointer: bayesian-torch's own MOPED idiom re-binds a layer's
+        parameters with ``p.data = ...``, which moves that one tensor and no other."""
+        return tuple(t.data_ptr() for e in self.entries for t in e[:2])
+
     def fwd_table(self, device):
-        key = tuple(e[0].data_ptr() for e in self.entries[:1])
+        key = self._ptr_key()
         if self._fwd is None or self._fwd_key != key:
             self._fwd = self._build(False, device)
             self._fwd_key = key
         return self._fwd
 
     def bwd_table(self, device):
-        key = tuple((e[0].grad.data_ptr() if e[0].grad is not None else 0) for e in self.entries)
+        key = self._ptr_key() + tuple((t.grad.data_ptr() if t.grad is not None else 0)
+                                      for e in self.entries for t in e[:2])
         if self._bwd is None or self._bwd_key != key:
             for mu, rho, _, _ in self.entries:
                 if mu.requires_grad and (mu.grad is None or rho.grad is None):
@@ -87,6 +94,10 @@ class _KL(torch.autograd.Function):
         coef = g.reshape(1).float().contiguous()
         ops.kl_bwd(tab.bwd_table(dev), tab.n, coef)
         st.kl_bwd_count += 1
+        if st.grad_ready_hook is not None:   # DistributedMC orders its slice all-reduces after it
+            ev = torch.cuda.Event()
+            ev.record()
+            st.kl_bwd_event = ev
         return None, None
 
 

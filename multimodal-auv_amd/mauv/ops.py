@@ -24,27 +24,35 @@ def stream():
 H16 = {torch.bfloat16: 0, torch.float16: 1}   # C-ABI dtype codes of the 16-bit path
 
 
+def _raise(t, dt):
+    cur = torch.cuda.current_device() if t.is_cuda else None
+    raise ValueError(f"mauv kernel operand must be a contiguous {dt} tensor on the current ROCm "
+                     f"device cuda:{cur} (the launch stream's), got {t.dtype} on {t.device} "
+                     f"(contiguous={t.is_contiguous()}, shape={tuple(t.shape)})")
+
+
 def _h16(dt, *ts):
+    cur = None
     for t in ts:
-        if t is not None:
-            assert t.is_cuda and t.dtype == dt and t.is_contiguous(), \
-                (t.device, t.dtype, dt, t.is_contiguous(), t.shape)
+        if t is None:
+            continue
+        if not (t.is_cuda and t.dtype == dt and t.is_contiguous()):
+            _raise(t, dt)
+        if cur is None:
+            cur = torch.cuda.current_device()
+        if t.device.index != cur:
+            _raise(t, dt)
 
 
 def _f32(*ts):
-    for t in ts:
-        if t is not None:
-            assert t.is_cuda and t.dtype == torch.float32 and t.is_contiguous(), \
-                (t.device, t.dtype, t.is_contiguous(), t.shape)
+    _h16(torch.float32, *ts)
 
 
 def _dev(dt, *ts):
-    """Every tensor handed to a kernel is a contiguous device tensor of dtype ``dt``: a host
-    pointer reaching a HIP kernel is a memory-access fault the caller cannot catch."""
-    for t in ts:
-        if t is not None and not (t.is_cuda and t.dtype == dt and t.is_contiguous()):
-            raise ValueError(f"mauv kernel operand must be a contiguous {dt} ROCm tensor, got "
-                             f"{t.dtype} on {t.device} (contiguous={t.is_contiguous()})")
+    """Every tensor handed to a kernel is a contiguous device tensor of dtype ``dt`` on the
+    device whose current stream the launch uses: a host pointer (or another GPU's) reaching a
+    HIP kernel is a memory-access fault the caller cannot catch."""
+    _h16(dt, *ts)
 
 
 def out_hw(H, R, stride, pad):
@@ -115,14 +123,14 @@ def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_stri
     if w.dtype in H16:
         assert bias is None, "16-bit convs carry no bias (the trunks' convs are bias=False)"
         _h16(w.dtype, w, y)
-        assert x.is_cuda and x.dtype == w.dtype
+        assert x.is_cuda and x.dtype == w.dtype and x.device.index == torch.cuda.current_device()
         with _Prof("fwd_" + str(w.dtype)[6:], fl, nb):
             check(lib.mauv_conv2d_fwd_h16(H16[w.dtype], _p(x), xs, _p(sc), _p(sh), int(rl), _p(w),
                                           _p(y), G, B, H, W, Cin, Cout, R, R, stride, pad,
                                           _p(sm), _p(s2), _p(sn), stream()), "conv2d_fwd_h16")
         return
     _f32(w, y, bias)
-    assert x.is_cuda and x.dtype == torch.float32
+    assert x.is_cuda and x.dtype == torch.float32 and x.device.index == torch.cuda.current_device()
     with _Prof("fwd", fl, nb):
         check(lib.mauv_conv2d_fwd_f32(_p(x), xs, _p(sc), _p(sh), int(rl), _p(w), _p(bias), _p(y),
                                       G, B, H, W, Cin, Cout, R, R, stride, pad, _p(sm), _p(s2),
@@ -181,7 +189,7 @@ def conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, R, stride, pad,
     if dy.dtype in H16:
         _h16(dy.dtype, dy)
         _f32(ws)
-        assert x.is_cuda and x.dtype == dy.dtype
+        assert x.is_cuda and x.dtype == dy.dtype and x.device.index == torch.cuda.current_device()
         with _Prof("wgrad_" + str(dy.dtype)[6:], fl, nb):
             check(lib.mauv_conv2d_bwd_weight_h16(H16[dy.dtype], _p(x), xs, _p(sc), _p(sh), int(rl),
                                                  _p(dy), _p(ws), splits, G, B, H, W, Cin, Cout,

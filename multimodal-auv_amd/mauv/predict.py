@@ -112,12 +112,14 @@ def multimodal_predict_and_save(multimodal_model, dataloader, device, csv_path,
                                 model_type="multimodal"):
     """inference/predictors.py:9-97 (model kept in .train(): BN uses batch statistics; MC
     passes under torch.amp.autocast as predictors.py:55 -> f16 trunks on a ROCm device)."""
-    device = torch.device(device)
+    from .train import loop_device, is_writer, _NullFile
+    device = torch.device(loop_device(multimodal_model, device))
     amp_device = "cuda" if device.type == "cuda" else "cpu"
     group = _shard_group(multimodal_model)
+    writer = is_writer(multimodal_model)   # MC-sharded: every rank holds the same rows
     multimodal_model.train()
     logging.info(f"CSV will be saved to: {csv_path}")
-    with open(csv_path, mode="w", newline="") as fh:
+    with (open(csv_path, mode="w", newline="") if writer else _NullFile()) as fh:
         w = csv.writer(fh)
         w.writerow(["Image Name", "Predicted Class", "Predictive Uncertainty",
                     "Aleatoric Uncertainty"])
@@ -127,6 +129,8 @@ def multimodal_predict_and_save(multimodal_model, dataloader, device, csv_path,
                 bathy = bathy.to(device, non_blocking=True)
                 sss = sss.to(device, non_blocking=True)
                 if hasattr(unwrap(multimodal_model), "mc_forward"):
+                    if group is not None:
+                        multimodal_model.check_same_batch(inputs.size(0))
                     with torch.amp.autocast(device_type=amp_device):
                         st = mc_statistics(multimodal_model, inputs, bathy, sss,
                                            num_mc_samples, group=group)

@@ -126,6 +126,35 @@ def mc_train_step(model, inputs_tuple, labels, criterion, optimizer, num_mc, bat
                 scaled_kl=scaled_kl.detach(), stepped=stepped)
 
 
+def loop_device(model, device):
+    """The device a loop moves its batches to.  Under torchrun the mauv model sits on this
+    rank's GPU (mauv.device.move_model_to_device) while the reference scripts keep passing
+    ``devices[0]`` to the loops (Example_training_from_scratch.py:93): the batches follow the
+    model, as they must for its kernels.  Foreign models keep the caller's device."""
+    core = unwrap(model)
+    if hasattr(core, "mc_forward"):
+        for p in core.parameters():
+            if p.is_cuda and p.device != torch.device(device):
+                return p.device
+            break
+    return device
+
+
+def is_writer(model):
+    """Only rank 0 of a DistributedMC job writes CSV rows, plots and checkpoints; the other
+    ranks run the same batches and collectives."""
+    return not (getattr(model, "_mauv_wrapper", False) and getattr(model, "world", 1) > 1
+                and getattr(model, "rank", 0) != 0)
+
+
+def sum_ranks(model, values):
+    """Element-wise sum of a list of floats over the ranks of a DistributedMC job (identity
+    on one process)."""
+    if hasattr(model, "sum_ranks") and getattr(model, "world", 1) > 1:
+        return model.sum_ranks(values)
+    return list(values)
+
+
 def _batch_to(batch, device, bathy_patch_type, sss_patch_type):
     inputs = batch["main_image"].to(device, non_blocking=True)
     labels = batch["label"].long().to(device, non_blocking=True)
@@ -140,6 +169,19 @@ def _batch_to(batch, device, bathy_patch_type, sss_patch_type):
     return inputs, labels, bathy, sss
 
 
+class _NullFile:
+    """What a non-writing rank "opens" instead of the CSV file."""
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+    def write(self, s):
+        return len(s)
+
+
 def _patch_tag(t, kind):
     return t.replace("patch_", "").replace(f"_{kind}", "") if t else "none"
 
@@ -150,11 +192,13 @@ def train_multimodal_model(multimodal_model, dataloader, criterion, optimizer, e
     """train/multimodal.py:25-202 -> (train_loss, train_accuracy)."""
     from .checkpointing import save_model
     multimodal_model.train()
+    device = loop_device(multimodal_model, device)
+    writer = is_writer(multimodal_model)
     csv_path = str(Path(csv_path))
     sss_tag, bathy_tag = _patch_tag(sss_patch_type, "sss"), _patch_tag(bathy_patch_type, "bathy")
     new_file = not os.path.isfile(csv_path)
     try:
-        with open(csv_path, mode="a", newline="") as fh:
+        with (open(csv_path, mode="a", newline="") if writer else _NullFile()) as fh:
             w = csv.writer(fh)
             if new_file:
                 w.writerow(["Epoch", "Model type", "Loss", "Accuracy", "lr", "kl loss",
@@ -177,6 +221,8 @@ def train_multimodal_model(multimodal_model, dataloader, criterion, optimizer, e
                 sum_writer.add_scalar("Loss/train", lv, i)
                 logging.info(f"[Epoch {epoch} | Batch {i}] Loss: {lv:.4f}, "
                              f"Accuracy: {correct / max(total, 1):.4f}")
+            # DistributedMC: the epoch's figures over every rank's batches
+            total_loss, correct, total = sum_ranks(multimodal_model, [total_loss, correct, total])
             train_accuracy = correct / total
             train_loss = total_loss / total
             lr = optimizer.param_groups[0]["lr"]
@@ -184,12 +230,13 @@ def train_multimodal_model(multimodal_model, dataloader, criterion, optimizer, e
                          f"Accuracy: {train_accuracy:.4f}, LR: {lr:.6f}")
             w.writerow([epoch, model_type, train_loss, train_accuracy, lr,
                         last["scaled_kl"].item(), last["ce"].item(), sss_tag, bathy_tag])
-        if epoch % 5 == 0:
+        if epoch % 5 == 0 and writer:
             save_model(multimodal_model, csv_path,
                        f"{model_type}_bathy_patch{bathy_tag}_sss_patch{sss_tag}")
     except Exception:
-        save_model(multimodal_model, csv_path,
-                   f"{model_type}_bathy_patch{bathy_tag}_sss_patch{sss_tag}")
+        if writer:
+            save_model(multimodal_model, csv_path,
+                       f"{model_type}_bathy_patch{bathy_tag}_sss_patch{sss_tag}")
         logging.error(f"Error at epoch {epoch}", exc_info=True)
         train_loss, train_accuracy = 0.0, 0.0
     return train_loss, train_accuracy
@@ -264,12 +311,16 @@ class _EvalEpoch:
 def evaluate_multimodal_model(multimodal_model, dataloader, device, epoch, total_num_epochs,
                               num_mc, model_type, bathy_patch_type=None, sss_patch_type=None,
                               csv_path=""):
-    """train/multimodal.py:204-369 -> test accuracy (BN stays in train mode, :232)."""
+    """train/multimodal.py:204-369 -> test accuracy (BN stays in train mode, :232).
+    DistributedMC: accuracy, loss and the uncertainty means are taken over every rank's
+    batches; rank 0 writes the row and the confusion plot."""
     multimodal_model.train()
+    device = loop_device(multimodal_model, device)
+    writer = is_writer(multimodal_model)
     csv_path = str(Path(csv_path))
     new_file = not os.path.isfile(csv_path)
     try:
-        with open(csv_path, mode="a", newline="") as fh:
+        with (open(csv_path, mode="a", newline="") if writer else _NullFile()) as fh:
             w = csv.writer(fh)
             if new_file:
                 w.writerow(["Epoch", "Model Type", "Test Loss", "Test Accuracy",
@@ -288,11 +339,21 @@ def evaluate_multimodal_model(multimodal_model, dataloader, device, epoch, total
                     ep = ep or _EvalEpoch(logits.shape[2])
                     pu = st["predictive_entropy"]
                     ep.add(ce + kl_scaled, labels, predicted, pu=pu, mu=pu - st["aleatoric"])
-            test_accuracy = ep.correct_count() / ep.total
-            test_loss = ep.loss_sum() / len(dataloader)
-            _confusion_png(ep.confusion(), csv_path, model_type, epoch)
-            w.writerow([epoch + 1, model_type, test_loss, test_accuracy, np.mean(ep.values("pu")),
-                        np.mean(ep.values("mu")), kl_scaled.item(), ce.item(),
+            pu, mu = ep.values("pu"), ep.values("mu")
+            correct, total, loss_sum, nb, pu_s, mu_s, n_u = sum_ranks(
+                multimodal_model, [ep.correct_count(), ep.total, ep.loss_sum(), len(dataloader),
+                                   float(np.sum(pu, dtype=np.float64)),
+                                   float(np.sum(mu, dtype=np.float64)), pu.size])
+            test_accuracy = correct / total
+            test_loss = loss_sum / nb
+            if nb == len(dataloader):   # one process: the reference's float32 means
+                pu_m, mu_m = np.mean(pu), np.mean(mu)
+            else:
+                pu_m, mu_m = pu_s / n_u, mu_s / n_u
+            if writer:
+                _confusion_png(ep.confusion(), csv_path, model_type, epoch)
+            w.writerow([epoch + 1, model_type, test_loss, test_accuracy, pu_m,
+                        mu_m, kl_scaled.item(), ce.item(),
                         bathy_patch_type or "patch_30_bathy", sss_patch_type or "patch_30_sss"])
             logging.info(f"Epoch {epoch + 1}: Test Loss: {test_loss:.4f}, "
                          f"Accuracy: {test_accuracy:.4f}")
@@ -311,6 +372,7 @@ def train_unimodal_model(model, dataloader, criterion, optimizer, epoch, total_n
     """train/unimodal.py:21-175 -> (train_accuracy, train_loss) (note the reference's order)."""
     from .checkpointing import save_model
     model.train()
+    device = loop_device(model, device)
     model.to(device)
     kl_w = kl_weight_for(epoch, total_num_epochs)
     new_file = not os.path.isfile(csv_path)
@@ -360,6 +422,7 @@ def evaluate_unimodal_model(model, dataloader, device, epoch, csv_path, total_nu
                             model_type="image", patch_type=None):
     """train/unimodal.py:178-365 -> accuracy (epistemic = var over MC, eps 1e-7 entropy)."""
     model.train()
+    device = loop_device(model, device)
     kl_w = kl_weight_for(epoch, total_num_epochs)
     new_file = not os.path.isfile(csv_path)
     try:

@@ -71,6 +71,56 @@ def oracle64(o, store, fn):
     return o64, out
 
 
+def oracle_replay(o, store, fn, dtype=torch.float32, device="cpu"):
+    """``fn(copy)`` on a copy of the oracle moved to ``device`` / ``dtype``, replaying the
+    recorded epsilons (EpsBridge.collect) in the same per-layer order.  With device="cuda"
+    and ``fn`` running under torch.autocast this is the reference's own mixed-precision
+    scheme (inference/predictors.py:55) on the same weights and epsilons: the bar for the
+    16-bit HIP paths."""
+    import copy
+    oc = copy.deepcopy(o).to(device=device, dtype=dtype)
+    for p in oc.parameters():
+        p.grad = None
+    names = {id(mod): n for n, mod in oc.named_modules()}
+    cnt = {}
+
+    def src(layer, name, shape):
+        k = (names[id(layer)], name)
+        i = cnt.get(k, 0)
+        cnt[k] = i + 1
+        return store[k][i].to(dtype).reshape(shape)
+    bayes_ref.set_eps_source(src)
+    try:
+        out = fn(oc)
+    finally:
+        bayes_ref.set_eps_source(None)
+    return oc, out
+
+
+def cosines(params, truth_params):
+    """name -> cosine similarity of each parameter's gradient with the truth's gradient
+    (tensors whose true gradient is zero are skipped)."""
+    out = {}
+    for (n, p), pt in zip(params, truth_params):
+        if pt.grad is None or p.grad is None:
+            continue
+        t = pt.grad.detach().double().cpu().flatten()
+        if t.norm() == 0:
+            continue
+        a = p.grad.detach().double().cpu().flatten()
+        out[n] = float(a @ t / (a.norm() * t.norm() + 1e-300))
+    return out
+
+
+def spread_head(*models, gain=30.0):
+    """Make a random-init model's argmax depend on its input (tests of class agreement): the
+    last layer's mean weights scaled, its mean bias zeroed, identically in every model."""
+    with torch.no_grad():
+        for m in models:
+            m.fc2.mu_weight.mul_(gain)
+            m.fc2.mu_bias.zero_()
+
+
 def grad_error_profile(hip_params, cpu_params, truth_params):
     """Per-tensor max-relative errors of HIP and CPU-fp32 grads vs the fp64 truth."""
     hip, cpu = [], []

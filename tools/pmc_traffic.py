@@ -31,6 +31,15 @@ def load(d, counter):
     return out
 
 
+def library_sha16():
+    import hashlib
+    import os
+    so = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                      "multimodal-auv_amd", "mauv", "libmauv_hip.so")
+    with open(so, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def main(fetch_dir, write_dir, out_json, fam=None):
     fe, wr = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
     agg = defaultdict(lambda: [0, 0, 0.0, 0.0])
@@ -50,7 +59,9 @@ def main(fetch_dir, write_dir, out_json, fam=None):
                       "conv_h16": "conv_h16 (conv_pipe16 + conv_gemm_h16)"}[fam],
            "bytes_per_launch": round(conv["bytes_per_launch"]),
            "launches": conv["launches"], "per_family": rows,
-           "method": "2*FETCH_SIZE + WRITE_SIZE (rocprofv3 PMC, separate passes, KiB units)"}
+           "method": "2*FETCH_SIZE + WRITE_SIZE (rocprofv3 PMC, separate passes, KiB units)",
+           # the library the passes profiled: bench.py reports whether its own matches
+           "library_sha16": library_sha16()}
     with open(out_json, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
     for k, v in sorted(rows.items(), key=lambda kv: -(kv[1]["read_bytes"] + kv[1]["write_bytes"]))[:15]:
