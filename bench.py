@@ -517,8 +517,8 @@ def main():
                     "optical_px": args.optical, "ms_per_batch": round(d / nb * 1e3, 2),
                     "sharding": "mc" if world > 1 else "none", "mc_chunk": ck,
                     "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)}
-            except torch.OutOfMemoryError as e:
-                infer_sweep[name] = {"error": "out of memory", "detail": str(e)[:200]}
+            except Exception as e:   # a leg that fails is reported; the headline still prints
+                infer_sweep[name] = {"error": type(e).__name__, "detail": str(e)[:200]}
             finally:
                 batches = None
 

@@ -342,6 +342,19 @@ int mauv_stage_u8(const unsigned char* x, int B, int H, int W, int C, const floa
                   const float* dist, float depth, float* out, hipStream_t stream);
 int mauv_uifm(const float* x, int B, int C, int H, int W, const float* bt, const float* binf,
               const float* dist, float depth, float* out, hipStream_t stream);
+/* data/datasets.py:240-246 transforms.Resize((256, 256)) of the decoded tiles = PIL's
+ * Image.resize(size, BILINEAR) (antialiased when downscaling), bit-exact with Pillow's 8-bit
+ * separable resampler (libImaging/Resample.c; the reference pins pillow 11.0.0): uint8
+ * [B][H][W][C] (1 <= C <= 4) -> uint8 [B][Ho][Wo][C] (out_u8), or — out_f32 instead — the
+ * resized tile through mauv_stage_u8's ToTensor / Normalize / UIFM maths into fp32 NCHW
+ * [B][C][Ho][Wo] in the same pass (mean/std, uifm_bt/binf, dist [B][1][Ho][Wo] nullable as
+ * there).  workspace: mauv_resize_workspace_bytes(...) device bytes (coefficient tables and
+ * the 8-bit horizontal-pass image), caller-owned; -1 = bad shape. */
+long long mauv_resize_workspace_bytes(int B, int H, int W, int C, int Ho, int Wo);
+int mauv_resize_u8(const unsigned char* x, int B, int H, int W, int C, int Ho, int Wo,
+                   void* workspace, unsigned char* out_u8, const float* mean, const float* stdv,
+                   const float* uifm_bt, const float* uifm_binf, const float* dist, float depth,
+                   float* out_f32, hipStream_t stream);
 
 /* ---- evaluation metrics (metrics.hip) ----------------------------------------------------
  * train/multimodal.py:312-347 (confusion matrix) and Examples/"Example training with image

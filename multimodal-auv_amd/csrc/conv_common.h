@@ -119,6 +119,29 @@ __device__ __forceinline__ unsigned udiv16(unsigned n, unsigned m) {
   return m ? __umulhi(n, m) : n;
 }
 
+// A forward whose input exceeds the pipelined kernels' 31-bit buffer offsets (configs[4]'s
+// 512 px sonar at B = 256: 2^31 bytes of layer-1 activations per MC group) runs as launches
+// over batch chunks: images are independent in a forward, every chunk covers whole 128-row
+// tiles (its statistics blocks start at st_base), y rows are written through plain pointers.
+// esz: bytes per element.  false: no chunking possible (the caller falls back).
+template <class F>
+bool conv_fwd_batch_chunks(const ConvArgs& a0, long long lim, int esz, F launch) {
+  const long long hw = (long long)a0.Ho * a0.Wo;
+  int bc = (int)(lim / a0.xs_b);
+  while (bc > 0 && (bc * hw) % 128) --bc;
+  if (bc <= 0 || a0.xs_b <= 0) return false;
+  for (int b0 = 0; b0 < a0.B; b0 += bc) {
+    ConvArgs c = a0;
+    c.B = a0.B - b0 < bc ? a0.B - b0 : bc;
+    c.M = (int)(c.B * hw);
+    c.x = (const float*)((const char*)a0.x + (long long)b0 * a0.xs_b * esz);
+    c.out = (float*)((char*)a0.out + (long long)b0 * hw * a0.N * esz);
+    c.st_base = a0.st_base + (int)(b0 * hw / 128);
+    if (!launch(c)) return false;
+  }
+  return true;
+}
+
 // Launch the pipelined split-fp32 kernel (conv_split.hip) for an fp32 conv; false when the
 // problem is outside its vector paths (the caller then runs conv_gemm.hip's kernels).
 bool conv_split_launch(int mode, const ConvArgs& a, int oneacc, hipStream_t st);

@@ -661,7 +661,25 @@ MAUV_API int mauv_stem_fwd_f32(const float* cols, const float* w, float* y, int 
   a.st_mean = st_mean; a.st_m2 = st_m2; a.st_cnt = st_cnt;
   a.st_nblk = stat_blocks(M, Cout, G); a.st_base = 0;
   const int fm = f32_math();
-  if ((fm == 6 || fm == 5) && conv_split_launch(FWD, a, fm == 5, stream)) return check_launch("stem_fwd_f32");
+  if (fm == 6 || fm == 5) {
+    // the split kernel reads cols by a buffer descriptor (31-bit byte offsets): more rows
+    // (configs[4]'s 512 px sonar at B = 256) go in chunks of whole 128-row tiles, each writing
+    // its rows of y and its statistics blocks (st_base)
+    const long long lim_rows = (0x7fff0000LL / 4 / Kp) / 128 * 128;
+    bool ok = true;
+    for (long long r0 = 0; r0 < M && ok; r0 += lim_rows) {
+      ConvArgs c = a;
+      c.M = (int)(M - r0 < lim_rows ? M - r0 : lim_rows);
+      c.W = c.Wo = c.M;                        // cols as one 1 x M image of Kp channels
+      c.xs_h = c.xs_b = (long long)c.M * Kp;
+      c.x = cols + r0 * Kp;
+      c.out = y + r0 * Cout;
+      c.st_base = (int)(r0 / 128);
+      ok = conv_split_launch(FWD, c, fm == 5, stream);
+      if (!ok && r0 > 0) { set_error("stem_fwd_f32: chunk outside the split kernel"); return kErrArg; }
+    }
+    if (ok) return check_launch("stem_fwd_f32");
+  }
   if (Kp % 32 == 0) launch_tiles<FWD, true, true>(a, stream);
   else launch_tiles<FWD, false, true>(a, stream);
   return check_launch("stem_fwd_f32");

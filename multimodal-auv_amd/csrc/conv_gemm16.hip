@@ -566,7 +566,21 @@ MAUV_API int mauv_stem_fwd_h16(int dtype, const void* cols, const void* w, void*
   h.st_nblk = ceil_div(M, conv_tile_rows(M));
   ConvArgs a = pipe_args(h);
   a.cpg = Cout;
-  if (!conv_pipe16_launch(FWD, dtype, a, stream)) { set_error("stem_fwd_h16: shape outside the pipelined kernel"); return kErrArg; }
+  // the pipelined kernel reads cols by a buffer descriptor (31-bit byte offsets): rows beyond
+  // that (configs[4]'s 512 px sonar at B = 256: 16.8 M rows) go in chunks of whole 128-row
+  // tiles, each writing its rows of y and its statistics blocks (st_base)
+  const long long lim_rows = (0x7fff0000LL / 2 / Kp) / 128 * 128;
+  for (long long r0 = 0; r0 < M; r0 += lim_rows) {
+    ConvArgs c = a;
+    c.M = (int)(M - r0 < lim_rows ? M - r0 : lim_rows);
+    // cols as one 1 x M "image" of Kp channels (make_args16 above): the chunk is 1 x c.M
+    c.W = c.Wo = c.M;
+    c.xs_h = c.xs_b = (long long)c.M * Kp;
+    c.x = (const float*)((const u16*)cols + r0 * Kp);
+    c.out = (float*)((u16*)y + r0 * Cout);
+    c.st_base = (int)(r0 / 128);
+    if (!conv_pipe16_launch(FWD, dtype, c, stream)) { set_error("stem_fwd_h16: shape outside the pipelined kernel"); return kErrArg; }
+  }
   return check_launch("stem_fwd_h16");
 }
 

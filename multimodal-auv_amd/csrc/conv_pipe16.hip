@@ -458,10 +458,10 @@ void conv_pipe16(const ConvArgs a) {
       const int mt = m0 / BM;
       const int col = n0 + tid;
       const int gc = a.cpg ? col / a.cpg : g, cc = a.cpg ? col % a.cpg : col;
-      const long long so = ((long long)gc * a.st_nblk + mt) * (a.cpg ? a.cpg : a.N) + cc;
+      const long long so = ((long long)gc * a.st_nblk + a.st_base + mt) * (a.cpg ? a.cpg : a.N) + cc;
       a.st_mean[so] = t1 / (float)nvalid;
       a.st_m2[so] = t2;
-      if (cc == 0) a.st_cnt[(long long)gc * a.st_nblk + mt] = (float)nvalid;
+      if (cc == 0) a.st_cnt[(long long)gc * a.st_nblk + a.st_base + mt] = (float)nvalid;
     }
     __syncthreads();  // red is overwritten by the staged store below
   }
@@ -566,6 +566,10 @@ static void pipe16_dt(int dt, const ConvArgs& a, hipStream_t st) {
 bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
   const long long lim = 0x7fff0000LL / 2;  // elements addressable by a 31-bit byte offset
   const long long nx = (long long)a0.B * a0.xs_b, ny = (long long)a0.B * a0.Ho * a0.Wo * a0.Cout;
+  if (mode == FWD && nx > lim && !a0.cpg)
+    return conv_fwd_batch_chunks(a0, lim, 2, [&](const ConvArgs& c) {
+      return conv_pipe16_launch(FWD, dt, c, st);
+    });
   // (the FWD output is stored through plain pointers: only dgrad / wgrad read y by rsrc)
   if (nx > lim || (mode != FWD && ny > lim) || a0.ws_g > lim) return false;
   const bool xs8 = a0.xs_w % 8 == 0 && a0.xs_h % 8 == 0 && a0.xs_b % 8 == 0 && a0.xs_g % 8 == 0;

@@ -452,6 +452,10 @@ static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
 bool conv_split_launch(int mode, const ConvArgs& a0, int oneacc, hipStream_t st) {
   const long long lim = 0x7fff0000LL / 4;  // floats addressable by a 31-bit byte offset
   const long long nx = (long long)a0.B * a0.xs_b, ny = (long long)a0.B * a0.Ho * a0.Wo * a0.Cout;
+  if (mode == FWD && nx > lim && !a0.cpg && a0.xs_g != 0)
+    return conv_fwd_batch_chunks(a0, lim, 4, [&](const ConvArgs& c) {
+      return conv_split_launch(FWD, c, oneacc, st);
+    });
   // (the FWD output is stored through plain pointers: only dgrad / wgrad read y by rsrc)
   if (nx > lim || (mode != FWD && ny > lim) || a0.ws_g > lim) return false;
   ConvArgs a = a0;

@@ -90,13 +90,15 @@ SIGNATURES = {
     # staging.hip
     "mauv_stage_u8": [P, I, I, I, I, P, P, P, P, P, F, P, P],
     "mauv_uifm": [P, I, I, I, I, P, P, P, F, P, P],
+    "mauv_resize_workspace_bytes": [I, I, I, I, I, I],
+    "mauv_resize_u8": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, F, P, P],
     # metrics.hip
     "mauv_confusion_update": [P, P, I, I, P, P],
     "mauv_calibration_update": [P, P, I, I, I, P, P, P],
     "mauv_auroc_pairs": [P, P, I, P, P],
 }
 _RESTYPES = {"mauv_last_error": ctypes.c_char_p, "mauv_bn_workspace_floats": LL,
-             "mauv_bn_stats_workspace_floats": LL}
+             "mauv_bn_stats_workspace_floats": LL, "mauv_resize_workspace_bytes": LL}
 
 
 class MauvError(RuntimeError):

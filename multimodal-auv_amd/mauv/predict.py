@@ -112,7 +112,7 @@ def multimodal_predict_and_save(multimodal_model, dataloader, device, csv_path,
                                 model_type="multimodal"):
     """inference/predictors.py:9-97 (model kept in .train(): BN uses batch statistics; MC
     passes under torch.amp.autocast as predictors.py:55 -> f16 trunks on a ROCm device)."""
-    from .train import loop_device, is_writer, _NullFile
+    from .train import loop_device, is_writer, _NullFile, _tile_to
     device = torch.device(loop_device(multimodal_model, device))
     amp_device = "cuda" if device.type == "cuda" else "cpu"
     group = _shard_group(multimodal_model)
@@ -125,9 +125,9 @@ def multimodal_predict_and_save(multimodal_model, dataloader, device, csv_path,
                     "Aleatoric Uncertainty"])
         with torch.no_grad():
             for batch_idx, (inputs, bathy, sss, image_name) in enumerate(dataloader):
-                inputs = inputs.to(device, non_blocking=True)
-                bathy = bathy.to(device, non_blocking=True)
-                sss = sss.to(device, non_blocking=True)
+                inputs = _tile_to(inputs, device, optical=True)   # uint8 tiles: staged
+                bathy = _tile_to(bathy, device)                    # on the device
+                sss = _tile_to(sss, device)
                 if hasattr(unwrap(multimodal_model), "mc_forward"):
                     if group is not None:
                         multimodal_model.check_same_batch(inputs.size(0))

@@ -155,17 +155,25 @@ def sum_ranks(model, values):
     return list(values)
 
 
+def _tile_to(t, device, optical=False):
+    """Move one image batch to the device; decoded uint8 HWC tiles (4x fewer bytes over PCIe
+    than the reference's fp32 tensors) get datasets.py:239-250's Resize / ToTensor /
+    Normalize on the device (mauv.staging, bit-exact with PIL + torchvision)."""
+    t = t.to(device, non_blocking=True)
+    if t.dtype == torch.uint8 and t.is_cuda:
+        from .staging import stage_tile_batch
+        t = stage_tile_batch(t, optical)
+    return t
+
+
 def _batch_to(batch, device, bathy_patch_type, sss_patch_type):
-    inputs = batch["main_image"].to(device, non_blocking=True)
+    inputs = _tile_to(batch["main_image"], device, optical=True)
     labels = batch["label"].long().to(device, non_blocking=True)
-    bathy = batch["bathy_image"].to(device, non_blocking=True)
-    sss = batch["sss_image"].to(device, non_blocking=True)
     # only the selected patch tensors move to the device (the reference copies all of them)
     pb, ps = batch.get("patch_bathy", {}), batch.get("patch_sss", {})
-    if bathy_patch_type in pb:
-        bathy = pb[bathy_patch_type].to(device, non_blocking=True)
-    if sss_patch_type in ps:
-        sss = ps[sss_patch_type].to(device, non_blocking=True)
+    bathy = _tile_to(pb[bathy_patch_type] if bathy_patch_type in pb else batch["bathy_image"],
+                     device)
+    sss = _tile_to(ps[sss_patch_type] if sss_patch_type in ps else batch["sss_image"], device)
     return inputs, labels, bathy, sss
 
 

@@ -112,13 +112,16 @@ def cosines(params, truth_params):
     return out
 
 
-def spread_head(*models, gain=30.0):
-    """Make a random-init model's argmax depend on its input (tests of class agreement): the
-    last layer's mean weights scaled, its mean bias zeroed, identically in every model."""
+def center_head(mean_logits, *models, gain=1.0):
+    """Make a random-init model's argmax depend on its input (tests of class agreement): at
+    random init every item's logits sit near one bias-dominated point (every golden class is
+    4), so the last layer's mean bias is shifted by the batch's mean logits ``mean_logits``
+    [C] and the layer scaled by ``gain`` — identically in every model given."""
     with torch.no_grad():
         for m in models:
+            m.fc2.mu_bias.sub_(mean_logits.to(m.fc2.mu_bias.device))
+            m.fc2.mu_bias.mul_(gain)
             m.fc2.mu_weight.mul_(gain)
-            m.fc2.mu_bias.zero_()
 
 
 def grad_error_profile(hip_params, cpu_params, truth_params):

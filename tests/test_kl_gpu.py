@@ -13,10 +13,10 @@ pytestmark = pytest.mark.gpu
 def _rebind(model, gen):
     """Give two non-first layers fresh storages (new pointers, new values)."""
     conv = model.bathy_model_feat.layer2[1].conv2
-    conv.rho_kernel.data = conv.rho_kernel.data.clone() - 0.5 * torch.rand(
+    conv.rho_kernel.data = conv.rho_kernel.data.clone() - 2.0 * torch.rand(
         conv.rho_kernel.shape, generator=gen).to(conv.rho_kernel.device)
     fc1 = model.fc1
-    fc1.mu_weight.data = fc1.mu_weight.data.clone() + 0.1 * torch.randn(
+    fc1.mu_weight.data = fc1.mu_weight.data.clone() + 1.0 * torch.randn(
         fc1.mu_weight.shape, generator=gen).to(fc1.mu_weight.device)
 
 
@@ -30,7 +30,8 @@ def test_kl_follows_rebound_parameters():
     torch.cuda.synchronize()
     ref = bayes_ref.get_kl_loss(o)
     kl = get_kl_loss(m)
-    assert abs(kl.item() - kl0) > 1e-3 * abs(kl0)    # the change is visible at all
+    assert abs(kl.item() - kl0) > 1e-4 * abs(kl0)    # 10x the tolerance below: visible
+    print(f"KL {kl0:.4f} -> {kl.item():.4f} (oracle {ref.item():.4f})")
     assert abs(kl.item() - ref.item()) <= 1e-5 * abs(ref.item()), (kl.item(), ref.item())
     # the backward writes dKL into the re-bound parameters' gradients
     ref.backward()
