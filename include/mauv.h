@@ -105,6 +105,20 @@ int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, void* dx,
                              const void* addend, int accumulate, int G, int B, int H, int W,
                              int Cin, int Cout, int R, int S, int stride, int pad,
                              hipStream_t stream);
+/* the same data gradient with w_rsck (nullable) = the weights transposed to
+ * [G][R][S][Cin][Cout] by mauv_weights_rsck_h16: both GEMM operands are then k-contiguous rows
+ * and the LDS-DMA kernel (conv_dma16.hip) runs the shapes it covers (Cout % 64 == 0, >= 128
+ * rows and input channels); others take the pipelined kernel over w. */
+int mauv_conv2d_bwd_data_h16_t(int dtype, const void* dy, const void* w, const void* w_rsck,
+                               void* dx, const void* addend, int accumulate, int G, int B, int H,
+                               int W, int Cin, int Cout, int R, int S, int stride, int pad,
+                               hipStream_t stream);
+/* 1 (default, env MAUV_DMA16) = the LDS-DMA kernels run the 16-bit convs they cover, 0 = the
+ * pipelined register-staged kernels; -1 queries.  Returns the previous setting. */
+int mauv_set_dma16(int on);
+/* 16-bit KRSC [G][Cout][RS][Cin] -> RSCK [G][RS][Cin][Cout] (Cout, Cin % 8 == 0). */
+int mauv_weights_rsck_h16(const void* w, void* w_rsck, int G, int Cout, int RS, int Cin,
+                          hipStream_t stream);
 int mauv_conv2d_bwd_weight_h16(int dtype, const void* x, const long long* x_strides,
                                const float* x_scale, const float* x_shift, int x_relu,
                                const void* dy, float* ws, int splits, int G, int B, int H, int W,

@@ -41,6 +41,8 @@ BN_RELU_MASK = os.environ.get("MAUV_BN_RELU_MASK", "1") == "1"
 # The stems as ONE GEMM over im2col rows shared by the G samples, the G weight sets stacked
 # along N (stem.hip), instead of G implicit GEMMs over channel-padded pixels.
 STEM_GEMM = os.environ.get("MAUV_STEM_GEMM", "1") == "1"
+# 16-bit data gradients on the LDS-DMA kernel over RSCK-transposed weights (conv_dma16.hip)
+DMA_DGRAD = os.environ.get("MAUV_DMA_DGRAD", "1") == "1"
 _STREAMS = {}
 
 
@@ -402,8 +404,13 @@ class TrunkRunner(_Runner):
             return None
         if dx is None:
             dx = torch.empty(G, B, H, W, Cin, device=dy.device, dtype=self.dt)
+        wt = None
+        if DMA_DGRAD and self.dt != torch.float32 and Cout % 64 == 0 and Cin >= 128 and cp == Cin:
+            # the LDS-DMA data gradient reads the weights as [R][S][Cin][Cout] rows
+            wt = torch.empty(G, k * k, Cin, Cout, device=dy.device, dtype=self.dt)
+            ops.weights_rsck(w, G, Cout, k * k, Cin, wt)
         ops.conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, k, st, pd, addend=addend,
-                            accumulate=accumulate)
+                            accumulate=accumulate, w_rsck=wt)
         return dx
 
     def _stem(self, conv, x, B, H, W):

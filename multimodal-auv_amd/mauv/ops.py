@@ -145,10 +145,24 @@ def dgrad_stat_blocks(G, B, H, W, Cin, Cout, R, stride, pad):
     return lib.mauv_conv2d_bwd_data_stat_blocks(G, B, H, W, Cin, Cout, R, R, stride, pad)
 
 
+def set_dma16(on):
+    """Select the LDS-DMA 16-bit conv kernels (True, default) or the pipelined register-staged
+    ones (False), process-wide; returns the previous setting."""
+    return bool(lib.mauv_set_dma16(int(bool(on))))
+
+
+def weights_rsck(w, G, Cout, RS, Cin, out):
+    """16-bit KRSC [G][Cout][RS][Cin] -> RSCK [G][RS][Cin][Cout] (the LDS-DMA data gradient's
+    B operand)."""
+    _h16(w.dtype, w, out)
+    check(lib.mauv_weights_rsck_h16(_p(w), _p(out), G, Cout, RS, Cin, stream()), "weights_rsck_h16")
+
+
 def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=None,
-                    accumulate=False, bn=None):
+                    accumulate=False, bn=None, w_rsck=None):
     """bn = dict(y, out|None, scale, shift, mean, invstd, relu, p1, p2): dx is the output
-    gradient of that BatchNorm; the epilogue writes its backward partial sums into p1/p2."""
+    gradient of that BatchNorm; the epilogue writes its backward partial sums into p1/p2.
+    w_rsck (16-bit only): the weights transposed by weights_rsck (LDS-DMA kernel)."""
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
     b = bn or {}
     fl = 2.0 * G * B * Ho * Wo * Cout * R * R * Cin
@@ -159,10 +173,12 @@ def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=Non
     if w.dtype in H16:
         assert bn is None, "16-bit dgrad has no BN-partials epilogue"
         _h16(w.dtype, dy, w, dx, addend)
+        _h16(w.dtype, w_rsck)
         with _Prof("dgrad_" + str(w.dtype)[6:], fl, nb, nl):
-            check(lib.mauv_conv2d_bwd_data_h16(H16[w.dtype], _p(dy), _p(w), _p(dx), _p(addend),
-                                               int(accumulate), G, B, H, W, Cin, Cout, R, R,
-                                               stride, pad, stream()), "conv2d_bwd_data_h16")
+            check(lib.mauv_conv2d_bwd_data_h16_t(H16[w.dtype], _p(dy), _p(w), _p(w_rsck), _p(dx),
+                                                 _p(addend), int(accumulate), G, B, H, W, Cin,
+                                                 Cout, R, R, stride, pad, stream()),
+                  "conv2d_bwd_data_h16")
         return
     _f32(dy, w, dx, addend)
     with _Prof("dgrad", fl, nb, nl):
