@@ -42,6 +42,13 @@ F32_PEAK_TF = {"split": BF16_MFMA_PEAK_TF / 6, "split1": BF16_MFMA_PEAK_TF / 6,
                "split3": BF16_MFMA_PEAK_TF / 3, "exact": FP32_MFMA_PEAK_TF}
 
 
+def progress(msg):
+    """One line per bench leg on rank 0's stderr (a run that prints nothing for minutes looks
+    hung to the harness)."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def synthetic_batch(B, S_opt, S_son, device, seed):
     g = torch.Generator(device="cpu").manual_seed(seed)
     x = torch.randn(B, 3, S_opt, S_opt, generator=g)
@@ -369,7 +376,9 @@ def main():
         return t
 
     exact = None
+    progress("roofline step done")
     if args.dtype == "fp32" and args.exact_steps > 0 and f32_math != "exact":
+        progress("exact-f32 leg")
         # the same step with every fp32 product on v_mfma_f32_32x32x2_f32 (reference point)
         ops.set_f32_math("exact")
         step()
@@ -381,6 +390,7 @@ def main():
 
     bf16 = None
     if not args.no_bf16:
+        progress("bf16 leg")
         from mauv.engine import set_precision
         set_precision(model.module if world > 1 else model, torch.bfloat16)
         step()                                   # warm-up (16-bit kernels, allocator)
@@ -409,6 +419,7 @@ def main():
         legs = [(f"sonar{S}", args.sweep_batch, S, args.num_mc) for S in (128, 512)]
         legs.append(("num_mc12", args.batch, args.sonar, 12))
         for name, Bs, S, nmc in legs:
+            progress(f"train_sweep {name}")
             opt.zero_grad(set_to_none=True)
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
@@ -438,6 +449,7 @@ def main():
 
     infer = None
     if not args.no_infer:
+        progress("inference leg")
         from mauv.predict import multimodal_predict_and_save
         opt.zero_grad(set_to_none=True)
         xi, bi, si, _ = synthetic_batch(args.infer_batch, args.optical, args.sonar, dev, 99)
@@ -495,6 +507,7 @@ def main():
                 for S in (128, 512)]
         legs.append(("main_py_b8_mc12", 8, args.sonar, 12, 32))
         for name, Bi, S, Ni, nb in legs:
+            progress(f"infer_sweep {name}")
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             torch.cuda.reset_peak_memory_stats(dev)
@@ -524,6 +537,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("cpu baseline")
         cpu = cpu_baseline(args)
 
     if rank == 0:

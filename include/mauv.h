@@ -113,8 +113,9 @@ int mauv_conv2d_bwd_data_h16_t(int dtype, const void* dy, const void* w, const v
                                void* dx, const void* addend, int accumulate, int G, int B, int H,
                                int W, int Cin, int Cout, int R, int S, int stride, int pad,
                                hipStream_t stream);
-/* 1 (default, env MAUV_DMA16) = the LDS-DMA kernels run the 16-bit convs they cover, 0 = the
- * pipelined register-staged kernels; -1 queries.  Returns the previous setting. */
+/* 1 (default, env MAUV_DMA16) = the LDS-DMA kernels run the 16-bit convs they cover, 2 = also
+ * the forwards with a pending BN on x (register-staged A, DMA B), 0 = the pipelined
+ * register-staged kernels; -1 queries.  Returns the previous setting. */
 int mauv_set_dma16(int on);
 /* 16-bit KRSC [G][Cout][RS][Cin] -> RSCK [G][RS][Cin][Cout] (Cout, Cin % 8 == 0). */
 int mauv_weights_rsck_h16(const void* w, void* w_rsck, int G, int Cout, int RS, int Cin,

@@ -41,7 +41,13 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned char* l
 
 }  // namespace
 
-template <int MODE, int DT>
+constexpr int kMaxXbnD = 512;  // ABN: input channels whose pending-BN scale/shift sit in LDS
+
+// ABN (FWD only): x carries the producing layer's pending BN(+ReLU) (conv2 / conv3 of every
+// bottleneck): A is register-staged — 16-byte global loads of stage t+1 issued before the MFMAs
+// of stage t, the BN applied and the swizzled row image written after them — while B still
+// lands by DMA.
+template <int MODE, int DT, bool ABN = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_dma16(const ConvArgs a) {
   constexpr int BM = 128, BN = 128, BK = 64;
@@ -49,8 +55,11 @@ void conv_dma16(const ConvArgs a) {
   constexpr int ROWB = BK * 2;                        // bytes per LDS row
   constexpr int A_B = BM * ROWB, B_B = BN * ROWB, STG = A_B + B_B;
   constexpr int NBUF = 2, PIECES = BM / 8 / 4;        // DMA pieces per wave per operand (4)
+  constexpr int NVA = BM * 8 / 256;                   // ABN: 16-byte A chunks per thread (4)
   static_assert(BM == BN, "one piece schedule for both operands");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * STG];
+  static_assert(!ABN || MODE == FWD, "pending BN on the forward input only");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * STG + (ABN ? 8 * kMaxXbnD : 0)];
+  float* xbn = (float*)(smem + NBUF * STG);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -101,6 +110,33 @@ void conv_dma16(const ConvArgs a) {
     bbase[i] = n < a.N ? (unsigned)((MODE == FWD ? n * a.K + 8 * c : n * a.Cout + 8 * c) * 2) : kOOBd;
   }
 
+  // ---- ABN: register-staged A (thread chunk j = row (tid + 256 j) >> 3, k-chunk tid & 7) ----
+  unsigned rbase[ABN ? NVA : 1];
+  int rq0[ABN ? NVA : 1], rq1[ABN ? NVA : 1];
+  const int rc = tid & 7;
+  if constexpr (ABN) {
+#pragma unroll
+    for (int j = 0; j < NVA; ++j) {
+      const int row = (tid + 256 * j) >> 3;
+      const int m = m0 + row;
+      const bool ok = m < a.M;
+      const int mm = ok ? m : 0;
+      const int HW = a.Ho * a.Wo, b = mm / HW, rem = mm - b * HW;
+      const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+      const int p0 = oh * a.stride - a.pad, p1 = ow * a.stride - a.pad;
+      rbase[j] = (unsigned)((b * xs_b + p0 * xs_h + p1 * xs_w + 8 * rc) * 2);
+      rq0[j] = ok ? p0 : -(1 << 28);
+      rq1[j] = p1;
+    }
+    for (int i = tid; i < a.Cin; i += 256) {
+      xbn[i] = a.xsc[g * a.Cin + i];
+      xbn[kMaxXbnD + i] = a.xsh[g * a.Cin + i];
+    }
+  }
+  u32x4 areg[ABN ? NVA : 1];
+  unsigned aok = 0;
+  int a_c = 0;   // input-channel offset of the staged A registers' k slice
+
   int t_r = 0, t_s = 0, t_c = 0;  // tile-uniform k position (FWD: r, s, cin; DGRAD: tr, ts, cout)
   auto load = [&](int t, int buf) {
     unsigned char* As = smem + buf * STG;
@@ -114,14 +150,27 @@ void conv_dma16(const ConvArgs a) {
       const int r = a.r0 + a.stride * t_r, s = a.s0 + a.stride * t_s;
       boff = (unsigned)(((r * a.S + s) * a.Cin * a.Cout + t_c) * 2);
     }
+    if constexpr (ABN) {   // A into registers (BN + the LDS write after the stage's MFMAs)
+      aok = 0;
+      a_c = t_c;
 #pragma unroll
-    for (int i = 0; i < PIECES; ++i) {
-      bool ok;
-      if constexpr (MODE == FWD)
-        ok = ((unsigned)(aq0[i] + t_r) < (unsigned)a.H) & ((unsigned)(aq1[i] + t_s) < (unsigned)a.W);
-      else
-        ok = ((unsigned)(aq0[i] - t_r) < (unsigned)a.Ho) & ((unsigned)(aq1[i] - t_s) < (unsigned)a.Wo);
-      dma16(ra, As + (wave * PIECES + i) * 1024, sel_off(ok, abase[i] + soff, kOOBd));
+      for (int j = 0; j < NVA; ++j) {
+        const bool ok = ((unsigned)(rq0[j] + t_r) < (unsigned)a.H) &
+                        ((unsigned)(rq1[j] + t_s) < (unsigned)a.W);
+        areg[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                      ra, (int)sel_off(ok, rbase[j] + soff, kOOBd), 0, 0));
+        aok |= (unsigned)ok << j;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PIECES; ++i) {
+        bool ok;
+        if constexpr (MODE == FWD)
+          ok = ((unsigned)(aq0[i] + t_r) < (unsigned)a.H) & ((unsigned)(aq1[i] + t_s) < (unsigned)a.W);
+        else
+          ok = ((unsigned)(aq0[i] - t_r) < (unsigned)a.Ho) & ((unsigned)(aq1[i] - t_s) < (unsigned)a.Wo);
+        dma16(ra, As + (wave * PIECES + i) * 1024, sel_off(ok, abase[i] + soff, kOOBd));
+      }
     }
 #pragma unroll
     for (int i = 0; i < PIECES; ++i)
@@ -166,19 +215,38 @@ void conv_dma16(const ConvArgs a) {
     }
   };
 
+  // ABN: the staged A registers -> BN(+ReLU) -> swizzled row image of buffer buf
+  const unsigned rfloor = a.xrelu ? 0u : 0x80008000u;
+  auto store_a = [&](int buf) {
+    if constexpr (ABN) {
+      unsigned char* As = smem + buf * STG;
+      const floatx8 fsc = ldf8(xbn + a_c + 8 * rc), fsh = ldf8(xbn + kMaxXbnD + a_c + 8 * rc);
+#pragma unroll
+      for (int j = 0; j < NVA; ++j) {
+        const int row = (tid + 256 * j) >> 3;
+        *(u32x4*)(As + row * ROWB + ((rc ^ ((row >> 1) & 7)) << 4)) =
+            bn_relu8<DT>(areg[j], fsc, fsh, rfloor, (aok >> j) & 1);
+      }
+    }
+  };
+
+  if constexpr (ABN) __syncthreads();   // xbn staged
   load(0, 0);
+  store_a(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int t = 0; t < nt; ++t) {
     if (t + 1 < nt) load(t + 1, (t + 1) & 1);
     compute(t & 1);
+    if (t + 1 < nt) store_a((t + 1) & 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of stage t+1 landed
     __syncthreads();                                  // ... and every wave's; stage t read
   }
   epilogue16<MODE, DT, BM, BN, MI, NI, WGM, WGN, NBUF * STG>(a, acc, smem, m0, n0, g);
 }
 
-// MAUV_DMA16 (default 1) / mauv_set_dma16: 0 sends these convs to conv_pipe16.hip (A/B)
+// MAUV_DMA16 (default 1) / mauv_set_dma16: 0 sends these convs to conv_pipe16.hip (A/B); 2 also
+// runs the forwards with a pending BN on x (ABN) here
 static int g_dma16 = -1;
 static int dma16_on() {
   if (g_dma16 < 0) { const char* e = getenv("MAUV_DMA16"); g_dma16 = e ? atoi(e) : 1; }
@@ -197,14 +265,18 @@ bool conv_dma16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
   if (a0.N % 8) return false;  // the epilogue stores 8-channel rows
   if (mode == FWD) {
     const bool xs8 = a0.xs_w % 8 == 0 && a0.xs_h % 8 == 0 && a0.xs_b % 8 == 0 && a0.xs_g % 8 == 0;
-    if (a0.xsc || a0.cpg || a0.Cin % 64 || !xs8) return false;
+    if (a0.cpg || a0.Cin % 64 || !xs8 || (a0.xsc && (a0.Cin > kMaxXbnD || dma16_on() < 2)))
+      return false;
   } else {
     if (a0.Cout % 64 || a0.Cin % 8) return false;
   }
   ConvArgs a = a0;
   a.xcd_grid = conv_xcd_grid();
   dim3 grid(ceil_div(a.M, 128) * ceil_div(a.N, 128), a.G);
-  if (mode == FWD) {
+  if (mode == FWD && a.xsc) {
+    if (dt == DT_BF16) hipLaunchKernelGGL((conv_dma16<FWD, DT_BF16, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv_dma16<FWD, DT_F16, true>), grid, dim3(256), 0, st, a);
+  } else if (mode == FWD) {
     if (dt == DT_BF16) hipLaunchKernelGGL((conv_dma16<FWD, DT_BF16>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((conv_dma16<FWD, DT_F16>), grid, dim3(256), 0, st, a);
   } else {
@@ -218,6 +290,6 @@ bool conv_dma16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
 
 MAUV_API int mauv_set_dma16(int on) {
   const int prev = mauv::dma16_on();
-  if (on >= 0) mauv::g_dma16 = on ? 1 : 0;
+  if (on >= 0) mauv::g_dma16 = on;
   return prev;
 }

@@ -37,34 +37,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc16(const void* p, long lon
 __device__ __forceinline__ unsigned mdiv16(unsigned n, unsigned long long m, int s) {
   return (unsigned)(((unsigned long long)n * m) >> s);
 }
-// The producing layer's pending BN(+ReLU) on one 8-channel chunk: fp32 fma per element, one
-// round-to-nearest-even, then ReLU on the packed words as a signed-int16 max against `floor`
-// (0 with ReLU: both formats keep the sign in bit 15, so exactly the negative values and -0
-// become +0; 0x80008000 without).  Chunks outside the image (padding, ragged rows) become 0.
-template <int DT>
-__device__ __forceinline__ u32x4 bn_relu8(u32x4 v, const floatx8& sc, const floatx8& sh,
-                                          unsigned floor, bool ok) {
-  typedef short s2 __attribute__((ext_vector_type(2)));
-  u32x4 o;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float lo, hi;
-    if constexpr (DT == DT_BF16) {
-      lo = bf_lo(v[i]);
-      hi = bf_hi(v[i]);
-    } else {
-      lo = (float)__builtin_bit_cast(_Float16, (u16)(v[i] & 0xffffu));
-      hi = (float)__builtin_bit_cast(_Float16, (u16)(v[i] >> 16));
-    }
-    unsigned p = pk2<DT>(__builtin_fmaf(lo, sc[2 * i], sh[2 * i]),
-                         __builtin_fmaf(hi, sc[2 * i + 1], sh[2 * i + 1]));
-    asm("" : "+v"(p));  // keeps one v_cvt_pk per pair (else: two single conversions + v_perm)
-    const s2 m = __builtin_elementwise_max(__builtin_bit_cast(s2, p), __builtin_bit_cast(s2, floor));
-    o[i] = ok ? __builtin_bit_cast(unsigned, m) : 0u;
-  }
-  return o;
-}
-
 template <int NVA, int NVB>
 struct Stage16 {
   u32x4 a[NVA], b[NVB];

@@ -145,10 +145,11 @@ def dgrad_stat_blocks(G, B, H, W, Cin, Cout, R, stride, pad):
     return lib.mauv_conv2d_bwd_data_stat_blocks(G, B, H, W, Cin, Cout, R, R, stride, pad)
 
 
-def set_dma16(on):
-    """Select the LDS-DMA 16-bit conv kernels (True, default) or the pipelined register-staged
-    ones (False), process-wide; returns the previous setting."""
-    return bool(lib.mauv_set_dma16(int(bool(on))))
+def set_dma16(mode):
+    """Select the 16-bit conv kernels, process-wide: 1 (True, default) = the LDS-DMA kernels for
+    the shapes they take, 2 = also the forwards with a pending BN on x, 0 (False) = the
+    pipelined register-staged kernels; returns the previous setting."""
+    return int(lib.mauv_set_dma16(int(mode)))
 
 
 def weights_rsck(w, G, Cout, RS, Cin, out):

@@ -112,16 +112,21 @@ def cosines(params, truth_params):
     return out
 
 
-def center_head(mean_logits, *models, gain=1.0):
-    """Make a random-init model's argmax depend on its input (tests of class agreement): at
-    random init every item's logits sit near one bias-dominated point (every golden class is
-    4), so the last layer's mean bias is shifted by the batch's mean logits ``mean_logits``
-    [C] and the layer scaled by ``gain`` — identically in every model given."""
-    with torch.no_grad():
-        for m in models:
-            m.fc2.mu_bias.sub_(mean_logits.to(m.fc2.mu_bias.device))
-            m.fc2.mu_bias.mul_(gain)
-            m.fc2.mu_weight.mul_(gain)
+def fit_model(m, x, b, s, labels, steps=20, lr=1e-3, num_mc=2):
+    """A few FusedAdam MC training steps (fp32) of a mauv model on one batch so that its
+    predicted class depends on the input (tests of class agreement): at random init the
+    per-item logits differ by ~3e-4 — less than the MC noise — and every item gets one class
+    (every golden row is class 4).  Returns the cross-entropy of the last step."""
+    from mauv.optim import FusedAdam
+    from mauv.train import mc_train_step
+    opt = FusedAdam(m.parameters(), lr=lr)
+    crit = torch.nn.CrossEntropyLoss()
+    ce = None
+    for _ in range(steps):
+        r = mc_train_step(m, (x, b, s), labels, crit, opt, num_mc, labels.numel(), 1e-6)
+        ce = float(r["ce"])
+    opt.zero_grad(set_to_none=True)
+    return ce
 
 
 def grad_error_profile(hip_params, cpu_params, truth_params):

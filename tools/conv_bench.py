@@ -70,10 +70,10 @@ def main():
                          "statistics partials from the fwd epilogue")
     ap.add_argument("--dma", type=int, default=1,
                     help="16-bit: LDS-DMA kernels (conv_dma16.hip) for the shapes they take "
-                         "(forward without pending BN, data gradient over RSCK weights); 0 = "
-                         "the pipelined register-staged kernels")
+                         "(forward without pending BN, data gradient over RSCK weights); 2 = "
+                         "also the forwards with a pending BN; 0 = the pipelined kernels")
     a = ap.parse_args()
-    ops.set_dma16(bool(a.dma))
+    ops.set_dma16(a.dma)
     global REPS
     REPS = a.reps
     G, B, dev = a.G, a.B, "cuda"
