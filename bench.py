@@ -290,6 +290,9 @@ def main():
                     help="triplets per GPU of the configs[4] training legs (256 over 8 GPUs)")
     ap.add_argument("--infer-sweep-batch", type=int, default=256)
     ap.add_argument("--infer-sweep-mc", type=int, default=100)
+    ap.add_argument("--grad-exchange", default="fp32", choices=["fp32", "bf16"],
+                    help="world > 1: gradient all-reduce in fp32 (587 MB per step) or as a bf16 "
+                         "copy of the arena (294 MB, mauv.ddp.DistributedMC grad_dtype)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for world > 1 (nccl = RCCL over xGMI; gloo "
                          "rehearses the multi-rank harness, e.g. two ranks on one GPU)")
@@ -316,7 +319,8 @@ def main():
     model = define_models(None, 7, DEFAULT_PRIOR)["multimodal_model"].to(dev)
     if world > 1:
         from mauv.ddp import DistributedMC
-        model = DistributedMC(model)
+        model = DistributedMC(model, grad_dtype=torch.bfloat16 if args.grad_exchange == "bf16"
+                              else torch.float32)
     from mauv.optim import FusedAdam   # what mauv.loop_utils builds for GPU models
     opt = FusedAdam(model.parameters(), lr=5e-5)
     crit = torch.nn.CrossEntropyLoss()
@@ -552,7 +556,8 @@ def main():
                                    f"B={args.batch}/GPU {args.dtype}, num_mc={args.num_mc}, optical "
                                    f"{args.optical}px + bathy/SSS {args.sonar}px",
                        "global_batch": args.batch * world, "num_mc": args.num_mc,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       "grad_exchange": args.grad_exchange if world > 1 else None},
             "f32_math": f32_math if args.dtype == "fp32" else None,
             "fp32_exact_mfma": exact,
             "inference": infer, "infer_sweep": infer_sweep, "bf16_train": bf16,

@@ -193,3 +193,42 @@ def test_nan_loss_on_one_rank_skips_on_all(tmp_path):
         assert skipped and same and stepped
     for a, b in zip(res[0][3], res[1][3]):
         assert torch.equal(a, b)
+
+
+def _bf16_worker(rank, world, port, q):
+    """grad_dtype=bf16: the exchange moves bf16 (half the bytes of the fp32 arena); the
+    averaged fp32 gradients equal the fp32 exchange's within bf16 rounding of each rank's
+    contribution, on every rank bit-identically."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "multimodal-auv_amd")]
+    _init(rank, world, port)
+    from mauv.ddp import DistributedMC
+    from mauv.engine import root_state
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(50, 70), torch.nn.Linear(70, 30))
+    ddp = DistributedMC(net, bucket_bytes=1000, grad_dtype=torch.bfloat16)
+    assert ddp.bucket_elems == 500      # bf16 buckets hold twice the values of fp32 ones
+    st = root_state(net)
+    st.grads(torch.device("cpu"))
+    g = torch.Generator().manual_seed(10 + rank)
+    local = [torch.randn(p.shape, generator=g) * (rank + 1) for p in net.parameters()]
+    for p, v in zip(net.parameters(), local):
+        p.grad.copy_(v)
+    ddp.allreduce_grads()
+    torch.save(([p.grad.clone() for p in net.parameters()], local, ddp._lp.dtype),
+               os.path.join(q, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_bf16_gradient_exchange(tmp_path):
+    res = _run(_bf16_worker, tmp_path)
+    (g0, l0, dt0), (g1, l1, _) = res
+    assert dt0 == torch.bfloat16
+    for a, b, x, y in zip(g0, g1, l0, l1):
+        assert torch.equal(a, b)                       # every rank holds the same average
+        exact = (x + y) / 2
+        # each contribution rounded to bf16 (2^-9 relative), the sum rounded once more
+        tol = (x.abs() + y.abs()) * 2.0 ** -8 / 2 + exact.abs() * 2.0 ** -8
+        assert ((a - exact).abs() <= tol + 1e-12).all()
+        assert not torch.equal(a, exact)               # it really went through bf16
