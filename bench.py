@@ -113,14 +113,29 @@ def cpu_baseline(args):
     from oracle.model_ref import define_models, DEFAULT_PRIOR
     from oracle import loops_ref
     host = _host_cpu()
-    # torch.set_num_threads(<physical cores>): the physical cores of the CPUs
-    # this process may run on, whatever OMP_NUM_THREADS the box exports
-    threads = max(1, host["usable_physical_cores"])
     prev_threads = torch.get_num_threads()
-    torch.set_num_threads(threads)
     torch.manual_seed(0)
     models = define_models(None, 7, DEFAULT_PRIOR)
     model = models["multimodal_model"]
+    # torch.set_num_threads(<physical cores>).  On a shared GPU box every
+    # physical core is not this job's (OMP_NUM_THREADS is the box's per-GPU share), and
+    # oversubscribed threads run the oracle ~13x slower (round 3: 0.042 triplets/s at 128
+    # threads vs 0.56 at 16) — so the thread count is CALIBRATED: one trunk forward timed at
+    # the box's share, 2x, 4x and the physical cores of the affinity set; the fastest is used
+    # and every candidate is reported.
+    xc, _, _, _ = synthetic_batch(2, args.optical, args.sonar, "cpu", 5)
+    cands = sorted({max(1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)) * k
+                    for k in (1, 2, 4)} | {max(1, host["usable_physical_cores"])})
+    calib = {}
+    with torch.no_grad():
+        for n in cands:
+            torch.set_num_threads(n)
+            model.image_model_feat(xc)                   # warm-up at this thread count
+            t0 = time.perf_counter()
+            model.image_model_feat(xc)
+            calib[n] = round(time.perf_counter() - t0, 4)
+    threads = min(calib, key=calib.get)
+    torch.set_num_threads(threads)
     opt = torch.optim.Adam(model.parameters(), lr=5e-5)
     crit = torch.nn.CrossEntropyLoss()
     Bc, Nc = 2, 2
@@ -138,6 +153,7 @@ def cpu_baseline(args):
                      f"num_mc={args.num_mc}), {args.optical}/{args.sonar} px, torch-CPU fp32, "
                      f"{reps} timed steps of {dt:.2f} s"}
     out.update(host)
+    out["threads_calibration_s"] = {str(k): v for k, v in calib.items()}
     # configs[0]: the unimodal CPU path, timed in full
     uni = models["image_model"]
     uopt = torch.optim.Adam(uni.parameters(), lr=5e-5)

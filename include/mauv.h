@@ -105,21 +105,6 @@ int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, void* dx,
                              const void* addend, int accumulate, int G, int B, int H, int W,
                              int Cin, int Cout, int R, int S, int stride, int pad,
                              hipStream_t stream);
-/* the same data gradient with w_rsck (nullable) = the weights transposed to
- * [G][R][S][Cin][Cout] by mauv_weights_rsck_h16: both GEMM operands are then k-contiguous rows
- * and the LDS-DMA kernel (conv_dma16.hip) runs the shapes it covers (Cout % 64 == 0, >= 128
- * rows and input channels); others take the pipelined kernel over w. */
-int mauv_conv2d_bwd_data_h16_t(int dtype, const void* dy, const void* w, const void* w_rsck,
-                               void* dx, const void* addend, int accumulate, int G, int B, int H,
-                               int W, int Cin, int Cout, int R, int S, int stride, int pad,
-                               hipStream_t stream);
-/* 1 (default, env MAUV_DMA16) = the LDS-DMA kernels run the 16-bit convs they cover, 2 = also
- * the forwards with a pending BN on x (register-staged A, DMA B), 0 = the pipelined
- * register-staged kernels; -1 queries.  Returns the previous setting. */
-int mauv_set_dma16(int on);
-/* 16-bit KRSC [G][Cout][RS][Cin] -> RSCK [G][RS][Cin][Cout] (Cout, Cin % 8 == 0). */
-int mauv_weights_rsck_h16(const void* w, void* w_rsck, int G, int Cout, int RS, int Cin,
-                          hipStream_t stream);
 int mauv_conv2d_bwd_weight_h16(int dtype, const void* x, const long long* x_strides,
                                const float* x_scale, const float* x_shift, int x_relu,
                                const void* dy, float* ws, int splits, int G, int B, int H, int W,
@@ -152,6 +137,15 @@ int mauv_reparam_sample_h16(int dtype, const float* mu, const float* rho, const 
                             unsigned long long seed, unsigned long long sample0,
                             unsigned int layer, int G, int Cout, int Cin, int RS, int cin_pad,
                             void* out, long long out_gstride, hipStream_t stream);
+/* The three sampling forms in one entry (dtype -1 = fp32, 0 = bf16, 1 = f16; KRSC with cin_pad
+ * >= Cin channels, pad untouched) whose MC sample index is sample0 + *sample_base + g when
+ * sample_base (nullable device counter) is given: a HIP graph captured around a forward
+ * replays with fresh samples after the caller updates the counter. */
+int mauv_reparam_sample_ex(int dtype, const float* mu, const float* rho, const float* eps,
+                           unsigned long long seed, unsigned long long sample0,
+                           const unsigned long long* sample_base, unsigned int layer, int G,
+                           int Cout, int Cin, int RS, int cin_pad, void* out,
+                           long long out_gstride, hipStream_t stream);
 /* fp32 counterpart of mauv_reparam_sample_h16's padded layout (the fp32 stems' 4-channel KRSC
  * weights); same sampling as mauv_reparam_sample, pad channels not written. */
 int mauv_reparam_sample_padded(const float* mu, const float* rho, const float* eps,

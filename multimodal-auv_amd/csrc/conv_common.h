@@ -148,9 +148,6 @@ bool conv_split_launch(int mode, const ConvArgs& a, int oneacc, hipStream_t st);
 // pipelined 16-bit kernels (conv_pipe16.hip); x/w/dy/out/addend hold 16-bit data of type dt
 // (DT_BF16 / DT_F16), WGRAD out stays fp32 slabs; false: shape not covered
 bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
-// LDS-DMA 16-bit kernels (conv_dma16.hip): FWD without a pending BN, DGRAD with a.w = the
-// RSCK-transposed weights; false: shape not covered (the caller takes conv_pipe16.hip)
-bool conv_dma16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
 
 __device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int relu) {
   v = v * sc + sh;

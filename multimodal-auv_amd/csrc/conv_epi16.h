@@ -1,4 +1,4 @@
-// Epilogue of the 16-bit implicit-GEMM convs (conv_pipe16.hip, conv_dma16.hip) for FWD and
+// Epilogue of the 16-bit implicit-GEMM convs (conv_pipe16.hip) for FWD and
 // DGRAD: BN statistics partials of y from the fp32 accumulators (tile mean, then M2 around it;
 // FWD with st_mean), then the 16-bit output through LDS as 16-byte row chunks (DGRAD: residual
 // addend / previous dx added in fp32, one rounding; parity-class row remap).  acc[MI][NI] are

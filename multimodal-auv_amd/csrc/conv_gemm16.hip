@@ -544,8 +544,7 @@ MAUV_API int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_st
   a.out_sg = (long long)a.M * a.N;
   a.st_mean = st_mean; a.st_m2 = st_m2; a.st_cnt = st_cnt;
   a.st_nblk = ceil_div(a.M, conv_tile_rows(a.M));
-  if (conv_dma16_launch(FWD, dtype, pipe_args(a), stream)) {}
-  else if (conv_pipe16_launch(FWD, dtype, pipe_args(a), stream)) {}
+  if (conv_pipe16_launch(FWD, dtype, pipe_args(a), stream)) {}
   else if (Cin % HBK == 0) dispatch16<H_FWD, true>(dtype, a, stream);
   else dispatch16<H_FWD, false>(dtype, a, stream);
   return check_launch("conv2d_fwd_h16");
@@ -589,17 +588,7 @@ MAUV_API int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, 
                                       const void* addend, int accumulate, int G, int B, int H,
                                       int W, int Cin, int Cout, int R, int S, int stride, int pad,
                                       hipStream_t stream) {
-  return mauv_conv2d_bwd_data_h16_t(dtype, dy, w, nullptr, dx, addend, accumulate, G, B, H, W,
-                                    Cin, Cout, R, S, stride, pad, stream);
-}
-
-MAUV_API int mauv_conv2d_bwd_data_h16_t(int dtype, const void* dy, const void* w,
-                                        const void* w_rsck, void* dx, const void* addend,
-                                        int accumulate, int G, int B, int H, int W, int Cin,
-                                        int Cout, int R, int S, int stride, int pad,
-                                        hipStream_t stream) {
   if (int e = check_shape16("conv2d_bwd_data_h16", dtype, G, B, Cin, Cout, nullptr)) return e;
-  if (w_rsck && !aligned16(w_rsck)) { set_error("conv2d_bwd_data_h16: w_rsck must be 16-B aligned"); return kErrArg; }
   if (Cout % HBK) { set_error("conv2d_bwd_data_h16: needs Cout % 32 == 0"); return kErrArg; }
   ConvArgs16 a = make_args16(G, B, H, W, Cin, Cout, R, S, stride, pad, nullptr);
   a.dy = (const u16*)dy; a.w = (const u16*)w; a.out = dx;
@@ -620,11 +609,6 @@ MAUV_API int mauv_conv2d_bwd_data_h16_t(int dtype, const void* dy, const void* w
       if (a.M <= 0) continue;
       // a tapless class accumulating into dx adds nothing (stride-2 1x1 downsample: 3 of 4)
       if (a.K == 0 && accumulate && !addend) continue;
-      if (w_rsck) {   // LDS-DMA kernel over the transposed weights (conv_dma16.hip)
-        ConvArgs d = pipe_args(a);
-        d.w = (const float*)w_rsck;
-        if (conv_dma16_launch(DGRAD, dtype, d, stream)) continue;
-      }
       if (!conv_pipe16_launch(DGRAD, dtype, pipe_args(a), stream))
         dispatch16<H_DGRAD, true>(dtype, a, stream);
     }
@@ -649,45 +633,3 @@ MAUV_API int mauv_conv2d_bwd_weight_h16(int dtype, const void* x, const long lon
   return check_launch("conv2d_bwd_weight_h16");
 }
 
-// KRSC [G][Cout][R*S][Cin] -> RSCK [G][R*S][Cin][Cout] (16-bit): the data gradient's B operand
-// as k-contiguous rows for the LDS-DMA kernel.  64 x 64 (cout x cin) tiles through LDS, 16-byte
-// loads and stores.
-namespace mauv {
-__global__ __launch_bounds__(256) void rsck_kernel(const u16* __restrict__ w, u16* __restrict__ wt,
-                                                  int Cout, int RS, int Cin) {
-  __shared__ __attribute__((aligned(16))) u16 tile[64][64 + 8];
-  const int g_rs = blockIdx.z, rs = g_rs % RS, g = g_rs / RS;
-  const int co0 = blockIdx.y * 64, ci0 = blockIdx.x * 64;
-  const long long wg = (long long)g * Cout * RS * Cin;
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {   // 64 rows (cout) x 8 chunks of 8 cin
-    const int idx = t + 256 * j, r = idx >> 3, c = (idx & 7) * 8;
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (co0 + r < Cout && ci0 + c < Cin)
-      v = *(const u32x4*)(w + wg + ((long long)(co0 + r) * RS + rs) * Cin + ci0 + c);
-    const u16* e = (const u16*)&v;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) tile[c + q][r] = e[q];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {   // 64 rows (cin) x 8 chunks of 8 cout
-    const int idx = t + 256 * j, r = idx >> 3, c = (idx & 7) * 8;
-    if (ci0 + r < Cin && co0 + c < Cout)
-      *(u32x4*)(wt + wg + ((long long)rs * Cin + ci0 + r) * Cout + co0 + c) = *(const u32x4*)&tile[r][c];
-  }
-}
-}  // namespace mauv
-
-MAUV_API int mauv_weights_rsck_h16(const void* w, void* w_rsck, int G, int Cout, int RS, int Cin,
-                                   hipStream_t stream) {
-  if (G <= 0 || Cout <= 0 || RS <= 0 || Cin <= 0 || Cout % 8 || Cin % 8 || !w || !w_rsck ||
-      !aligned16(w) || !aligned16(w_rsck)) {
-    set_error("weights_rsck_h16: bad shape (Cout, Cin % 8 == 0, 16-B aligned pointers)");
-    return kErrArg;
-  }
-  hipLaunchKernelGGL(rsck_kernel, dim3(ceil_div(Cin, 64), ceil_div(Cout, 64), G * RS), dim3(256),
-                     0, stream, (const u16*)w, (u16*)w_rsck, Cout, RS, Cin);
-  return check_launch("weights_rsck_h16");
-}

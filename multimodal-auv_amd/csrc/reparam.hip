@@ -23,7 +23,11 @@ template <class S>
 __global__ __launch_bounds__(256) void reparam_sample_kernel(
     const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
     uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS, int cin_pad,
-    typename S::T* __restrict__ out, long long out_gs) {
+    typename S::T* __restrict__ out, long long out_gs,
+    const unsigned long long* __restrict__ base = nullptr) {
+  // base (nullable): a device counter added to sample0 — a captured HIP graph replays the
+  // same launch with fresh MC samples by updating it (mauv_reparam_sample_ex)
+  if (base) sample0 += *base;
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
   for (long long q = blockIdx.x * 256LL + threadIdx.x; q < nq; q += (long long)gridDim.x * 256) {
@@ -274,6 +278,33 @@ MAUV_API int mauv_reparam_sample_h16(int dtype, const float* mu, const float* rh
   MAUV_DT_DISPATCH(dtype, "reparam_sample_h16", L)
 #undef L
   return check_launch("reparam_sample_h16");
+}
+
+// All three sampling forms in one entry (dtype -1 = fp32, 0 = bf16, 1 = f16; cin_pad >= Cin,
+// pad channels untouched) with the MC sample index sample0 + *sample_base + g when sample_base
+// (a device counter) is given: a captured HIP graph of a forward replays with fresh samples.
+MAUV_API int mauv_reparam_sample_ex(int dtype, const float* mu, const float* rho,
+                                    const float* eps, unsigned long long seed,
+                                    unsigned long long sample0,
+                                    const unsigned long long* sample_base, unsigned int layer,
+                                    int G, int Cout, int Cin, int RS, int cin_pad, void* out,
+                                    long long out_gstride, hipStream_t stream) {
+  if (cin_pad < Cin) { set_error("reparam_sample_ex: cin_pad < Cin"); return kErrArg; }
+  const long long numel = (long long)Cout * Cin * RS;
+  const long long nq = (numel + 3) / 4;
+  const long long gs = out_gstride ? out_gstride : (long long)Cout * RS * cin_pad;
+  if (dtype < 0) {
+    hipLaunchKernelGGL(reparam_sample_kernel<SF32>, sample_grid(nq, G), dim3(256), 0, stream, mu,
+                       rho, eps, seed, sample0, layer, G, Cout, Cin, RS, cin_pad, (float*)out, gs,
+                       sample_base);
+    return check_launch("reparam_sample_ex");
+  }
+#define L(D) hipLaunchKernelGGL(reparam_sample_kernel<S16<D>>, sample_grid(nq, G), dim3(256), 0, \
+                                stream, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS,   \
+                                cin_pad, (u16*)out, gs, sample_base);
+  MAUV_DT_DISPATCH(dtype, "reparam_sample_ex", L)
+#undef L
+  return check_launch("reparam_sample_ex");
 }
 
 // dmu += sum_g sum_s dw[s][g];  drho += sum_g (sum_s dw[s][g]) * eps_g' * sigmoid(rho), where

@@ -41,8 +41,6 @@ BN_RELU_MASK = os.environ.get("MAUV_BN_RELU_MASK", "1") == "1"
 # The stems as ONE GEMM over im2col rows shared by the G samples, the G weight sets stacked
 # along N (stem.hip), instead of G implicit GEMMs over channel-padded pixels.
 STEM_GEMM = os.environ.get("MAUV_STEM_GEMM", "1") == "1"
-# 16-bit data gradients on the LDS-DMA kernel over RSCK-transposed weights (conv_dma16.hip)
-DMA_DGRAD = os.environ.get("MAUV_DMA_DGRAD", "1") == "1"
 _STREAMS = {}
 
 
@@ -117,6 +115,9 @@ class RootState:
         self.grad_ready_hook = None
         self.kl_bwd_count = 0
         self.kl_bwd_event = None   # recorded after the last KL backward (mauv.kl)
+        # device int64 [1] added to every sampled MC index while a forward is being captured
+        # into a HIP graph (mauv.predict): the replay draws fresh samples after it is updated
+        self.sample_base = None
 
     def trunk_dtype(self):
         if self.precision is not None:
@@ -210,6 +211,12 @@ class _Runner:
     # ---- Bayesian parameter sampling (mauv_reparam_sample) ----
     def _sample(self, m, mu, rho, name, out, Cout, Cin, RS, bias=False, out_gstride=0,
                 cin_pad=None):
+        if self.st.sample_base is not None:   # inside a captured inference graph (predict.py)
+            ops.reparam_sample_ex(mu, rho, out, self.G, self.st.seed, self.s0,
+                                  self.st.sample_base, self.st.layer_id(m, bias), Cout, Cin, RS,
+                                  eps=self._eps(m, name), out_gstride=out_gstride,
+                                  cin_pad=cin_pad)
+            return
         ops.reparam_sample(mu, rho, out, self.G, self.st.seed, self.s0,
                            self.st.layer_id(m, bias), Cout, Cin, RS, eps=self._eps(m, name),
                            out_gstride=out_gstride, cin_pad=cin_pad)
@@ -404,13 +411,8 @@ class TrunkRunner(_Runner):
             return None
         if dx is None:
             dx = torch.empty(G, B, H, W, Cin, device=dy.device, dtype=self.dt)
-        wt = None
-        if DMA_DGRAD and self.dt != torch.float32 and Cout % 64 == 0 and Cin >= 128 and cp == Cin:
-            # the LDS-DMA data gradient reads the weights as [R][S][Cin][Cout] rows
-            wt = torch.empty(G, k * k, Cin, Cout, device=dy.device, dtype=self.dt)
-            ops.weights_rsck(w, G, Cout, k * k, Cin, wt)
         ops.conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, k, st, pd, addend=addend,
-                            accumulate=accumulate, w_rsck=wt)
+                            accumulate=accumulate)
         return dx
 
     def _stem(self, conv, x, B, H, W):

@@ -145,25 +145,10 @@ def dgrad_stat_blocks(G, B, H, W, Cin, Cout, R, stride, pad):
     return lib.mauv_conv2d_bwd_data_stat_blocks(G, B, H, W, Cin, Cout, R, R, stride, pad)
 
 
-def set_dma16(mode):
-    """Select the 16-bit conv kernels, process-wide: 1 (True, default) = the LDS-DMA kernels for
-    the shapes they take, 2 = also the forwards with a pending BN on x, 0 (False) = the
-    pipelined register-staged kernels; returns the previous setting."""
-    return int(lib.mauv_set_dma16(int(mode)))
-
-
-def weights_rsck(w, G, Cout, RS, Cin, out):
-    """16-bit KRSC [G][Cout][RS][Cin] -> RSCK [G][RS][Cin][Cout] (the LDS-DMA data gradient's
-    B operand)."""
-    _h16(w.dtype, w, out)
-    check(lib.mauv_weights_rsck_h16(_p(w), _p(out), G, Cout, RS, Cin, stream()), "weights_rsck_h16")
-
-
 def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=None,
-                    accumulate=False, bn=None, w_rsck=None):
+                    accumulate=False, bn=None):
     """bn = dict(y, out|None, scale, shift, mean, invstd, relu, p1, p2): dx is the output
-    gradient of that BatchNorm; the epilogue writes its backward partial sums into p1/p2.
-    w_rsck (16-bit only): the weights transposed by weights_rsck (LDS-DMA kernel)."""
+    gradient of that BatchNorm; the epilogue writes its backward partial sums into p1/p2."""
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
     b = bn or {}
     fl = 2.0 * G * B * Ho * Wo * Cout * R * R * Cin
@@ -174,12 +159,10 @@ def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=Non
     if w.dtype in H16:
         assert bn is None, "16-bit dgrad has no BN-partials epilogue"
         _h16(w.dtype, dy, w, dx, addend)
-        _h16(w.dtype, w_rsck)
         with _Prof("dgrad_" + str(w.dtype)[6:], fl, nb, nl):
-            check(lib.mauv_conv2d_bwd_data_h16_t(H16[w.dtype], _p(dy), _p(w), _p(w_rsck), _p(dx),
-                                                 _p(addend), int(accumulate), G, B, H, W, Cin,
-                                                 Cout, R, R, stride, pad, stream()),
-                  "conv2d_bwd_data_h16")
+            check(lib.mauv_conv2d_bwd_data_h16(H16[w.dtype], _p(dy), _p(w), _p(dx), _p(addend),
+                                               int(accumulate), G, B, H, W, Cin, Cout, R, R,
+                                               stride, pad, stream()), "conv2d_bwd_data_h16")
         return
     _f32(dy, w, dx, addend)
     with _Prof("dgrad", fl, nb, nl):
@@ -239,6 +222,18 @@ def reparam_sample(mu, rho, out, G, seed, sample0, layer, Cout, Cin, RS, eps=Non
         return
     check(lib.mauv_reparam_sample(_p(mu), _p(rho), _p(eps), seed, sample0, layer, G, Cout, Cin,
                                   RS, _p(out), out_gstride, stream()), "reparam_sample")
+
+
+def reparam_sample_ex(mu, rho, out, G, seed, sample0, sample_base, layer, Cout, Cin, RS, eps=None,
+                      out_gstride=0, cin_pad=None):
+    """reparam_sample with the MC sample index sample0 + sample_base[0] + g read on the device
+    (sample_base: int64 [1] device tensor) — what a replayed HIP graph of a forward uses."""
+    _f32(mu, rho, eps)
+    _dev(torch.int64, sample_base)
+    code = -1 if out.dtype == torch.float32 else H16[out.dtype]
+    check(lib.mauv_reparam_sample_ex(code, _p(mu), _p(rho), _p(eps), seed, sample0,
+                                     _p(sample_base), layer, G, Cout, Cin, RS, cin_pad or Cin,
+                                     _p(out), out_gstride, stream()), "reparam_sample_ex")
 
 
 def reparam_bwd(dw, splits, mu, rho, dmu, drho, G, seed, sample0, layer, Cout, Cin, RS,

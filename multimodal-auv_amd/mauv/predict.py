@@ -16,6 +16,7 @@ and every reduction stay fp32/fp64.
 import csv
 import logging
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -63,6 +64,77 @@ def _param_device(core):
     return None
 
 
+# Small MC chunks (the reference's own call shape: batch_size_unimodal=8, num_mc=12,
+# main.py:261-271,310,315) are launch-bound: ~1,000 C-ABI launches per tri-modal forward from
+# Python.  Their forward is captured once per shape into a HIP graph and replayed; the MC
+# samples stay fresh on every replay because the sampling kernels read their sample index from
+# a device counter (mauv_reparam_sample_ex).  MAUV_GRAPH_INFER=0 turns it off; chunks above
+# the activation budget below always run eagerly (a graph's pool keeps its activations).
+GRAPH_INFER = os.environ.get("MAUV_GRAPH_INFER", "1") == "1"
+_GRAPH_MAX_BYTES = 6 << 30
+
+
+class _GraphedChunk:
+    """One captured MC-chunk forward: static inputs in, static [G, B, C] logits out."""
+
+    def __init__(self, core, inputs, G):
+        st = root_state(core)
+        dev = inputs[0].device
+        self.core, self.G = core, G
+        self.static = [t.clone() for t in inputs]
+        self.base = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.graph = torch.cuda.CUDAGraph()
+        saved = st.offset
+        st.sample_base, st.offset = self.base, 0      # captured with sample0 = 0 + *base
+        try:
+            with torch.cuda.graph(self.graph):
+                self.out = core.mc_forward(*self.static, G)
+        finally:
+            st.sample_base, st.offset = None, saved
+
+    def __call__(self, inputs):
+        st = root_state(self.core)
+        for d, x in zip(self.static, inputs):
+            d.copy_(x)
+        self.base.fill_(st.next_samples(self.G))       # this chunk's MC sample indices
+        self.graph.replay()
+        return self.out
+
+
+def _chunk_forward(core, inputs, G):
+    """core.mc_forward(*inputs, G), through a captured HIP graph for small chunks once a shape
+    has run eagerly (the first run also loads every kernel the capture records)."""
+    if not GRAPH_INFER or torch.is_grad_enabled() or not inputs[0].is_cuda:
+        return core.mc_forward(*inputs, G)
+    base = unwrap(core)
+    st = root_state(base)
+    if st.eps_provider is not None:                    # tests feed explicit epsilons: eager
+        return base.mc_forward(*inputs, G)
+    dt = st.trunk_dtype()
+    B = inputs[0].shape[0]
+    per = mc_chunk_bytes(B, dt, [t.shape[-2:] for t in inputs])
+    if per * G > _GRAPH_MAX_BYTES:
+        return base.mc_forward(*inputs, G)
+    key = (tuple(tuple(t.shape) for t in inputs), tuple(t.dtype for t in inputs), G, dt,
+           inputs[0].device)
+    cache = base.__dict__.setdefault("_mauv_graphs", {})
+    g = cache.get(key)
+    if g is None:
+        if key in base.__dict__.setdefault("_mauv_graph_seen", set()):
+            g = cache[key] = _GraphedChunk(base, inputs, G)
+        else:
+            base.__dict__["_mauv_graph_seen"].add(key)
+            return base.mc_forward(*inputs, G)
+    return g(inputs)
+
+
+def mc_chunk_bytes(batch_size, dtype, hw):
+    """Estimated peak activation bytes of one MC sample of one inference forward."""
+    esize = torch.tensor([], dtype=dtype or torch.float32).element_size()
+    grid = max(math.ceil(h / 4) * math.ceil(w / 4) for h, w in hw)
+    return esize * _PEAK_CH_L1 * grid * batch_size * _ALLOC_SLACK
+
+
 def local_mc_count(num_mc, rank, world):
     """MC samples this rank draws when ``num_mc`` are sharded over ``world`` ranks."""
     return num_mc // world + (1 if rank < num_mc % world else 0)
@@ -86,7 +158,7 @@ def mc_statistics(model, inputs, bathy, sss, num_mc, eps_h=1e-7, eps_pred=1e-8, 
     done = 0
     while done < local:
         g = min(chunk, local - done)
-        logits = core.mc_forward(inputs, bathy, sss, g)
+        logits = _chunk_forward(core, (inputs, bathy, sss), g)
         sums = mchead.mc_stats(logits, eps_h, sums)
         done += g
         del logits

@@ -263,90 +263,3 @@ def test_reparam16_padded_sample_and_bwd(dt):
                     Cin, RS)
     assert torch.equal(dmu_a, dmu_b) and torch.equal(drho_a, drho_b)
 
-
-DMA_CASES = [
-    # G, B, H, Cin, Cout, R, stride, pad — shapes the LDS-DMA kernels take (>= 128 rows and
-    # output channels; FWD Cin % 64, DGRAD Cout % 64): ragged m / n tiles, padding, stride 2
-    (2, 4, 12, 128, 128, 3, 1, 1),
-    (1, 2, 15, 128, 256, 3, 2, 1),
-    (2, 2, 14, 256, 512, 1, 2, 0),
-    (2, 3, 9, 256, 128, 1, 1, 0),
-    (1, 2, 7, 512, 2048, 1, 1, 0),
-    (2, 2, 8, 192, 320, 3, 1, 1),
-]
-
-
-@pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
-@pytest.mark.parametrize("case", DMA_CASES)
-def test_conv16_dma_bit_identical_to_pipelined(case, dt):
-    """conv_dma16.hip (LDS-DMA, 64 x 64 wave tiles, swizzled row images) accumulates every
-    output element in the same k order as conv_pipe16.hip: forward outputs and data gradients
-    (over the RSCK-transposed weights) are bit-identical, the BN statistics partials equal to
-    summation order, all within the float64 bar of test_conv16_fwd_dgrad_wgrad."""
-    from mauv import ops
-    G, B, H, Cin, Cout, R, st, pad = case
-    torch.manual_seed(1)
-    x = torch.randn(G, B, H, H, Cin).to(dt).to(dev)
-    w = (torch.randn(G, Cout, R, R, Cin) / math.sqrt(Cin * R * R)).to(dt).to(dev)
-    Ho = ops.out_hw(H, R, st, pad)
-    M = B * Ho * Ho
-    nblk = ops.fwd_stat_blocks(G, B, H, H, Cin, Cout, R, st, pad)
-    outs = []
-    for on in (True, False):
-        prev = ops.set_dma16(on)
-        try:
-            y = torch.empty(G, B, Ho, Ho, Cout, device=dev, dtype=dt)
-            part = torch.full((2 * G * nblk * Cout + G * nblk,), float("nan"), device=dev)
-            ops.conv2d_fwd(x, w, y, G, B, H, H, Cin, Cout, R, st, pad,
-                           stats=(part[:G * nblk * Cout], part[G * nblk * Cout:2 * G * nblk * Cout],
-                                  part[2 * G * nblk * Cout:]))
-            outs.append((y, part))
-        finally:
-            ops.set_dma16(prev)
-    assert torch.equal(outs[0][0], outs[1][0])
-    # statistics partials: per-tile sums over 2 (DMA) vs 4 (pipelined) wave rows — order only
-    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-6)
-    close(outs[0][0], ref_conv(x.cpu(), w.cpu(), st, pad), 2 * ULP[dt])
-    # data gradient: pipelined over w vs LDS-DMA over the transposed weights
-    wt = torch.empty(G, R * R, Cin, Cout, device=dev, dtype=dt)
-    ops.weights_rsck(w, G, Cout, R * R, Cin, wt)
-    assert torch.equal(wt.cpu(), w.cpu().permute(0, 2, 3, 4, 1).reshape(G, R * R, Cin, Cout))
-    dy = torch.randn(G, B, Ho, Ho, Cout).to(dt).to(dev)
-    addend = torch.randn(G, B, H, H, Cin).to(dt).to(dev)
-    dxs = []
-    for wr in (None, wt):
-        dx = torch.empty(G, B, H, H, Cin, device=dev, dtype=dt)
-        ops.conv2d_bwd_data(dy, w, dx, G, B, H, H, Cin, Cout, R, st, pad, addend=addend, w_rsck=wr)
-        dxs.append(dx)
-    assert torch.equal(dxs[0], dxs[1])
-
-
-@pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
-@pytest.mark.parametrize("case", DMA_CASES[:4] + DMA_CASES[5:])
-@pytest.mark.parametrize("relu", [1, 0])
-def test_conv16_dma_pending_bn_bit_identical(case, dt, relu):
-    """The forward with the producing layer's pending BN(+ReLU) on x (conv2 / conv3 of a
-    bottleneck): register-staged A with the BN applied, B by LDS-DMA (mauv_set_dma16(2)) —
-    outputs bit-identical to the pipelined kernel, statistics partials to summation order."""
-    from mauv import ops
-    G, B, H, Cin, Cout, R, st, pad = case
-    torch.manual_seed(2)
-    x = torch.randn(G, B, H, H, Cin).to(dt).to(dev)
-    w = (torch.randn(G, Cout, R, R, Cin) / math.sqrt(Cin * R * R)).to(dt).to(dev)
-    xbn = (torch.rand(G, Cin, device=dev) + 0.5, torch.randn(G, Cin, device=dev), relu)
-    Ho = ops.out_hw(H, R, st, pad)
-    nblk = ops.fwd_stat_blocks(G, B, H, H, Cin, Cout, R, st, pad)
-    outs = []
-    for mode in (2, 0):
-        prev = ops.set_dma16(mode)
-        try:
-            y = torch.empty(G, B, Ho, Ho, Cout, device=dev, dtype=dt)
-            part = torch.full((2 * G * nblk * Cout + G * nblk,), float("nan"), device=dev)
-            ops.conv2d_fwd(x, w, y, G, B, H, H, Cin, Cout, R, st, pad, x_bn=xbn,
-                           stats=(part[:G * nblk * Cout], part[G * nblk * Cout:2 * G * nblk * Cout],
-                                  part[2 * G * nblk * Cout:]))
-            outs.append((y, part))
-        finally:
-            ops.set_dma16(prev)
-    assert torch.equal(outs[0][0], outs[1][0])
-    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-6)

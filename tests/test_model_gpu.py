@@ -376,3 +376,38 @@ def test_configs3_full_size_inference_properties():
     # H[p_bar] (eps 1e-8) >= E[H[p]] (eps 1e-7) up to the different log epsilons
     assert (ent - alea >= -1e-4).all()
     assert torch.equal(pred, mp.argmax(1))
+
+
+def test_graphed_small_chunk_inference_equals_eager():
+    """The reference's predictor call shape (main.py:261-271: batch 8, num_mc 12) runs its MC
+    chunk as a replayed HIP graph (mauv.predict._chunk_forward): every replay draws fresh MC
+    samples from the device counter and gives bit-identically the eager statistics of the same
+    samples."""
+    from mauv import predict
+    from mauv.engine import root_state
+    from mauv.predict import mc_statistics
+    _, m = build_pair()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(8, 3, 64, 64, generator=g).cuda()
+    b = torch.rand(8, 3, 64, 64, generator=g).cuda()
+    s = torch.rand(8, 1, 64, 64, generator=g).cuda()
+    st = root_state(m)
+    runs = {}
+    prev = predict.GRAPH_INFER
+    try:
+        for graph in (False, True):
+            predict.GRAPH_INFER = graph
+            m.__dict__.pop("_mauv_graphs", None)
+            m.__dict__.pop("_mauv_graph_seen", None)
+            st.offset = 0
+            with torch.no_grad(), torch.autocast("cuda"):
+                runs[graph] = [{k: v.clone() for k, v in mc_statistics(m, x, b, s, 12).items()}
+                               for _ in range(4)]
+            if graph:
+                assert len(m.__dict__["_mauv_graphs"]) == 1   # captured once, replayed twice
+    finally:
+        predict.GRAPH_INFER = prev
+    for e, gr in zip(runs[False], runs[True]):
+        for k in e:
+            assert torch.equal(e[k], gr[k]), k
+    assert not torch.equal(runs[True][2]["var"], runs[True][3]["var"])   # fresh samples

@@ -68,12 +68,7 @@ def main():
     ap.add_argument("--fused", action="store_true",
                     help="as in the model: BN+ReLU applied on load (fwd, wgrad) and BN "
                          "statistics partials from the fwd epilogue")
-    ap.add_argument("--dma", type=int, default=1,
-                    help="16-bit: LDS-DMA kernels (conv_dma16.hip) for the shapes they take "
-                         "(forward without pending BN, data gradient over RSCK weights); 2 = "
-                         "also the forwards with a pending BN; 0 = the pipelined kernels")
     a = ap.parse_args()
-    ops.set_dma16(a.dma)
     global REPS
     REPS = a.reps
     G, B, dev = a.G, a.B, "cuda"
@@ -107,11 +102,11 @@ def main():
             # (wgrad: its fp32 split-K slabs are written once)
             nx, ny, nw = G * B * H * H * Cin, G * B * Ho * Ho * Cout, G * Cout * R * R * Cin
             sp_ = ops.wgrad_splits(G, B, H, H, Cin, Cout, R, st, pd)
-            byt = {"fwd": esz * (nx + nw + ny), "dgrad": esz * (ny + nw + nx), "rsck": 2 * esz * nw,
+            byt = {"fwd": esz * (nx + nw + ny), "dgrad": esz * (ny + nw + nx),
                    "wgrad": esz * (nx + ny) + 4 * sp_ * nw}
             if key in cache:
                 for kind, ms in cache[key]:
-                    rows.append((trunk, name, kind, key, ms, 0.0 if kind == "rsck" else fl, byt[kind]))
+                    rows.append((trunk, name, kind, key, ms, fl, byt[kind]))
                 continue
             res = []
             if dt != torch.float32 and Cin % 8:
@@ -137,13 +132,9 @@ def main():
                                                                  x_strides=xstr))))
             if "dgrad" in kinds and name != "stem" and (dt == torch.float32 or Cout % 32 == 0):
                 dx = torch.empty_like(x)
-                wt = None
-                if a.dma and dt != torch.float32 and Cout % 64 == 0 and Cin >= 128:
-                    wt = torch.empty(G, R * R, Cin, Cout, device=dev, dtype=dt)
-                    res.append(("rsck", timeit(lambda: ops.weights_rsck(w, G, Cout, R * R, Cin, wt))))
                 mark(trunk, name, "dgrad", key, byt["dgrad"])
-                res.append(("dgrad", timeit(lambda: ops.conv2d_bwd_data(y, w, dx, G, B, H, H, Cin, Cout, R, st, pd, w_rsck=wt))))
-                del dx, wt
+                res.append(("dgrad", timeit(lambda: ops.conv2d_bwd_data(y, w, dx, G, B, H, H, Cin, Cout, R, st, pd))))
+                del dx
             if "wgrad" in kinds:
                 sp = ops.wgrad_splits(G, B, H, H, Cin, Cout, R, st, pd)
                 ws = torch.empty(sp, G, Cout, R * R * Cin, device=dev)
@@ -155,7 +146,7 @@ def main():
             torch.cuda.empty_cache()
             cache[key] = res
             for kind, ms in res:
-                rows.append((trunk, name, kind, key, ms, 0.0 if kind == "rsck" else fl, byt[kind]))
+                rows.append((trunk, name, kind, key, ms, fl, byt[kind]))
     # per-launch roofline time: max(flops / MFMA peak, algorithmic bytes / HBM peak)
     peak = 2.5e15 / 6 if a.dtype == "fp32" else 2.5e15
     tot = defaultdict(lambda: [0.0, 0.0, 0.0])
