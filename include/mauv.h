@@ -105,6 +105,14 @@ int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, void* dx,
                              const void* addend, int accumulate, int G, int B, int H, int W,
                              int Cin, int Cout, int R, int S, int stride, int pad,
                              hipStream_t stream);
+/* Prototype: mauv_conv2d_bwd_data_h16 whose dy is the BatchNorm backward of
+ * (y, dout) computed in the A-loader instead of read materialised: dy = alpha*dz + beta*y +
+ * gamma per channel, dz = dout * [y*sc + sh > 0] when relu, coef = fp32 [5][G][Cout] (alpha,
+ * beta, gamma, sc, sh).  Cout % 64 == 0. */
+int mauv_conv2d_bwd_data_fold_h16(int dtype, const void* dout, const void* y, const float* coef,
+                                  int relu, const void* w, void* dx, const void* addend,
+                                  int accumulate, int G, int B, int H, int W, int Cin, int Cout,
+                                  int R, int S, int stride, int pad, hipStream_t stream);
 int mauv_conv2d_bwd_weight_h16(int dtype, const void* x, const long long* x_strides,
                                const float* x_scale, const float* x_shift, int x_relu,
                                const void* dy, float* ws, int splits, int G, int B, int H, int W,

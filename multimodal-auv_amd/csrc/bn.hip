@@ -745,6 +745,7 @@ static int bn_bwd_impl(const typename S::T* y, const typename S::T* out,
   if (dgamma || dbeta)
     hipLaunchKernelGGL(bn_bwd_param_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C, M,
                        k1, k2, dgamma, dbeta);
+  if (!dy && !dres) return check_launch("bn_bwd");   // partial sums / parameter grads only
   if (mask || use_rows(C)) {
     int anblk, arpb;
     rows_geometry(M, C, anblk, arpb);

@@ -54,6 +54,11 @@ struct ConvArgs {
   int cpg;
   // block order over the whole grid (1, default) or over blockIdx.x only (0): see conv_block_tile
   int xcd_grid;
+  // 16-bit DGRAD with the BN backward folded into the A-loader (conv_pipe16.hip bn_bwd8): dy =
+  // dout (a.dy) of that BN, fy its input y, fcoef [5][G][Cout] = alpha, beta, gamma, sc, sh
+  const void* fy;
+  const float* fcoef;
+  int frelu;
 };
 
 // XCD-aware block -> (tile, group / split-K slice) map.  Blocks are dealt round-robin over the 8

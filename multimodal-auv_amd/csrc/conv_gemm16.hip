@@ -615,6 +615,45 @@ MAUV_API int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, 
   return check_launch("conv2d_bwd_data_h16");
 }
 
+// Prototype: the data gradient whose dy is the BN backward of (y, dout)
+// computed in the A-loader, dy = alpha*dz + beta*y + gamma with dz = dout * [y*sc + sh > 0]
+// (relu) — coef [5][G][Cout] = alpha, beta, gamma, sc, sh — instead of a materialised dy.
+// Pipelined-kernel shapes only (Cout % 64 == 0, Cin % 8 == 0).
+MAUV_API int mauv_conv2d_bwd_data_fold_h16(int dtype, const void* dout, const void* y,
+                                           const float* coef, int relu, const void* w, void* dx,
+                                           const void* addend, int accumulate, int G, int B,
+                                           int H, int W, int Cin, int Cout, int R, int S,
+                                           int stride, int pad, hipStream_t stream) {
+  if (int e = check_shape16("conv2d_bwd_data_fold_h16", dtype, G, B, Cin, Cout, nullptr)) return e;
+  if (Cout % 64 || !y || !coef) { set_error("conv2d_bwd_data_fold_h16: needs Cout % 64 == 0, y, coef"); return kErrArg; }
+  ConvArgs16 a = make_args16(G, B, H, W, Cin, Cout, R, S, stride, pad, nullptr);
+  a.dy = (const u16*)dout; a.w = (const u16*)w; a.out = dx;
+  a.addend = (const u16*)addend; a.accumulate = accumulate;
+  a.N = Cin;
+  a.out_sg = (long long)B * H * W * Cin;
+  for (int ph = 0; ph < stride; ++ph)
+    for (int pw = 0; pw < stride; ++pw) {
+      a.ph = ph; a.pw = pw;
+      a.Hc = (H - ph + stride - 1) / stride;
+      a.Wc = (W - pw + stride - 1) / stride;
+      a.r0 = (ph + pad) % stride;
+      a.s0 = (pw + pad) % stride;
+      a.nr = a.r0 < R ? (R - a.r0 + stride - 1) / stride : 0;
+      a.ns = a.s0 < S ? (S - a.s0 + stride - 1) / stride : 0;
+      a.M = B * a.Hc * a.Wc;
+      a.K = a.nr * a.ns * Cout;
+      if (a.M <= 0) continue;
+      if (a.K == 0 && accumulate && !addend) continue;
+      ConvArgs p = pipe_args(a);
+      p.fy = y; p.fcoef = coef; p.frelu = relu;
+      if (!conv_pipe16_launch(DGRAD, dtype, p, stream)) {
+        set_error("conv2d_bwd_data_fold_h16: shape outside the pipelined kernel");
+        return kErrArg;
+      }
+    }
+  return check_launch("conv2d_bwd_data_fold_h16");
+}
+
 MAUV_API int mauv_conv2d_bwd_weight_h16(int dtype, const void* x, const long long* x_strides,
                                         const float* x_scale, const float* x_shift, int x_relu,
                                         const void* dy, float* ws, int splits, int G, int B,

@@ -35,6 +35,7 @@ SIGNATURES = {
     # conv_gemm16.hip
     "mauv_conv2d_fwd_h16": [I, P, P, P, P, I, P, P] + [I] * 10 + [P, P, P, P],
     "mauv_conv2d_bwd_data_h16": [I, P, P, P, P, I] + [I] * 10 + [P],
+    "mauv_conv2d_bwd_data_fold_h16": [I, P, P, P, I, P, P, P, I] + [I] * 10 + [P],
     "mauv_reparam_sample_ex": [I, P, P, P, ctypes.c_ulonglong, ctypes.c_ulonglong, P, ctypes.c_uint,
                                I, I, I, I, I, P, LL, P],
     "mauv_conv2d_bwd_weight_h16": [I, P, P, P, P, I, P, P, I] + [I] * 10 + [P],

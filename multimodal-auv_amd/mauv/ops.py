@@ -173,6 +173,23 @@ def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=Non
             _p(b.get("p1")), _p(b.get("p2")), stream()), "conv2d_bwd_data")
 
 
+def conv2d_bwd_data_fold(dout, y, coef, relu, w, dx, G, B, H, W, Cin, Cout, R, stride, pad,
+                         addend=None, accumulate=False):
+    """16-bit prototype: conv2d_bwd_data of dy = alpha*dz + beta*y + gamma computed in the
+    A-loader from the BN's (y, dout); coef fp32 [5][G][Cout] (alpha, beta, gamma, sc, sh)."""
+    _h16(w.dtype, dout, y, w, dx, addend)
+    _f32(coef)
+    Ho = out_hw(H, R, stride, pad)
+    fl = 2.0 * G * B * Ho * Ho * Cout * R * R * Cin
+    nb = w.element_size() * (2 * G * B * Ho * Ho * Cout + G * Cout * R * R * Cin +
+                             G * B * H * W * Cin * (1 + (addend is not None) + bool(accumulate)))
+    with _Prof("dgrad_" + str(w.dtype)[6:], fl, nb):
+        check(lib.mauv_conv2d_bwd_data_fold_h16(H16[w.dtype], _p(dout), _p(y), _p(coef), int(relu),
+                                                _p(w), _p(dx), _p(addend), int(accumulate), G, B,
+                                                H, W, Cin, Cout, R, R, stride, pad, stream()),
+              "conv2d_bwd_data_fold_h16")
+
+
 def wgrad_splits(G, B, H, W, Cin, Cout, R, stride, pad):
     return lib.mauv_conv2d_wgrad_splits(G, B, H, W, Cin, Cout, R, R, stride, pad)
 

@@ -263,3 +263,39 @@ def test_reparam16_padded_sample_and_bwd(dt):
                     Cin, RS)
     assert torch.equal(dmu_a, dmu_b) and torch.equal(drho_a, drho_b)
 
+
+
+@pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
+@pytest.mark.parametrize("case", [(2, 2, 8, 64, 64, 3, 1, 1), (1, 3, 9, 128, 128, 3, 2, 1),
+                                  (2, 2, 6, 256, 64, 1, 1, 0)])
+def test_conv16_dgrad_bn_fold_prototype(case, dt):
+    """The BN-backward-fold prototype: the data gradient with dy = alpha*dz +
+    beta*y + gamma computed in the A-loader equals the data gradient of the materialised
+    16-bit dy of the same BN backward (ReLU mask from y*sc+sh) within the 16-bit rounding of dy."""
+    from mauv import ops
+    G, B, H, Cin, Cout, R, st, pad = case
+    torch.manual_seed(3)
+    Ho = ops.out_hw(H, R, st, pad)
+    M = B * Ho * Ho
+    y = torch.randn(G, B, Ho, Ho, Cout).to(dt)
+    dout = torch.randn(G, B, Ho, Ho, Cout).to(dt)
+    w = (torch.randn(G, Cout, R, R, Cin) / math.sqrt(Cin * R * R)).to(dt)
+    mean = torch.randn(G, Cout) * 0.1
+    invstd = torch.rand(G, Cout) + 0.5
+    sc = torch.rand(G, Cout) + 0.5
+    sh = torch.randn(G, Cout) * 0.1
+    yd, dd = y.double().view(G, M, Cout), dout.double().view(G, M, Cout)
+    dz = dd * ((yd * sc.double()[:, None] + sh.double()[:, None]) > 0)
+    xh = (yd - mean.double()[:, None]) * invstd.double()[:, None]
+    k1, k2 = dz.mean(1), (dz * xh).mean(1)
+    dy = (sc.double()[:, None] * (dz - k1[:, None] - xh * k2[:, None])).to(dt)
+    coef = torch.stack([sc.double(), -sc.double() * invstd.double() * k2,
+                        sc.double() * (invstd.double() * k2 * mean.double() - k1), sc.double(),
+                        sh.double()]).float()
+    dx_ref = torch.empty(G, B, H, H, Cin, device=dev, dtype=dt)
+    ops.conv2d_bwd_data(dy.view(G, B, Ho, Ho, Cout).to(dev), w.to(dev), dx_ref, G, B, H, H, Cin,
+                        Cout, R, st, pad)
+    dx = torch.empty_like(dx_ref)
+    ops.conv2d_bwd_data_fold(dout.to(dev), y.to(dev), coef.to(dev).contiguous(), 1, w.to(dev), dx,
+                             G, B, H, H, Cin, Cout, R, st, pad)
+    close(dx, dx_ref, 8 * ULP[dt])
