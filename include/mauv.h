@@ -58,11 +58,17 @@ int mauv_conv2d_fwd_stat_blocks(int G, int B, int H, int W, int Cin, int Cout, i
  * bn_* (nullable): dx is the output gradient of a BatchNorm(+ReLU) whose backward partial
  * sums (sum dz, sum dz*xhat per channel; [G][nblk][Cin], nblk from
  * mauv_conv2d_bwd_data_stat_blocks) the epilogue writes for mauv_bn_bwd's pre_p1/pre_p2;
- * the ReLU mask comes from bn_out, else from bn_y*bn_scale+bn_shift. */
+ * the ReLU mask comes from bn_mask bits (mauv_bn_apply_mask), else bn_out, else from
+ * bn_y*bn_scale+bn_shift.  addend_mask
+ * (nullable): the addend counts only where these ReLU-mask bits ([G][B*H*W][Cin] / 8,
+ * mauv_bn_apply_mask) are set — a block output's residual gradient dres = dout * mask added
+ * without being stored. */
 int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx, const float* addend,
+                             const unsigned char* addend_mask,
                              int accumulate, int G, int B, int H, int W, int Cin, int Cout,
                              int R, int S, int stride, int pad, const float* bn_y,
-                             const float* bn_out, const float* bn_scale, const float* bn_shift,
+                             const float* bn_out, const unsigned char* bn_mask,
+                             const float* bn_scale, const float* bn_shift,
                              const float* bn_mean, const float* bn_invstd, int bn_relu,
                              float* bn_p1, float* bn_p2, hipStream_t stream);
 int mauv_conv2d_bwd_data_stat_blocks(int G, int B, int H, int W, int Cin, int Cout, int R,
@@ -105,14 +111,21 @@ int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, void* dx,
                              const void* addend, int accumulate, int G, int B, int H, int W,
                              int Cin, int Cout, int R, int S, int stride, int pad,
                              hipStream_t stream);
-/* Prototype: mauv_conv2d_bwd_data_h16 whose dy is the BatchNorm backward of
- * (y, dout) computed in the A-loader instead of read materialised: dy = alpha*dz + beta*y +
- * gamma per channel, dz = dout * [y*sc + sh > 0] when relu, coef = fp32 [5][G][Cout] (alpha,
- * beta, gamma, sc, sh).  Cout % 64 == 0. */
-int mauv_conv2d_bwd_data_fold_h16(int dtype, const void* dout, const void* y, const float* coef,
-                                  int relu, const void* w, void* dx, const void* addend,
-                                  int accumulate, int G, int B, int H, int W, int Cin, int Cout,
-                                  int R, int S, int stride, int pad, hipStream_t stream);
+/* mauv_conv2d_bwd_data_h16 whose epilogue also writes the BatchNorm-backward partial sums of
+ * the BN whose output gradient dx is (bn_p1 = sum dz, bn_p2 = sum dz*xhat, [G][nblk][Cin], nblk
+ * = mauv_conv2d_bwd_data_stat_blocks), for mauv_bn_bwd_ex's pre_p1/pre_p2: the standalone
+ * partial pass over (y, dout) of models/resnet50_variational.py's BN backward disappears.
+ * ReLU mask: bn_mask bits (mauv_bn_apply_mask) else bn_out > 0 else bn_y*bn_scale+bn_shift > 0.
+ * addend_mask as in mauv_conv2d_bwd_data_f32.  bn_p1 and addend_mask NULL =
+ * mauv_conv2d_bwd_data_h16.  Cout % 64 == 0 with partials or addend_mask. */
+int mauv_conv2d_bwd_data_bn_h16(int dtype, const void* dy, const void* w, void* dx,
+                                const void* addend, int accumulate, int G, int B, int H, int W,
+                                int Cin, int Cout, int R, int S, int stride, int pad,
+                                const unsigned char* addend_mask, const void* bn_y, const void* bn_out,
+                                const unsigned char* bn_mask, const float* bn_scale,
+                                const float* bn_shift, const float* bn_mean,
+                                const float* bn_invstd, int bn_relu, float* bn_p1, float* bn_p2,
+                                hipStream_t stream);
 int mauv_conv2d_bwd_weight_h16(int dtype, const void* x, const long long* x_strides,
                                const float* x_scale, const float* x_shift, int x_relu,
                                const void* dy, float* ws, int splits, int G, int B, int H, int W,
@@ -257,6 +270,15 @@ int mauv_bn_bwd_mask(int dtype, const void* y, const unsigned char* mask, const 
                      const float* mean, const float* invstd, const float* scale, int G,
                      long long M, int C, float* workspace, void* dy, void* dres, float* dgamma,
                      float* dbeta, hipStream_t stream);
+/* Every form above in one entry (dtype -1 fp32, 0 bf16, 1 f16): ReLU mask from mask bits, else
+ * out, else y*scale+shift; pre_p1/pre_p2/pre_nblk (nullable): partial sums a data-gradient
+ * epilogue already wrote (mauv_conv2d_bwd_data_bn_h16 / _f32), so only the finalize and the
+ * apply pass run.  dy and dres both NULL: partials / parameter gradients only. */
+int mauv_bn_bwd_ex(int dtype, const void* y, const void* out, const unsigned char* mask,
+                   const void* dout, int relu, const float* mean, const float* invstd,
+                   const float* scale, const float* shift, int G, long long M, int C,
+                   float* workspace, void* dy, void* dres, float* dgamma, float* dbeta,
+                   const float* pre_p1, const float* pre_p2, int pre_nblk, hipStream_t stream);
 
 /* ---- pooling (pool.hip): torchvision stem maxpool 3x3/2 pad 1 and adaptive avgpool ------ */
 /* max-pool forward: C % 8 == 0 (the stem: 64); backward: C % 4 == 0. */

@@ -406,6 +406,63 @@ __global__ __launch_bounds__(1024) void bn_bwd_final(int G, int nblk, int C, lon
   k2[g * C + c] = (float)(b / (double)M);
 }
 
+// Many partials per channel (the data-gradient epilogue's one per 128-row tile: thousands at the
+// layer-1 shapes) are reduced in segments of SEGB by (C/64, G, S) blocks into double pairs, then
+// one thread per channel sums the segments in order, forms k1 / k2 for every group and the
+// parameter gradients (stage 3 below, fused) — the single-block-per-(group, 64 channels) stage
+// 2 above walks every partial of a layer with G * C / 64 blocks.
+// (Only above 1024 partials — the epilogue's — : for the standalone pass's <= 1024 the extra
+// launch ate the gain, bf16 step 3.55 vs 3.55 ms of finalize kernels, tools/gpubatch_r3i.sh.)
+constexpr int SEGB = 128, kSegAbove = 1024;
+static inline int bwd_segs(int nblk) { return (nblk + SEGB - 1) / SEGB; }
+
+__global__ __launch_bounds__(1024) void bn_bwd_seg(int nblk, int C, const float* __restrict__ p1,
+                                                   const float* __restrict__ p2,
+                                                   double* __restrict__ seg) {
+  const int g = blockIdx.y, sg = blockIdx.z, S = gridDim.z;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int b0 = sg * SEGB, b1 = min(nblk, b0 + SEGB);
+  __shared__ double red[FIN_L][64];
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int k = b0 + ty; k < b1; k += FIN_L) {
+      const long long o = ((long long)g * nblk + k) * C + c;
+      a += p1[o];
+      b += p2[o];
+    }
+  }
+  a = lane_sum16(a, red, tx, ty);
+  b = lane_sum16(b, red, tx, ty);
+  if (ty != 0 || c >= C) return;
+  double* o = seg + (((long long)g * S + sg) * C + c) * 2;
+  o[0] = a;
+  o[1] = b;
+}
+
+__global__ void bn_bwd_merge(int G, int S, int C, long long M, const double* __restrict__ seg,
+                             float* __restrict__ k1, float* __restrict__ k2,
+                             float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double tg = 0.0, tb = 0.0;
+  for (int g = 0; g < G; ++g) {
+    double a = 0.0, b = 0.0;
+    for (int s = 0; s < S; ++s) {
+      const double* o = seg + (((long long)g * S + s) * C + c) * 2;
+      a += o[0];
+      b += o[1];
+    }
+    const float f1 = (float)(a / (double)M), f2 = (float)(b / (double)M);
+    k1[g * C + c] = f1;
+    k2[g * C + c] = f2;
+    tb += f1;
+    tg += f2;
+  }
+  if (dgamma) dgamma[c] += (float)(tg * (double)M);
+  if (dbeta) dbeta[c] += (float)(tb * (double)M);
+}
+
 // Backward stage 3: dgamma += M * sum_g k2, dbeta += M * sum_g k1 (sample order).
 __global__ void bn_bwd_param_kernel(int G, int C, long long M, const float* __restrict__ k1,
                                     const float* __restrict__ k2, float* __restrict__ dgamma,
@@ -654,7 +711,11 @@ MAUV_API long long mauv_bn_workspace_floats(int G, long long M, int C) {
   const long long fwd = (long long)G * nblk * (2LL * C + 1) + 2LL * G * C + stats_ws_floats(G, nblk, C);
   if (C <= 0 || C % 8 != 0 || C > 2048) return fwd;
   bwd_geometry(M, C, bnblk, brpb);
-  const long long bwd = 2LL * G * bnblk * C + 2LL * G * C;
+  // + the segment pairs of bn_bwd_seg for the most partials either source gives (the
+  // standalone pass's bnblk, or a data-gradient epilogue's one per >= 64 rows), 8-B aligned
+  const long long pre = (M + 63) / 64;
+  const long long nseg = (((pre > bnblk ? pre : bnblk) + SEGB - 1) / SEGB);
+  const long long bwd = 2LL * G * bnblk * C + 2LL * G * C + 4LL * G * nseg * C + 2;
   return fwd > bwd ? fwd : bwd;
 }
 
@@ -733,18 +794,29 @@ static int bn_bwd_impl(const typename S::T* y, const typename S::T* out,
   float* p2 = p1 + (long long)G * nblk * C;
   float* k1 = p2 + (long long)G * nblk * C;
   float* k2 = k1 + (long long)G * C;
-  if (pre_p1) {  // partial sums already produced by the dgrad epilogue (conv_gemm.hip)
-    hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, pre_nblk,
-                       C, M, pre_p1, pre_p2, k1, k2);
+  const float* q1 = p1;
+  const float* q2 = p2;
+  int qn = nblk;
+  if (pre_p1) {  // partial sums already produced by a data-gradient epilogue
+    q1 = pre_p1; q2 = pre_p2; qn = pre_nblk;
   } else {
     hipLaunchKernelGGL(bn_bwd_partial<S>, dim3(nblk, G), dim3(256), 0, stream, y, out, dout,
                        relu, mean, invstd, scale, shift, M, C, rpb, rm, p1, p2, mask);
-    hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, nblk, C,
-                       M, p1, p2, k1, k2);
   }
-  if (dgamma || dbeta)
-    hipLaunchKernelGGL(bn_bwd_param_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C, M,
-                       k1, k2, dgamma, dbeta);
+  const int nseg = qn > kSegAbove ? bwd_segs(qn) : 1;
+  if (nseg > 1) {
+    double* seg = (double*)(((uintptr_t)(k2 + (long long)G * C) + 7) & ~(uintptr_t)7);
+    hipLaunchKernelGGL(bn_bwd_seg, dim3((C + 63) / 64, G, nseg), dim3(1024), 0, stream, qn, C,
+                       q1, q2, seg);
+    hipLaunchKernelGGL(bn_bwd_merge, dim3((C + 255) / 256), dim3(256), 0, stream, G, nseg, C, M,
+                       seg, k1, k2, dgamma, dbeta);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, qn, C, M,
+                       q1, q2, k1, k2);
+    if (dgamma || dbeta)
+      hipLaunchKernelGGL(bn_bwd_param_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
+                         M, k1, k2, dgamma, dbeta);
+  }
   if (!dy && !dres) return check_launch("bn_bwd");   // partial sums / parameter grads only
   if (mask || use_rows(C)) {
     int anblk, arpb;
@@ -832,5 +904,25 @@ MAUV_API int mauv_bn_bwd_mask(int dtype, const void* y, const unsigned char* mas
                                         scale, nullptr, G, M, C, workspace, (u16*)dy, (u16*)dres, \
                                         dgamma, dbeta, nullptr, nullptr, 0, stream, mask);
   MAUV_DT_DISPATCH(dtype, "bn_bwd_mask", L)
+#undef L
+}
+
+MAUV_API int mauv_bn_bwd_ex(int dtype, const void* y, const void* out, const unsigned char* mask,
+                            const void* dout, int relu, const float* mean, const float* invstd,
+                            const float* scale, const float* shift, int G, long long M, int C,
+                            float* workspace, void* dy, void* dres, float* dgamma, float* dbeta,
+                            const float* pre_p1, const float* pre_p2, int pre_nblk,
+                            hipStream_t stream) {
+  if (pre_p1 && (!pre_p2 || pre_nblk <= 0)) { set_error("bn_bwd_ex: pre_p1 needs pre_p2 and pre_nblk > 0"); return kErrArg; }
+  if (mask) relu = 1, out = nullptr;
+  if (dtype < 0)
+    return bn_bwd_impl<SF32>((const float*)y, (const float*)out, (const float*)dout, relu, mean,
+                             invstd, scale, shift, G, M, C, workspace, (float*)dy, (float*)dres,
+                             dgamma, dbeta, pre_p1, pre_p2, pre_nblk, stream, mask);
+#define L(D) return bn_bwd_impl<S16<D>>((const u16*)y, (const u16*)out, (const u16*)dout, relu, mean, \
+                                        invstd, scale, shift, G, M, C, workspace, (u16*)dy,       \
+                                        (u16*)dres, dgamma, dbeta, pre_p1, pre_p2, pre_nblk,      \
+                                        stream, mask);
+  MAUV_DT_DISPATCH(dtype, "bn_bwd_ex", L)
 #undef L
 }

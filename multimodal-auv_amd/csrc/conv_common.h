@@ -42,6 +42,11 @@ struct ConvArgs {
   int bp_relu;
   float *bp_p1, *bp_p2;
   int bp_nblk, bp_base;
+  const unsigned char* bp_mask;  // DGRAD: the ReLU mask as bn_apply_mask's bits
+  // DGRAD: the residual addend is taken where this ReLU mask (bn_apply_mask's bits over the
+  // [G][M][N] output) is set, 0 elsewhere: the residual branch's gradient dres = dout * mask
+  // of a block output's BN is added without being written as a tensor
+  const unsigned char* add_mask;
   // WGRAD pixel -> (b, oh, ow) by multiply-shift division (conv_split.hip): n / d =
   // (n * mg) >> sh for n < 2^31 (mauv::magic_div)
   unsigned long long mg_hw, mg_w;
@@ -54,11 +59,6 @@ struct ConvArgs {
   int cpg;
   // block order over the whole grid (1, default) or over blockIdx.x only (0): see conv_block_tile
   int xcd_grid;
-  // 16-bit DGRAD with the BN backward folded into the A-loader (conv_pipe16.hip bn_bwd8): dy =
-  // dout (a.dy) of that BN, fy its input y, fcoef [5][G][Cout] = alpha, beta, gamma, sc, sh
-  const void* fy;
-  const float* fcoef;
-  int frelu;
 };
 
 // XCD-aware block -> (tile, group / split-K slice) map.  Blocks are dealt round-robin over the 8
@@ -210,7 +210,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx16 (&acc)
         if (bst) {
           bmu = a.bp_mean[g * a.N + col];
           bis = a.bp_invstd[g * a.N + col];
-          if (!a.bp_out) { bsc = a.bp_sc[g * a.N + col]; bsh = a.bp_sh[g * a.N + col]; }
+          if (!a.bp_out && !a.bp_mask) { bsc = a.bp_sc[g * a.N + col]; bsh = a.bp_sh[g * a.N + col]; }
         }
       }
 #pragma unroll
@@ -228,13 +228,20 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx16 (&acc)
         const long long o = MODE == FWD ? conv_out_index(a, orow, col) : orow * a.N + col;
         float v = acc[mi][ni][r] + bias;
         if constexpr (MODE == DGRAD) {
-          if (a.addend) v += a.addend[(long long)g * a.out_sg + o];
+          if (a.addend) {
+            const long long ao = (long long)g * a.out_sg + o;
+            if (!a.add_mask || ((a.add_mask[ao >> 3] >> (ao & 7)) & 1u)) v += a.addend[ao];
+          }
           if (a.accumulate) v += outg[o];
           if (bst) {
             const long long go = (long long)g * a.out_sg + o;
             const float yv = a.bp_y[go];
-            const float pre = a.bp_out ? a.bp_out[go] : yv * bsc + bsh;
-            const float dz = (!a.bp_relu || pre > 0.f) ? v : 0.f;
+            bool on = true;
+            if (a.bp_relu) {
+              if (a.bp_mask) on = (a.bp_mask[go >> 3] >> (go & 7)) & 1u;
+              else on = (a.bp_out ? a.bp_out[go] : yv * bsc + bsh) > 0.f;
+            }
+            const float dz = on ? v : 0.f;
             s1[ni] += dz;
             s2[ni] += dz * (yv - bmu) * bis;
           }

@@ -1,7 +1,8 @@
 // Epilogue of the 16-bit implicit-GEMM convs (conv_pipe16.hip) for FWD and
 // DGRAD: BN statistics partials of y from the fp32 accumulators (tile mean, then M2 around it;
 // FWD with st_mean), then the 16-bit output through LDS as 16-byte row chunks (DGRAD: residual
-// addend / previous dx added in fp32, one rounding; parity-class row remap).  acc[MI][NI] are
+// addend / previous dx added in fp32, one rounding; parity-class row remap; with bp_p1 the
+// BN-backward partial sums of the BatchNorm whose output gradient dx is).  acc[MI][NI] are
 // this wave's 32 x 32 accumulator tiles (C/D layout of v_mfma_f32_32x32x16: lane l = column
 // l & 31, register r = row (r & 3) + 8 (r >> 2) + 4 (l >> 5)); waves wave = wm * WGN + wn.
 // The caller's main loop ended with a barrier: the LDS (SCRATCH bytes) is free.
@@ -126,9 +127,68 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
   constexpr int SLD = BN + 4, CPR = BN / 8;
   constexpr int PASSES = BM * SLD * 4 <= SCRATCH ? 1 : WGM, PR = BM / PASSES;
   constexpr int NCH = PR * CPR;
+  static_assert(NT % CPR == 0 && 64 % CPR == 0, "a thread keeps one 8-column chunk");
   float* stile = (float*)smem;
   u16* outp = (u16*)a.out;
   const u16* addp = (const u16*)a.addend;
+  // DGRAD + bp_p1: this dx is the output gradient of a BatchNorm (+ReLU); the store loop also
+  // sums dz = dx * relu-mask and dz * xhat per column (bn_bwd_partial's two sums, bn.hip), from
+  // the ROUNDED 16-bit dx the apply pass will read, with y / the mask read as 16-byte chunks
+  // beside the store — one per-(m-tile, column) partial instead of a pass over y and dx
+  const bool bst = MODE == DGRAD && a.bp_p1;
+  const int bcol = n0 + 8 * (tid % CPR);
+  floatx8 b1 = {}, b2 = {}, bmu = {}, bis = {}, bsc = {}, bsh = {};
+  if (bst && bcol < a.N) {
+    bmu = ldf8(a.bp_mean + (long long)g * a.N + bcol);
+    bis = ldf8(a.bp_invstd + (long long)g * a.N + bcol);
+    if (a.bp_relu && !a.bp_out && !a.bp_mask) {
+      bsc = ldf8(a.bp_sc + (long long)g * a.N + bcol);
+      bsh = ldf8(a.bp_sh + (long long)g * a.N + bcol);
+    }
+  }
+  // chunk c of pass `pass` -> its output element offset (false: outside the tile)
+  auto chunk = [&](int pass, int c, long long& o) -> bool {
+    const int rl = c / CPR, cc = c - rl * CPR;
+    const int row = m0 + pass * PR + rl, col = n0 + 8 * cc;
+    if (row >= a.M || col >= a.N) return false;
+    long long orow = row;
+    if constexpr (MODE == DGRAD) {
+      if (a.stride != 1) {
+        const int HW = a.Hc * a.Wc, b = row / HW, rem = row - b * HW;
+        const int i = rem / a.Wc, jj = rem - i * a.Wc;
+        orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
+      }
+    }
+    o = (long long)g * a.out_sg + (MODE == FWD ? conv_out_index(a, orow, col) : orow * a.N + col);
+    return true;
+  };
+  // DGRAD, one pass: the residual addend, the BN's y and its mask bits are fetched into
+  // registers two chunks ahead — the first two BEFORE the accumulators are parked, so their
+  // latency hides behind the LDS round trip instead of serialising each chunk's store (a
+  // previous dx / the BN's stored output, the rarer forms, are read in the loop; deeper
+  // prefetch spills the 128-VGPR budget)
+  constexpr bool PF = MODE == DGRAD && PASSES == 1;
+  constexpr int CPT = (NCH + NT - 1) / NT, PFD = 2;
+  u32x4 pa[PFD], py[PFD];
+  unsigned pm[PFD], pam[PFD];
+  auto prefetch = [&](int k) {
+    long long o;
+    const int q = k % PFD;
+    pa[q] = py[q] = u32x4{0u, 0u, 0u, 0u};
+    pm[q] = pam[q] = 0u;
+    if (k < CPT && tid + k * NT < NCH && chunk(0, tid + k * NT, o)) {
+      if (addp) pa[q] = *(const u32x4*)(addp + o);
+      if (addp && a.add_mask) pam[q] = a.add_mask[o >> 3];
+      if (bst) {
+        py[q] = *(const u32x4*)((const u16*)a.bp_y + o);
+        if (a.bp_mask) pm[q] = a.bp_mask[o >> 3];
+      }
+    }
+  };
+  if constexpr (PF) {
+#pragma unroll
+    for (int k = 0; k < PFD; ++k) prefetch(k);
+  }
 #pragma unroll
   for (int pass = 0; pass < PASSES; ++pass) {
     if (PASSES == 1 || wm == pass) {
@@ -143,27 +203,30 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
     }
     __syncthreads();
 #pragma unroll
-    for (int c = tid; c < NCH; c += NT) {
+    for (int k = 0; k * NT < NCH; ++k) {
+      const int c = tid + k * NT;
+      long long o;
+      if (c >= NCH || !chunk(pass, c, o)) {
+        if constexpr (PF) prefetch(k + PFD);  // (slot k % PFD is this chunk's: free)
+        continue;
+      }
       const int rl = c / CPR, cc = c - rl * CPR;
-      const int row = m0 + pass * PR + rl, col = n0 + 8 * cc;
-      if (row >= a.M || col >= a.N) continue;
       const floatx4 v0 = *(const floatx4*)(stile + rl * SLD + 8 * cc);
       const floatx4 v1 = *(const floatx4*)(stile + rl * SLD + 8 * cc + 4);
       floatx8 f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) { f[e] = v0[e]; f[4 + e] = v1[e]; }
-      long long orow = row;
+      const int kk = k % PFD;
       if constexpr (MODE == DGRAD) {
-        if (a.stride != 1) {
-          const int HW = a.Hc * a.Wc, b = row / HW, rem = row - b * HW;
-          const int i = rem / a.Wc, jj = rem - i * a.Wc;
-          orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
+        if (addp) {
+          floatx8 av = unpack8<DT>(PF ? pa[kk] : *(const u32x4*)(addp + o));
+          if (a.add_mask) {  // dres = dout * mask of the block output's BN, never stored
+            const unsigned m = PF ? pam[kk] : a.add_mask[o >> 3];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) av[e] = (m >> e) & 1u ? av[e] : 0.f;
+          }
+          f += av;
         }
-      }
-      const long long o = (long long)g * a.out_sg +
-                          (MODE == FWD ? conv_out_index(a, orow, col) : orow * a.N + col);
-      if constexpr (MODE == DGRAD) {
-        if (addp) f += unpack8<DT>(*(const u32x4*)(addp + o));
         if (a.accumulate) f += unpack8<DT>(*(const u32x4*)(outp + o));
       }
       u32x4 pk;
@@ -173,8 +236,59 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
         asm("" : "+v"(pk[e]));
       }
       *(u32x4*)(outp + o) = pk;
+      if (bst) {
+        floatx8 dz = unpack8<DT>(pk);
+        const floatx8 yv = unpack8<DT>(PF ? py[kk] : *(const u32x4*)((const u16*)a.bp_y + o));
+        if (a.bp_relu) {
+          if (a.bp_mask) {  // bn_apply_mask's bits: one byte per 8 channels
+            const unsigned m = PF ? pm[kk] : a.bp_mask[o >> 3];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dz[e] = (m >> e) & 1u ? dz[e] : 0.f;
+          } else {
+            const floatx8 pre =
+                a.bp_out ? unpack8<DT>(*(const u32x4*)((const u16*)a.bp_out + o))
+                         : yv * bsc + bsh;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dz[e] = pre[e] > 0.f ? dz[e] : 0.f;
+          }
+        }
+        b1 += dz;
+        b2 += dz * (yv - bmu) * bis;
+      }
+      if constexpr (PF) prefetch(k + PFD);
     }
     if (pass + 1 < PASSES) __syncthreads();
+  }
+  if (bst) {
+    // the lanes of a wave that share a column chunk, then the waves, through LDS
+#pragma unroll
+    for (int off = CPR; off < 64; off *= 2)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        b1[e] += __shfl_xor(b1[e], off, 64);
+        b2[e] += __shfl_xor(b2[e], off, 64);
+      }
+    constexpr int NW = NT / 64;
+    static_assert(2 * NW * BN * 4 <= SCRATCH, "bn-backward partials scratch");
+    float* red = (float*)smem;
+    __syncthreads();  // the last pass's reads of stile are done
+    if (lane < CPR) {
+      *(floatx4*)(red + wave * BN + 8 * lane) = __builtin_shufflevector(b1, b1, 0, 1, 2, 3);
+      *(floatx4*)(red + wave * BN + 8 * lane + 4) = __builtin_shufflevector(b1, b1, 4, 5, 6, 7);
+      *(floatx4*)(red + (NW + wave) * BN + 8 * lane) = __builtin_shufflevector(b2, b2, 0, 1, 2, 3);
+      *(floatx4*)(red + (NW + wave) * BN + 8 * lane + 4) = __builtin_shufflevector(b2, b2, 4, 5, 6, 7);
+    }
+    __syncthreads();
+    if (tid < 2 * BN) {
+      const int col = tid % BN, which = tid / BN;
+      if (n0 + col < a.N) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) t += red[(which * NW + w) * BN + col];
+        const long long so = ((long long)g * a.bp_nblk + a.bp_base + m0 / BM) * a.N + n0 + col;
+        (which ? a.bp_p2 : a.bp_p1)[so] = t;
+      }
+    }
   }
 }
 

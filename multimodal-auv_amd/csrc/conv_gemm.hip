@@ -687,22 +687,25 @@ MAUV_API int mauv_stem_fwd_f32(const float* cols, const float* w, float* y, int 
 
 // Data gradient: dx[g] = conv_transpose(dy[g], W_g) (+ addend) (+ dx if accumulate).
 MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx,
-                                      const float* addend, int accumulate, int G, int B, int H,
+                                      const float* addend, const unsigned char* addend_mask,
+                                      int accumulate, int G, int B, int H,
                                       int W, int Cin, int Cout, int R, int S, int stride,
                                       int pad, const float* bn_y, const float* bn_out,
+                                      const unsigned char* bn_mask,
                                       const float* bn_scale, const float* bn_shift,
                                       const float* bn_mean, const float* bn_invstd, int bn_relu,
                                       float* bn_p1, float* bn_p2, hipStream_t stream) {
   ConvArgs a = make_args(G, B, H, W, Cin, Cout, R, S, stride, pad, nullptr);
   a.dy = dy; a.w = w; a.out = dx; a.addend = addend; a.accumulate = accumulate;
+  a.add_mask = addend ? addend_mask : nullptr;
   a.N = Cin;
   a.out_sg = (long long)B * H * W * Cin;
-  a.bp_y = bn_y; a.bp_out = bn_out; a.bp_sc = bn_scale; a.bp_sh = bn_shift;
+  a.bp_y = bn_y; a.bp_out = bn_out; a.bp_mask = bn_mask; a.bp_sc = bn_scale; a.bp_sh = bn_shift;
   a.bp_mean = bn_mean; a.bp_invstd = bn_invstd; a.bp_relu = bn_relu;
   a.bp_p1 = bn_p1; a.bp_p2 = bn_p2;
   a.bp_nblk = dgrad_stat_blocks(G, B, H, W, Cin, stride);
   a.bp_base = 0;
-  if (bn_p1 && bn_relu && !bn_out && !bn_shift) { set_error("conv2d_bwd_data: mask source"); return kErrArg; }
+  if (bn_p1 && bn_relu && !bn_out && !bn_mask && !bn_shift) { set_error("conv2d_bwd_data: mask source"); return kErrArg; }
   const bool va = (Cout % 32 == 0), vb = (Cin % 4 == 0);
   // one launch per output-parity class (stride^2 of them; 1 for stride 1)
   for (int ph = 0; ph < stride; ++ph)

@@ -588,13 +588,45 @@ MAUV_API int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, 
                                       const void* addend, int accumulate, int G, int B, int H,
                                       int W, int Cin, int Cout, int R, int S, int stride, int pad,
                                       hipStream_t stream) {
+  return mauv_conv2d_bwd_data_bn_h16(dtype, dy, w, dx, addend, accumulate, G, B, H, W, Cin, Cout,
+                                     R, S, stride, pad, nullptr, nullptr, nullptr, nullptr,
+                                     nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr,
+                                     stream);
+}
+
+// The data gradient with the BN-backward partial sums of the BatchNorm whose output gradient dx
+// is (bn_bwd_partial's sum dz, sum dz*xhat per [G][nblk][Cin], nblk =
+// mauv_conv2d_bwd_data_stat_blocks) written by the epilogue (conv_epi16.h).  ReLU mask source:
+// bn_mask bits (mauv_bn_apply_mask), else bn_out > 0, else bn_y*bn_scale + bn_shift > 0.  The
+// partials need the pipelined kernel (Cout % 64 == 0) and every dx row written by this call
+// (accumulate without addend over a tapless parity class is refused).  addend_mask (nullable):
+// the addend counts only where these ReLU-mask bits ([G][B*H*W][Cin] / 8, mauv_bn_apply_mask)
+// are set — the residual gradient of a block output's BN without a dres tensor.
+MAUV_API int mauv_conv2d_bwd_data_bn_h16(int dtype, const void* dy, const void* w, void* dx,
+                                         const void* addend, int accumulate, int G, int B, int H,
+                                         int W, int Cin, int Cout, int R, int S, int stride,
+                                         int pad, const unsigned char* addend_mask,
+                                         const void* bn_y, const void* bn_out,
+                                         const unsigned char* bn_mask, const float* bn_scale,
+                                         const float* bn_shift, const float* bn_mean,
+                                         const float* bn_invstd, int bn_relu, float* bn_p1,
+                                         float* bn_p2, hipStream_t stream) {
   if (int e = check_shape16("conv2d_bwd_data_h16", dtype, G, B, Cin, Cout, nullptr)) return e;
   if (Cout % HBK) { set_error("conv2d_bwd_data_h16: needs Cout % 32 == 0"); return kErrArg; }
+  const bool bst = bn_p1 != nullptr;
+  if (addend_mask && (!addend || Cout % 64)) { set_error("conv2d_bwd_data_bn_h16: addend_mask needs an addend and Cout % 64 == 0"); return kErrArg; }
+  if (bst) {
+    if (!bn_p2 || !bn_y || !bn_mean || !bn_invstd || Cout % 64) { set_error("conv2d_bwd_data_bn_h16: partials need p1, p2, y, mean, invstd and Cout % 64 == 0"); return kErrArg; }
+    if (bn_relu && !bn_mask && !bn_out && (!bn_scale || !bn_shift)) { set_error("conv2d_bwd_data_bn_h16: relu mask needs mask, out or scale/shift"); return kErrArg; }
+    if (!aligned16(bn_y) || !aligned16(bn_out)) { set_error("conv2d_bwd_data_bn_h16: y, out must be 16-B aligned"); return kErrArg; }
+  }
   ConvArgs16 a = make_args16(G, B, H, W, Cin, Cout, R, S, stride, pad, nullptr);
   a.dy = (const u16*)dy; a.w = (const u16*)w; a.out = dx;
   a.addend = (const u16*)addend; a.accumulate = accumulate;
   a.N = Cin;
   a.out_sg = (long long)B * H * W * Cin;
+  int bp_base = 0;
+  const int bp_nblk = bst ? mauv_conv2d_bwd_data_stat_blocks(G, B, H, W, Cin, Cout, R, S, stride, pad) : 0;
   for (int ph = 0; ph < stride; ++ph)
     for (int pw = 0; pw < stride; ++pw) {
       a.ph = ph; a.pw = pw;
@@ -608,50 +640,25 @@ MAUV_API int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, 
       a.K = a.nr * a.ns * Cout;
       if (a.M <= 0) continue;
       // a tapless class accumulating into dx adds nothing (stride-2 1x1 downsample: 3 of 4)
-      if (a.K == 0 && accumulate && !addend) continue;
-      if (!conv_pipe16_launch(DGRAD, dtype, pipe_args(a), stream))
-        dispatch16<H_DGRAD, true>(dtype, a, stream);
-    }
-  return check_launch("conv2d_bwd_data_h16");
-}
-
-// Prototype: the data gradient whose dy is the BN backward of (y, dout)
-// computed in the A-loader, dy = alpha*dz + beta*y + gamma with dz = dout * [y*sc + sh > 0]
-// (relu) — coef [5][G][Cout] = alpha, beta, gamma, sc, sh — instead of a materialised dy.
-// Pipelined-kernel shapes only (Cout % 64 == 0, Cin % 8 == 0).
-MAUV_API int mauv_conv2d_bwd_data_fold_h16(int dtype, const void* dout, const void* y,
-                                           const float* coef, int relu, const void* w, void* dx,
-                                           const void* addend, int accumulate, int G, int B,
-                                           int H, int W, int Cin, int Cout, int R, int S,
-                                           int stride, int pad, hipStream_t stream) {
-  if (int e = check_shape16("conv2d_bwd_data_fold_h16", dtype, G, B, Cin, Cout, nullptr)) return e;
-  if (Cout % 64 || !y || !coef) { set_error("conv2d_bwd_data_fold_h16: needs Cout % 64 == 0, y, coef"); return kErrArg; }
-  ConvArgs16 a = make_args16(G, B, H, W, Cin, Cout, R, S, stride, pad, nullptr);
-  a.dy = (const u16*)dout; a.w = (const u16*)w; a.out = dx;
-  a.addend = (const u16*)addend; a.accumulate = accumulate;
-  a.N = Cin;
-  a.out_sg = (long long)B * H * W * Cin;
-  for (int ph = 0; ph < stride; ++ph)
-    for (int pw = 0; pw < stride; ++pw) {
-      a.ph = ph; a.pw = pw;
-      a.Hc = (H - ph + stride - 1) / stride;
-      a.Wc = (W - pw + stride - 1) / stride;
-      a.r0 = (ph + pad) % stride;
-      a.s0 = (pw + pad) % stride;
-      a.nr = a.r0 < R ? (R - a.r0 + stride - 1) / stride : 0;
-      a.ns = a.s0 < S ? (S - a.s0 + stride - 1) / stride : 0;
-      a.M = B * a.Hc * a.Wc;
-      a.K = a.nr * a.ns * Cout;
-      if (a.M <= 0) continue;
-      if (a.K == 0 && accumulate && !addend) continue;
+      if (a.K == 0 && accumulate && !addend) {
+        if (bst) { set_error("conv2d_bwd_data_bn_h16: partials over a tapless accumulate class"); return kErrArg; }
+        continue;
+      }
       ConvArgs p = pipe_args(a);
-      p.fy = y; p.fcoef = coef; p.frelu = relu;
-      if (!conv_pipe16_launch(DGRAD, dtype, p, stream)) {
-        set_error("conv2d_bwd_data_fold_h16: shape outside the pipelined kernel");
-        return kErrArg;
+      p.add_mask = addend_mask;
+      if (bst) {
+        p.bp_y = (const float*)bn_y; p.bp_out = (const float*)bn_out; p.bp_mask = bn_mask;
+        p.bp_sc = bn_scale; p.bp_sh = bn_shift; p.bp_mean = bn_mean; p.bp_invstd = bn_invstd;
+        p.bp_relu = bn_relu; p.bp_p1 = bn_p1; p.bp_p2 = bn_p2;
+        p.bp_nblk = bp_nblk; p.bp_base = bp_base;
+        bp_base += ceil_div(a.M, conv_tile_rows(a.M));
+        if (!conv_pipe16_launch(DGRAD, dtype, p, stream)) { set_error("conv2d_bwd_data_bn_h16: shape outside the pipelined kernel"); return kErrArg; }
+      } else if (!conv_pipe16_launch(DGRAD, dtype, p, stream)) {
+        if (addend_mask) { set_error("conv2d_bwd_data_bn_h16: addend_mask outside the pipelined kernel"); return kErrArg; }
+        dispatch16<H_DGRAD, true>(dtype, a, stream);
       }
     }
-  return check_launch("conv2d_bwd_data_fold_h16");
+  return check_launch("conv2d_bwd_data_h16");
 }
 
 MAUV_API int mauv_conv2d_bwd_weight_h16(int dtype, const void* x, const long long* x_strides,

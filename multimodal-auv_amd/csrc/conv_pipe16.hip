@@ -37,46 +37,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc16(const void* p, long lon
 __device__ __forceinline__ unsigned mdiv16(unsigned n, unsigned long long m, int s) {
   return (unsigned)(((unsigned long long)n * m) >> s);
 }
-template <int NVA, int NVB, int NVY = 1>
+template <int NVA, int NVB>
 struct Stage16 {
   u32x4 a[NVA], b[NVB];
-  u32x4 y[NVY];  // DGRAD with the BN backward folded in: the BN input y beside dout
   unsigned ok;  // validity bits of pending-BN chunks: a j -> bit j, b j -> bit 8 + j
-  int tc;       // FWD / folded DGRAD: channel offset of this stage's k slice
+  int tc;       // FWD: input-channel offset of this stage's k slice
 };
-
-// The BatchNorm backward folded into the data gradient's A-loader (VERDICT r2 item 2,
-// prototype): instead of reading dy = bn_bwd_apply(y, dout), read y and dout and compute
-//   dy = alpha_c * dz + beta_c * y + gamma_c,  dz = dout * [y * sc_c + sh_c > 0 (relu)],
-// alpha = sc, beta = -sc * invstd * k2, gamma = sc * (invstd * k2 * mean - k1) (the apply pass's
-// sc * (dz - k1 - xhat * k2) regrouped), coefficients fcoef[5][G][C] (alpha, beta, gamma, sc,
-// sh) read per stage through L1.  Padding / ragged chunks stay 0.
-template <int DT>
-__device__ __forceinline__ u32x4 bn_bwd8(u32x4 dout, u32x4 y, const float* co, long long gc,
-                                         long long plane, int relu, bool ok) {
-  const floatx8 al = ldf8(co + gc), be = ldf8(co + plane + gc), ga = ldf8(co + 2 * plane + gc);
-  const floatx8 dz = unpack8<DT>(dout), yv = unpack8<DT>(y);
-  floatx8 v;
-  if (relu) {
-    const floatx8 sc = ldf8(co + 3 * plane + gc), sh = ldf8(co + 4 * plane + gc);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float z = __builtin_fmaf(yv[e], sc[e], sh[e]) > 0.f ? dz[e] : 0.f;
-      v[e] = __builtin_fmaf(al[e], z, __builtin_fmaf(be[e], yv[e], ga[e]));
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf(al[e], dz[e], __builtin_fmaf(be[e], yv[e], ga[e]));
-  }
-  u32x4 o;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    unsigned p = pk2<DT>(v[2 * i], v[2 * i + 1]);
-    asm("" : "+v"(p));
-    o[i] = ok ? p : 0u;
-  }
-  return o;
-}
 
 }  // namespace
 
@@ -221,10 +187,7 @@ void conv_pipe16(const ConvArgs a) {
   }
 
   int t_r = 0, t_s = 0, t_c = 0;  // tile-uniform k position (FWD: r, s, cin; DGRAD: tr, ts, cout)
-  constexpr bool FOLD = XBN && MODE == DGRAD;   // BN backward folded into the A-loader
-  typedef Stage16<NVA, NVB, FOLD ? NVA : 1> St;
-  __amdgpu_buffer_rsrc_t ry;
-  if constexpr (FOLD) ry = rsrc16((const u16*)a.fy + (long long)g * ny, ny);
+  typedef Stage16<NVA, NVB> St;
 
   auto load = [&](St& S, int t) {
     const int k0 = kbeg + t * BK;
@@ -251,16 +214,11 @@ void conv_pipe16(const ConvArgs a) {
       }
     } else if constexpr (MODE == DGRAD) {
       const unsigned soff = (unsigned)((t_c - (t_r * a.Wo + t_s) * a.Cout) * 2);
-      if constexpr (FOLD) { S.ok = 0; S.tc = t_c; }
 #pragma unroll
       for (int j = 0; j < NVA; ++j) {
         const bool ok = sok & ((unsigned)(aq0[j] - t_r) < (unsigned)a.Ho) &
                         ((unsigned)(aq1[j] - t_s) < (unsigned)a.Wo);
         S.a[j] = bload16(ra, sel_off(ok, abase[j] + soff, kOOB16));
-        if constexpr (FOLD) {
-          S.y[j] = bload16(ry, sel_off(ok, abase[j] + soff, kOOB16));
-          S.ok |= (unsigned)ok << j;
-        }
       }
       const int r = a.r0 + a.stride * t_r, s = a.s0 + a.stride * t_s;
       const unsigned woff = (unsigned)(((t_c * a.R + r) * a.S + s) * a.Cin * 2);
@@ -311,9 +269,6 @@ void conv_pipe16(const ConvArgs a) {
       const int idx = tid + NT * j;
       u32x4 v = S.a[j];
       if constexpr (XBN && MODE == FWD) v = bn_relu8<DT>(v, fsc, fsh, rfloor, (S.ok >> j) & 1);
-      if constexpr (FOLD)
-        v = bn_bwd8<DT>(v, S.y[j], a.fcoef, (long long)g * a.Cout + S.tc + EPC * kq,
-                        (long long)a.G * a.Cout, a.frelu, (S.ok >> j) & 1);
       const int off = A_COL ? (idx / (BM / EPC)) * (BM + 32) + EPC * (idx % (BM / EPC))
                             : (idx / KQ) * RLD + EPC * (idx % KQ);
       *(u32x4*)((!PA || idx < LA) ? As + off : dum) = v;
@@ -474,8 +429,7 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
     else pipe16_dt<FWD, false>(dt, a, st);
   } else if (mode == DGRAD) {
     if (a.Cout % 64 || a.Cin % 8) return false;
-    if (a.fy) pipe16_dt<DGRAD, true>(dt, a, st);   // BN backward folded into the A-loader
-    else pipe16_dt<DGRAD, false>(dt, a, st);
+    pipe16_dt<DGRAD, false>(dt, a, st);
   } else {
     if (a.Cout % 8 || a.Cin % 8 || !xs8 || a.kchunk % 64) return false;
     if (a.Wo > 4096 || a.Ho > 4096) return false;

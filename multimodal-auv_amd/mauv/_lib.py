@@ -27,7 +27,7 @@ SIGNATURES = {
     # conv_gemm.hip
     "mauv_conv2d_fwd_f32": [P, P, P, P, I, P, P, P] + [I] * 10 + [P, P, P, P],
     "mauv_conv2d_fwd_stat_blocks": [I] * 10,
-    "mauv_conv2d_bwd_data_f32": [P, P, P, P] + [I] * 11 + [P] * 6 + [I, P, P, P],
+    "mauv_conv2d_bwd_data_f32": [P, P, P, P, P] + [I] * 11 + [P] * 7 + [I, P, P, P],
     "mauv_conv2d_bwd_data_stat_blocks": [I] * 10,
     "mauv_conv2d_wgrad_splits": [I, I, I, I, I, I, I, I, I, I],
     "mauv_conv2d_bwd_weight_f32": [P, P, P, P, I, P, P] + [I] * 11 + [P],
@@ -35,7 +35,7 @@ SIGNATURES = {
     # conv_gemm16.hip
     "mauv_conv2d_fwd_h16": [I, P, P, P, P, I, P, P] + [I] * 10 + [P, P, P, P],
     "mauv_conv2d_bwd_data_h16": [I, P, P, P, P, I] + [I] * 10 + [P],
-    "mauv_conv2d_bwd_data_fold_h16": [I, P, P, P, I, P, P, P, I] + [I] * 10 + [P],
+    "mauv_conv2d_bwd_data_bn_h16": [I, P, P, P, P, I] + [I] * 10 + [P] * 8 + [I, P, P, P],
     "mauv_reparam_sample_ex": [I, P, P, P, ctypes.c_ulonglong, ctypes.c_ulonglong, P, ctypes.c_uint,
                                I, I, I, I, I, P, LL, P],
     "mauv_conv2d_bwd_weight_h16": [I, P, P, P, P, I, P, P, I] + [I] * 10 + [P],
@@ -66,6 +66,7 @@ SIGNATURES = {
     "mauv_maxpool_bn_fwd": [P, P, P, I, I, I, I, I, P, P, P],
     "mauv_bn_apply_mask": [I, P, P, P, P, P, P, P, P, I, LL, I, P],
     "mauv_bn_bwd_mask": [I, P, P, P, P, P, P, I, LL, I, P, P, P, P, P, P],
+    "mauv_bn_bwd_ex": [I, P, P, P, P, I, P, P, P, P, I, LL, I, P, P, P, P, P, P, P, I, P],
     "mauv_avgpool_fwd": [P, I, I, I, P, P],
     "mauv_avgpool_bwd": [P, I, I, I, P, P],
     "mauv_maxpool_fwd_h16": [I, P, I, I, I, I, P, P, P],

@@ -41,6 +41,10 @@ BN_RELU_MASK = os.environ.get("MAUV_BN_RELU_MASK", "1") == "1"
 # The stems as ONE GEMM over im2col rows shared by the G samples, the G weight sets stacked
 # along N (stem.hip), instead of G implicit GEMMs over channel-padded pixels.
 STEM_GEMM = os.environ.get("MAUV_STEM_GEMM", "1") == "1"
+# Training: a block output's residual gradient dres = dout * relu-mask is never written — the
+# conv1 data gradient adds dout where the block output's mask bit is set (identity blocks), the
+# downsample BN's backward reads dout with that mask (MAUV_RES_MASK=0: write dres).
+RES_MASK = os.environ.get("MAUV_RES_MASK", "1") == "1"
 _STREAMS = {}
 
 
@@ -394,7 +398,10 @@ class TrunkRunner(_Runner):
         rec = (conv, x, x_strides, x_bn, w, B, H, W) if self.save else None
         return y, rec, part
 
-    def _conv_bwd(self, rec, dy, need_dx=True, addend=None, dx=None, accumulate=False):
+    def _conv_bwd(self, rec, dy, need_dx=True, addend=None, dx=None, accumulate=False,
+                  addend_mask=None):
+        """Weight gradient (+ reparameterisation backward) and data gradient (+ addend, counted
+        only under addend_mask's ReLU bits when given)."""
         conv, x, xs, x_bn, w, B, H, W = rec
         G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
         st, pd = conv.stride[0], conv.padding[0]
@@ -412,7 +419,7 @@ class TrunkRunner(_Runner):
         if dx is None:
             dx = torch.empty(G, B, H, W, Cin, device=dy.device, dtype=self.dt)
         ops.conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, k, st, pd, addend=addend,
-                            accumulate=accumulate)
+                            accumulate=accumulate, addend_mask=addend_mask)
         return dx
 
     def _stem(self, conv, x, B, H, W):
@@ -493,7 +500,9 @@ class TrunkRunner(_Runner):
         self.last_lazy = (scale, shift, int(relu))  # for a consumer applying it on load
         return out, rec
 
-    def _bn_bwd(self, rec, dout, want_dres=False):
+    def _bn_bwd(self, rec, dout, want_dres=False, mask=None):
+        """mask: ReLU-mask bits applied to dout (a downsample BN fed the block output's
+        dres = dout * mask without that tensor)."""
         if not rec.batch_stats:
             raise NotImplementedError("mauv: backward through eval-mode BN is not on the path "
                                       "(the reference trains and predicts in .train())")
@@ -504,7 +513,10 @@ class TrunkRunner(_Runner):
         dg = bn.weight.grad if bn.weight.requires_grad else None
         db = bn.bias.grad if bn.bias.requires_grad else None
         s = rec.stats
-        if rec.mask is not None:
+        if mask is not None:
+            ops.bn_bwd_ex(rec.y, None, mask, dout, 1, s[0], s[1], s[2], s[3], G, M, C, ws, dy,
+                          dres, dg, db)
+        elif rec.mask is not None:
             ops.bn_bwd_mask(rec.y, rec.mask, dout, s[0], s[1], s[2], G, M, C, ws, dy, dres, dg, db)
         else:
             ops.bn_bwd(rec.y, rec.out, dout, rec.relu, s[0], s[1], s[2], G, M, C, ws, dy, dres,
@@ -608,7 +620,13 @@ class TrunkRunner(_Runner):
         del dfeat
         while self.recs:
             r1, s1, r2, s2, r3, s3, rd, sd = self.recs.pop()
-            dy3, dres = self._bn_bwd(s3, da, want_dres=True)
+            # the residual gradient: dres = da * mask3, kept implicit when bn3 has mask bits
+            rmask = s3.mask if RES_MASK and s3.mask is not None and \
+                (rd is not None or self.dt == torch.float32 or r1[0].out_channels % 64 == 0) \
+                else None
+            dy3, dres = self._bn_bwd(s3, da, want_dres=rmask is None)
+            if rmask is not None:
+                dres = da
             del da, s3
             da2 = self._conv_bwd(r3, dy3)
             del dy3, r3
@@ -619,13 +637,13 @@ class TrunkRunner(_Runner):
             dy1, _ = self._bn_bwd(s1, da1)
             del da1, s1
             if rd is not None:
-                dyd, _ = self._bn_bwd(sd, dres)
+                dyd, _ = self._bn_bwd(sd, dres, mask=rmask)
                 del dres, sd
                 dx = self._conv_bwd(r1, dy1)
                 self._conv_bwd(rd, dyd, dx=dx, accumulate=True)
                 del dyd, rd
             else:
-                dx = self._conv_bwd(r1, dy1, addend=dres)
+                dx = self._conv_bwd(r1, dy1, addend=dres, addend_mask=rmask)
                 del dres
             del dy1, r1
             da = dx

@@ -146,9 +146,15 @@ def dgrad_stat_blocks(G, B, H, W, Cin, Cout, R, stride, pad):
 
 
 def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=None,
-                    accumulate=False, bn=None):
-    """bn = dict(y, out|None, scale, shift, mean, invstd, relu, p1, p2): dx is the output
-    gradient of that BatchNorm; the epilogue writes its backward partial sums into p1/p2."""
+                    accumulate=False, bn=None, addend_mask=None):
+    """bn = dict(y, out|None, mask|None, scale, shift, mean, invstd, relu, p1, p2): dx is the
+    output gradient of that BatchNorm; the epilogue writes its backward partial sums into p1/p2.
+    addend_mask (uint8 ReLU-mask bits of dx's shape, bn_apply_mask): the addend counts only
+    where the bit is set (a block output's residual gradient without a dres tensor)."""
+    if addend_mask is not None:
+        _dev(torch.uint8, addend_mask)
+        if addend is None or addend_mask.numel() * 8 != dx.numel():
+            raise ValueError("conv2d_bwd_data: addend_mask needs an addend and dx.numel()/8 bytes")
     Ho, Wo = out_hw(H, R, stride, pad), out_hw(W, R, stride, pad)
     b = bn or {}
     fl = 2.0 * G * B * Ho * Wo * Cout * R * R * Cin
@@ -157,37 +163,36 @@ def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=Non
     nl = sum(1 for ph in range(stride) for pw in range(stride)
              if (H - ph + stride - 1) // stride > 0 and (W - pw + stride - 1) // stride > 0)
     if w.dtype in H16:
-        assert bn is None, "16-bit dgrad has no BN-partials epilogue"
-        _h16(w.dtype, dy, w, dx, addend)
+        _h16(w.dtype, dy, w, dx, addend, b.get("y"), b.get("out"))
+        _f32(b.get("scale"), b.get("shift"), b.get("mean"), b.get("invstd"), b.get("p1"),
+             b.get("p2"))
+        mk = b.get("mask")
+        if mk is not None:
+            _dev(torch.uint8, mk)
+        if bn is not None:      # + reads y (and out / mask bits) beside each dx chunk
+            nb += w.element_size() * G * B * H * W * Cin * (1 + (b.get("out") is not None))
         with _Prof("dgrad_" + str(w.dtype)[6:], fl, nb, nl):
-            check(lib.mauv_conv2d_bwd_data_h16(H16[w.dtype], _p(dy), _p(w), _p(dx), _p(addend),
-                                               int(accumulate), G, B, H, W, Cin, Cout, R, R,
-                                               stride, pad, stream()), "conv2d_bwd_data_h16")
+            check(lib.mauv_conv2d_bwd_data_bn_h16(
+                H16[w.dtype], _p(dy), _p(w), _p(dx), _p(addend), int(accumulate), G, B, H, W,
+                Cin, Cout, R, R, stride, pad, _p(addend_mask), _p(b.get("y")), _p(b.get("out")),
+                _p(mk),
+                _p(b.get("scale")), _p(b.get("shift")), _p(b.get("mean")), _p(b.get("invstd")),
+                int(b.get("relu", 0)), _p(b.get("p1")), _p(b.get("p2")), stream()),
+                "conv2d_bwd_data_h16")
         return
-    _f32(dy, w, dx, addend)
+    _f32(dy, w, dx, addend, b.get("y"), b.get("out"), b.get("scale"), b.get("shift"),
+         b.get("mean"), b.get("invstd"), b.get("p1"), b.get("p2"))
+    if b.get("mask") is not None:
+        _dev(torch.uint8, b["mask"])
+    if bn is not None:
+        nb += 4 * G * B * H * W * Cin * (1 + (b.get("out") is not None))
     with _Prof("dgrad", fl, nb, nl):
         check(lib.mauv_conv2d_bwd_data_f32(
-            _p(dy), _p(w), _p(dx), _p(addend), int(accumulate), G, B, H, W, Cin, Cout, R, R,
-            stride, pad, _p(b.get("y")), _p(b.get("out")), _p(b.get("scale")),
+            _p(dy), _p(w), _p(dx), _p(addend), _p(addend_mask), int(accumulate), G, B, H, W,
+            Cin, Cout, R, R,
+            stride, pad, _p(b.get("y")), _p(b.get("out")), _p(b.get("mask")), _p(b.get("scale")),
             _p(b.get("shift")), _p(b.get("mean")), _p(b.get("invstd")), int(b.get("relu", 0)),
             _p(b.get("p1")), _p(b.get("p2")), stream()), "conv2d_bwd_data")
-
-
-def conv2d_bwd_data_fold(dout, y, coef, relu, w, dx, G, B, H, W, Cin, Cout, R, stride, pad,
-                         addend=None, accumulate=False):
-    """16-bit prototype: conv2d_bwd_data of dy = alpha*dz + beta*y + gamma computed in the
-    A-loader from the BN's (y, dout); coef fp32 [5][G][Cout] (alpha, beta, gamma, sc, sh)."""
-    _h16(w.dtype, dout, y, w, dx, addend)
-    _f32(coef)
-    Ho = out_hw(H, R, stride, pad)
-    fl = 2.0 * G * B * Ho * Ho * Cout * R * R * Cin
-    nb = w.element_size() * (2 * G * B * Ho * Ho * Cout + G * Cout * R * R * Cin +
-                             G * B * H * W * Cin * (1 + (addend is not None) + bool(accumulate)))
-    with _Prof("dgrad_" + str(w.dtype)[6:], fl, nb):
-        check(lib.mauv_conv2d_bwd_data_fold_h16(H16[w.dtype], _p(dout), _p(y), _p(coef), int(relu),
-                                                _p(w), _p(dx), _p(addend), int(accumulate), G, B,
-                                                H, W, Cin, Cout, R, R, stride, pad, stream()),
-              "conv2d_bwd_data_fold_h16")
 
 
 def wgrad_splits(G, B, H, W, Cin, Cout, R, stride, pad):
@@ -343,6 +348,29 @@ def bn_bwd(y, out, dout, relu, mean, invstd, scale, G, M, C, ws, dy, dres=None, 
     check(lib.mauv_bn_bwd(_p(y), _p(out), _p(dout), int(relu), _p(mean), _p(invstd), _p(scale),
                           _p(shift), G, M, C, _p(ws), _p(dy), _p(dres), _p(dgamma), _p(dbeta),
                           _p(p1), _p(p2), nb, stream()), "bn_bwd")
+
+
+def bn_bwd_ex(y, out, mask, dout, relu, mean, invstd, scale, shift, G, M, C, ws, dy,
+              dres=None, dgamma=None, dbeta=None, pre=None):
+    """Every BN-backward form in one call: ReLU mask from `mask` bits (bn_apply_mask), else
+    `out`, else y*scale+shift; pre = (p1, p2, nblk) partials a data-gradient epilogue wrote
+    (conv2d_bwd_data(..., bn=...)) — the partial pass is skipped."""
+    if y.dtype in H16:
+        _h16(y.dtype, y, out, dout, dy, dres)
+    else:
+        _f32(y, out, dout, dy, dres)
+    _f32(mean, invstd, scale, shift, ws, dgamma, dbeta)
+    if mask is not None:
+        _dev(torch.uint8, mask)
+        if mask.numel() * 8 != G * M * C:
+            raise ValueError("bn_bwd_ex: mask size does not match (G, M, C)")
+    p1, p2, nb = pre if pre is not None else (None, None, 0)
+    if pre is not None:
+        _f32(p1, p2)
+    check(lib.mauv_bn_bwd_ex(_dt_code(y), _p(y), _p(out), _p(mask), _p(dout), int(relu),
+                             _p(mean), _p(invstd), _p(scale), _p(shift), G, M, C, _p(ws), _p(dy),
+                             _p(dres), _p(dgamma), _p(dbeta), _p(p1), _p(p2), nb, stream()),
+          "bn_bwd_ex")
 
 
 def _dt_code(t):

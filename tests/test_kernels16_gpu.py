@@ -265,37 +265,84 @@ def test_reparam16_padded_sample_and_bwd(dt):
 
 
 
-@pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
-@pytest.mark.parametrize("case", [(2, 2, 8, 64, 64, 3, 1, 1), (1, 3, 9, 128, 128, 3, 2, 1),
-                                  (2, 2, 6, 256, 64, 1, 1, 0)])
-def test_conv16_dgrad_bn_fold_prototype(case, dt):
-    """The BN-backward-fold prototype: the data gradient with dy = alpha*dz +
-    beta*y + gamma computed in the A-loader equals the data gradient of the materialised
-    16-bit dy of the same BN backward (ReLU mask from y*sc+sh) within the 16-bit rounding of dy."""
+@pytest.mark.parametrize("dt", DTYPES + [torch.float32], ids=["bf16", "f16", "fp32"])
+@pytest.mark.parametrize("case,src,res", [
+    ((2, 2, 8, 64, 64, 3, 1, 1), "lazy", False),       # bn1/bn2 of a block: mask from y*sc+sh
+    ((1, 3, 9, 128, 128, 3, 2, 1), "lazy", False),     # strided: four parity classes, ragged
+    ((2, 3, 9, 256, 64, 1, 1, 0), "mask", True),       # block output: mask bits + residual addend
+    ((2, 2, 15, 64, 128, 3, 2, 1), "out", False),      # BN 64-wide column tiles, odd extents
+    ((1, 2, 4, 512, 2048, 1, 1, 0), "none", True),     # no ReLU (the downsample's BN), BM = 64
+    ((1, 8, 136, 64, 64, 1, 1, 0), "mask", True),      # 1,156 partials per channel: the
+                                                       # segmented finalize (bn_bwd_seg)
+])
+def test_conv16_dgrad_bn_partials_epilogue(case, src, res, dt):
+    """The data gradient's epilogue writes the BN-backward partials of the BN whose output
+    gradient dx is (conv2d_bwd_data(..., bn=...); 16-bit: conv_epi16.h, fp32: the split
+    kernel's direct-store epilogue): dx bit-identical to the plain data gradient;
+    the BN backward finished from those partials (bn_bwd_ex(pre=...)) matches the standalone
+    partial pass within fp32 summation order, and both match float64 on the same 16-bit dx."""
     from mauv import ops
     G, B, H, Cin, Cout, R, st, pad = case
-    torch.manual_seed(3)
+    torch.manual_seed(5)
     Ho = ops.out_hw(H, R, st, pad)
-    M = B * Ho * Ho
-    y = torch.randn(G, B, Ho, Ho, Cout).to(dt)
-    dout = torch.randn(G, B, Ho, Ho, Cout).to(dt)
-    w = (torch.randn(G, Cout, R, R, Cin) / math.sqrt(Cin * R * R)).to(dt)
-    mean = torch.randn(G, Cout) * 0.1
-    invstd = torch.rand(G, Cout) + 0.5
-    sc = torch.rand(G, Cout) + 0.5
-    sh = torch.randn(G, Cout) * 0.1
-    yd, dd = y.double().view(G, M, Cout), dout.double().view(G, M, Cout)
-    dz = dd * ((yd * sc.double()[:, None] + sh.double()[:, None]) > 0)
+    C, M = Cin, B * H * H
+    dyc = (torch.randn(G, B, Ho, Ho, Cout) * 0.5).to(dt).to(dev)
+    w = (torch.randn(G, Cout, R, R, Cin) / math.sqrt(Cin * R * R)).to(dt).to(dev)
+    y = torch.randn(G, B, H, H, C).to(dt).to(dev)
+    mean = (torch.randn(G, C) * 0.1).to(dev)
+    invstd = (torch.rand(G, C) + 0.5).to(dev)
+    sc = (torch.rand(G, C) + 0.5).to(dev)
+    sh = (torch.randn(G, C) * 0.1).to(dev)
+    addend = torch.randn(G, B, H, H, C).to(dt).to(dev) if res else None
+    relu = src != "none"
+    out = mask = None
+    if src in ("out", "mask"):
+        out = torch.empty_like(y)
+        mask = torch.empty(G * M * C // 8, dtype=torch.uint8, device=dev)
+        ops.bn_apply_mask(y, sc, sh, None, out, mask, G, M, C)
+        if src == "mask":
+            out = None
+        else:
+            mask = None
+    dx_plain = torch.empty(G, B, H, H, C, device=dev, dtype=dt)
+    ops.conv2d_bwd_data(dyc, w, dx_plain, G, B, H, H, Cin, Cout, R, st, pad, addend=addend)
+    nblk = ops.dgrad_stat_blocks(G, B, H, H, Cin, Cout, R, st, pad)
+    p1 = torch.full((G, nblk, C), float("nan"), device=dev)
+    p2 = torch.full((G, nblk, C), float("nan"), device=dev)
+    dx = torch.empty_like(dx_plain)
+    bn = dict(y=y, out=out, mask=mask, scale=sc, shift=sh, mean=mean, invstd=invstd, relu=relu,
+              p1=p1, p2=p2)
+    ops.conv2d_bwd_data(dyc, w, dx, G, B, H, H, Cin, Cout, R, st, pad, addend=addend, bn=bn)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx_plain)
+    assert torch.isfinite(p1).all() and torch.isfinite(p2).all()    # every block written
+    ws = torch.empty(ops.bn_workspace_floats(G, M, C), device=dev)
+    res_ = {}
+    for key, pre in (("epi", (p1, p2, nblk)), ("pass", None)):
+        dyo = torch.empty_like(y)
+        dg = torch.zeros(C, device=dev)
+        db = torch.zeros(C, device=dev)
+        ops.bn_bwd_ex(y, out, mask, dx, relu, mean, invstd, sc, sh, G, M, C, ws, dyo,
+                      dgamma=dg, dbeta=db, pre=pre)
+        res_[key] = (dyo, dg, db)
+    # float64 truth on the same 16-bit dx
+    yd, dd = y.double().view(G, M, C), dx.double().view(G, M, C)
+    if relu:
+        pre_act = (out.double().view(G, M, C) if out is not None else
+                   (y.double().view(G, M, C) * sc.double()[:, None] + sh.double()[:, None]))
+        if mask is not None:     # the bits are of the stored (rounded) output
+            o16 = torch.empty_like(y)
+            ops.bn_apply(y, sc, sh, None, True, o16, G, M, C)
+            pre_act = o16.double().view(G, M, C)
+        dz = dd * (pre_act > 0)
+    else:
+        dz = dd
     xh = (yd - mean.double()[:, None]) * invstd.double()[:, None]
-    k1, k2 = dz.mean(1), (dz * xh).mean(1)
-    dy = (sc.double()[:, None] * (dz - k1[:, None] - xh * k2[:, None])).to(dt)
-    coef = torch.stack([sc.double(), -sc.double() * invstd.double() * k2,
-                        sc.double() * (invstd.double() * k2 * mean.double() - k1), sc.double(),
-                        sh.double()]).float()
-    dx_ref = torch.empty(G, B, H, H, Cin, device=dev, dtype=dt)
-    ops.conv2d_bwd_data(dy.view(G, B, Ho, Ho, Cout).to(dev), w.to(dev), dx_ref, G, B, H, H, Cin,
-                        Cout, R, st, pad)
-    dx = torch.empty_like(dx_ref)
-    ops.conv2d_bwd_data_fold(dout.to(dev), y.to(dev), coef.to(dev).contiguous(), 1, w.to(dev), dx,
-                             G, B, H, H, Cin, Cout, R, st, pad)
-    close(dx, dx_ref, 8 * ULP[dt])
+    dbeta_t, dgamma_t = dz.sum((0, 1)), (dz * xh).sum((0, 1))
+    for key in ("epi", "pass"):
+        dyo, dg, db = res_[key]
+        close(db, dbeta_t, 1e-4, 1e-3)
+        close(dg, dgamma_t, 1e-4, 1e-3)
+    close(res_["epi"][0], res_["pass"][0], 2 * ULP.get(dt, 2.0 ** -20))
+    close(res_["epi"][1], res_["pass"][1], 1e-5, 1e-4)
+    close(res_["epi"][2], res_["pass"][2], 1e-5, 1e-4)
