@@ -420,6 +420,32 @@ def test_reparam_and_kl():
         assert torch.equal(o1[0], outb[g])
 
 
+@pytest.mark.parametrize("G,Cout,Cin,R,fixed", [(11, 24, 20, 3, -1), (11, 8, 70, 1, -1),
+                                                  (5, 24, 20, 3, 2), (12, 16, 64, 3, -1)])
+def test_reparam_bwd_sample_batches(G, Cout, Cin, R, fixed):
+    """reparam_bwd with more MC samples than one LDS batch (RB_GC = 8): the per-sample terms
+    are added in sample order onto nonzero accumulated gradients; ragged channel blocks
+    (Cin % 16, Cin % 64), 1x1 and 3x3, and bayesian-torch's fixed-sample mode."""
+    from mauv import ops
+    torch.manual_seed(9)
+    splits = 3
+    mu = torch.randn(Cout, Cin, R, R) * 0.1
+    rho = torch.randn(Cout, Cin, R, R) - 3
+    eps = torch.randn(G, Cout * Cin * R * R)
+    dws = torch.randn(splits, G, Cout, R, R, Cin)
+    dmu0 = torch.randn(Cout, Cin, R, R)
+    drho0 = torch.randn(Cout, Cin, R, R)
+    dmu, drho = dmu0.clone().to(dev), drho0.clone().to(dev)
+    ops.reparam_bwd(dws.to(dev), splits, mu.to(dev), rho.to(dev), dmu, drho, G, 0, 0, 0, Cout,
+                    Cin, R * R, eps=eps.to(dev), fixed_sample=fixed)
+    dW = dws.double().sum(0).permute(0, 1, 4, 2, 3)  # [G][Cout][Cin][R][R]
+    e = eps.double().view(G, Cout, Cin, R, R)
+    if fixed >= 0:
+        e = e[fixed].expand_as(e)
+    close(dmu, dmu0.double() + dW.sum(0))
+    close(drho, drho0.double() + (dW * e).sum(0) * torch.sigmoid(rho.double()))
+
+
 def test_philox_matches_oracle_restatement():
     from mauv import ops
     from oracle.philox_ref import philox4x32_10, normal4
