@@ -21,5 +21,5 @@ MAUV_TRUNK_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output
 MAUV_TRUNK_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/e_st16 -o run -- python3 bench.py --dtype bf16 --steps 2 --warmup 1 $C --no-infer --no-bf16 > gpurun_out/e_st16.log 2>&1 || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/e_stinf -o run -- python3 bench.py --steps 1 --warmup 0 $C --no-bf16 --no-infer-fp32 > gpurun_out/e_stinf.log 2>&1 || exit 1
 echo done
-bash tools/gpubatch_s3traffic.sh > gpurun_out/e_shape_traffic.txt 2>&1 || exit 1
+bash tools/batches/gpubatch_s3traffic.sh > gpurun_out/e_shape_traffic.txt 2>&1 || exit 1
 grep TOTAL gpurun_out/e_shape_traffic.txt
