@@ -20,4 +20,7 @@ python3 -c "import json;d=json.load(open('gpurun_out/round3_bench.json'));print(
 C="--no-cpu-baseline --exact-steps 0 --no-roofline --no-sweep --no-infer --no-bf16"
 MAUV_TRUNK_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3_st32 -o run -- python3 bench.py --steps 2 --warmup 1 $C > gpurun_out/r3_st32.log 2>&1 || exit 1
 MAUV_TRUNK_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3_st16 -o run -- python3 bench.py --dtype bf16 --steps 2 --warmup 1 $C > gpurun_out/r3_st16.log 2>&1 || exit 1
+
+timeout -k 10 300 python -u tools/conv_bench.py --dtype bf16 --fused --top 80 > gpurun_out/r3_convbench_bf16.txt 2>&1 || exit 1
+tail -4 gpurun_out/r3_convbench_bf16.txt
 echo done

@@ -53,7 +53,10 @@ def main(fetch_dir, write_dir, out_json, fam=None):
         a[3] += v * 1024.0
     rows = {k: {"launches": v[0], "read_bytes": v[2], "write_bytes": v[3],
                 "bytes_per_launch": (v[2] + v[3]) / max(v[0], 1)} for k, v in agg.items()}
-    fam = fam or ("conv_f32" if "conv_f32" in rows else "conv_h16")
+    # the conv family of the profiled step: the one with more launches (a 16-bit step also runs
+    # the fusion head's fp32 linears on the split kernel)
+    fam = fam or max((k for k in ("conv_f32", "conv_h16") if k in rows),
+                     key=lambda k: rows[k]["launches"])
     conv = rows[fam]
     res = {"kernel": {"conv_f32": "conv_f32 (conv_split_f32 + stem conv_gemm_f32)",
                       "conv_h16": "conv_h16 (conv_pipe16 + conv_gemm_h16)"}[fam],
