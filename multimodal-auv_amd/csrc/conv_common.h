@@ -93,6 +93,8 @@ __device__ __forceinline__ void conv_block_tile(const ConvArgs& a, int& m0, int&
 
 // MAUV_XCD_GRID (default 1): conv_block_tile's order
 int conv_xcd_grid();
+// MAUV_DGRAD_SHORT (default 1): short-K kernels for the data gradients (conv_pipe16.hip)
+int dgrad_short();
 
 // output element (row, col) of a FWD/DGRAD epilogue, relative to the block's group base
 __device__ __forceinline__ long long conv_out_index(const ConvArgs& a, long long orow, int col) {
@@ -169,7 +171,7 @@ __device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int
 // lane l = column l&31, register r = row (r&3) + 8(r>>2) + 4(l>>5)).
 // WGM x WGN waves (wave = wm * WGN + wn).  BN statistics partials are per SR = min(BM, 128)
 // rows (the conv_tile_rows granularity the host sizes them with), so a 256-row tile writes two.
-template <int MODE, int BM, int BN, int MI, int NI, int WGM = 2, int WGN = 2>
+template <int MODE, int BM, int BN, int MI, int NI, int WGM = 2, int WGN = 2, bool BP = true>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx16 (&acc)[MI][NI],
                                               float* smem, int tid, int m0, int n0, int g,
                                               int sp) {
@@ -191,7 +193,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, floatx16 (&acc)
   //   DGRAD + bp_p1  : sum dz and sum dz*xhat of the BN whose output gradient this dx is
   //                    (dz = dx * relu-mask; mask/xhat from that BN's y and statistics)
   const bool fst = (MODE == FWD) && a.st_mean;
-  const bool bst = (MODE == DGRAD) && a.bp_p1;
+  const bool bst = (MODE == DGRAD) && BP && a.bp_p1;  // BP = false: compiled out
   float s1[NI], s2[NI];
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) { s1[ni] = 0.f; s2[ni] = 0.f; }

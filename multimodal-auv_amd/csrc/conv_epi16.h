@@ -50,7 +50,8 @@ __device__ __forceinline__ u32x4 bn_relu8(u32x4 v, const floatx8& sc, const floa
   return o;
 }
 
-template <int MODE, int DT, int BM, int BN, int MI, int NI, int WGM, int WGN, int SCRATCH>
+template <int MODE, int DT, int BM, int BN, int MI, int NI, int WGM, int WGN, int SCRATCH,
+          bool BP = false>
 __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI][NI], void* smem,
                                            int m0, int n0, int g) {
   constexpr int NT = 64 * WGM * WGN, WM = BM / WGM, WN = BN / WGN;
@@ -135,7 +136,9 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
   // sums dz = dx * relu-mask and dz * xhat per column (bn_bwd_partial's two sums, bn.hip), from
   // the ROUNDED 16-bit dx the apply pass will read, with y / the mask read as 16-byte chunks
   // beside the store — one per-(m-tile, column) partial instead of a pass over y and dx
-  const bool bst = MODE == DGRAD && a.bp_p1;
+  // (BP: the instantiation that carries this path; the plain data gradients compile it out,
+  // which keeps them within the short-K kernels' register budget)
+  const bool bst = MODE == DGRAD && BP && a.bp_p1;
   const int bcol = n0 + 8 * (tid % CPR);
   floatx8 b1 = {}, b2 = {}, bmu = {}, bis = {}, bsc = {}, bsh = {};
   if (bst && bcol < a.N) {

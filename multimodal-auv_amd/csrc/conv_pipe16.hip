@@ -65,7 +65,7 @@ struct Waves16 {
 // overlap inside a block, so more resident blocks are the cover for load and store latency
 // SHORT: 0 = the two-stage pipeline; 1 = exactly one stage (nt == 1, straight-line: 62 VGPRs,
 // up to four blocks per CU); 2 = short K through one buffer, stages one after another.
-template <int MODE, int DT, int BM, int BN, bool XBN, bool STEM, int SHORT = 0>
+template <int MODE, int DT, int BM, int BN, bool XBN, bool STEM, int SHORT = 0, bool BP = false>
 __global__ __launch_bounds__((Waves16<BM, BN>::T))
 __attribute__((amdgpu_waves_per_eu(SHORT ? 6 : Waves16<BM, BN>::EU)))
 void conv_pipe16(const ConvArgs a) {
@@ -364,14 +364,15 @@ void conv_pipe16(const ConvArgs a) {
     conv_epilogue<WGRAD, BM, BN, MI, NI, WGM, WGN>(a, acc, (float*)smem, tid, m0, n0, g, sp);
     return;
   }
-  epilogue16<MODE, DT, BM, BN, MI, NI, WGM, WGN, NBUF * STG * 2>(a, acc, smem, m0, n0, g);
+  epilogue16<MODE, DT, BM, BN, MI, NI, WGM, WGN, NBUF * STG * 2, BP>(a, acc, smem, m0, n0, g);
 }
 
-template <int MODE, int DT, int BM, int BN, bool XBN, bool STEM = false, int SHORT = 0>
+template <int MODE, int DT, int BM, int BN, bool XBN, bool STEM = false, int SHORT = 0,
+          bool BP = false>
 static void launch_pipe16(const ConvArgs& a, hipStream_t st) {
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
-  hipLaunchKernelGGL((conv_pipe16<MODE, DT, BM, BN, XBN, STEM, SHORT>), grid, dim3(Waves16<BM, BN>::T), 0, st,
-                     a);
+  hipLaunchKernelGGL((conv_pipe16<MODE, DT, BM, BN, XBN, STEM, SHORT, BP>), grid,
+                     dim3(Waves16<BM, BN>::T), 0, st, a);
 }
 
 // forward launches with K <= MAUV_P16_SHORT_K (default 256; 0 = off) take the short-K kernels
@@ -384,18 +385,36 @@ static int short_k() {
 }
 
 
+// data-gradient launches take the short-K kernels when MAUV_DGRAD_SHORT is not 0 (default 1;
+// both conv families)
+int dgrad_short() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("MAUV_DGRAD_SHORT"); v = e ? atoi(e) : 1; }
+  return v;
+}
+
 template <int MODE, int DT, bool XBN, bool STEM>
 static void pipe16_tiles(const ConvArgs& a, hipStream_t st) {
-  // short-K kernels: the forward only (the same variants for the data gradient, K = the
-  // parity class's taps x Cout, measured neutral on the bf16 step: 569-586 vs 577-581)
-  constexpr bool SHORT_OK = MODE == FWD && !STEM;
   const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
+  if constexpr (MODE == DGRAD) {
+    if (a.bp_p1) {  // BN-backward partials from the epilogue (mauv_conv2d_bwd_data_bn_h16)
+      if (bm == 64 && bn == 64) launch_pipe16<MODE, DT, 64, 64, XBN, STEM, 0, true>(a, st);
+      else if (bm == 64) launch_pipe16<MODE, DT, 64, 128, XBN, STEM, 0, true>(a, st);
+      else if (bn == 64) launch_pipe16<MODE, DT, 128, 64, XBN, STEM, 0, true>(a, st);
+      else launch_pipe16<MODE, DT, 128, 128, XBN, STEM, 0, true>(a, st);
+      return;
+    }
+  }
+  // short-K kernels: forwards, and data gradients without the BN-partials epilogue (K = the
+  // parity class's taps x Cout)
+  constexpr bool SHORT_OK = (MODE == FWD || MODE == DGRAD) && !STEM;
+  const bool use = MODE == FWD || dgrad_short();
   if (bm == 64 && bn == 64) launch_pipe16<MODE, DT, 64, 64, XBN, STEM>(a, st);
   else if (bm == 64) launch_pipe16<MODE, DT, 64, 128, XBN, STEM>(a, st);
   else if (bn == 64) launch_pipe16<MODE, DT, 128, 64, XBN, STEM>(a, st);
-  else if (SHORT_OK && a.K == 64 && short_k() >= 64)
+  else if (SHORT_OK && use && a.K == 64 && short_k() >= 64)
     launch_pipe16<MODE, DT, 128, 128, XBN, STEM, SHORT_OK ? 1 : 0>(a, st);
-  else if (SHORT_OK && a.K > 0 && a.K <= short_k())
+  else if (SHORT_OK && use && a.K > 0 && a.K <= short_k())
     launch_pipe16<MODE, DT, 128, 128, XBN, STEM, SHORT_OK ? 2 : 0>(a, st);
   else launch_pipe16<MODE, DT, 128, 128, XBN, STEM>(a, st);
 }

@@ -81,7 +81,7 @@ __device__ __forceinline__ int row_of(int idx) {
 // stages one after another, a register budget for three blocks per CU instead of two (the
 // 16-bit kernel's short-K variant, conv_pipe16.hip)
 template <int MODE, int BM, int BN, bool XBN, bool ONEACC, int WV, bool STEM = false,
-          bool SEQ = false>
+          bool SEQ = false, bool BP = false>
 __global__ __launch_bounds__((SplitWaves<BM, BN, WV>::T))
 __attribute__((amdgpu_waves_per_eu(SEQ ? 6 : SplitWaves<BM, BN, WV>::EU)))
 void conv_split_f32(const ConvArgs a) {
@@ -398,21 +398,24 @@ void conv_split_f32(const ConvArgs a) {
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) acc[mi][ni] += acl[mi][ni];
   }
-  conv_epilogue<MODE, BM, BN, MI, NI, WGM, WGN>(a, acc, (float*)smem, tid, m0, n0, g, sp);
+  conv_epilogue<MODE, BM, BN, MI, NI, WGM, WGN, BP>(a, acc, (float*)smem, tid, m0, n0, g, sp);
 }
 
-template <int MODE, int BM, int BN, bool XBN, int WV = 4, bool STEM = false, bool SEQ = false>
+template <int MODE, int BM, int BN, bool XBN, int WV = 4, bool STEM = false, bool SEQ = false,
+          bool BP = false>
 static void launch_split(const ConvArgs& a, int oneacc, hipStream_t st) {
   dim3 grid(ceil_div(a.M, BM) * ceil_div(a.N, BN), MODE == WGRAD ? a.G * a.splits : a.G);
   const dim3 block(SplitWaves<BM, BN, WV>::T);
   if constexpr (WV == 8) {  // one accumulator set (128-VGPR budget)
-    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV, STEM, SEQ>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV, STEM, SEQ, BP>), grid, block, 0, st,
+                       a);
   } else {
     if (oneacc)
-      hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV, STEM>), grid, block, 0, st, a);
+      hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, true, WV, STEM, false, BP>), grid, block,
+                         0, st, a);
     else
-      hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, false, WV, STEM>), grid, block, 0, st,
-                         a);
+      hipLaunchKernelGGL((conv_split_f32<MODE, BM, BN, XBN, false, WV, STEM, false, BP>), grid,
+                         block, 0, st, a);
   }
 }
 
@@ -432,13 +435,23 @@ static int split_short_k() {
 template <int MODE, bool XBN>
 static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
   const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
+  if constexpr (MODE == DGRAD) {
+    if (a.bp_p1) {  // BN-backward partials from the epilogue (the bn_p1 arguments of the C-ABI)
+      if (bm == 128 && bn == 128) launch_split<MODE, 128, 128, XBN, 8, false, false, true>(a, oneacc, st);
+      else if (bm == 128 && bn == 64) launch_split<MODE, 128, 64, XBN, 8, false, false, true>(a, oneacc, st);
+      else if (bm == 64 && bn == 128) launch_split<MODE, 64, 128, XBN, 8, false, false, true>(a, oneacc, st);
+      else launch_split<MODE, 64, 64, XBN, 4, false, false, true>(a, oneacc, st);
+      return;
+    }
+  }
   // eight-wave blocks (four waves per SIMD): 128 x 128 tiles as waves of 32 x 64, 128 x 64 and
   // 64 x 128 as waves of 32 x 32 — measured 200 vs 235 ms of convs per bench step over four
   // waves.  256-wide tiles (225 vs 229 ms of convs per step against two co-resident 128 x 128
-  // blocks) and a short-K data-gradient variant (neutral) were measured and
-  // removed.
-  if constexpr (MODE == FWD) {
-    if (bm == 128 && bn == 128 && a.K <= split_short_k()) {
+  // blocks) were measured and removed.  The short-K (SEQ) kernel serves the forwards and the
+  // data gradients without the BN-partials epilogue (MAUV_DGRAD_SHORT=0: forwards only).
+  if constexpr (MODE == FWD || MODE == DGRAD) {
+    if (bm == 128 && bn == 128 && a.K > 0 && a.K <= split_short_k() &&
+        (MODE == FWD || dgrad_short())) {
       launch_split<MODE, 128, 128, XBN, 8, false, true>(a, oneacc, st);
       return;
     }

@@ -49,7 +49,8 @@ CASES = [
                                     # the one-stage forward kernel
     (2, 3, 9, 128, 256, 1, 1, 0),   # K = 128 / 256: the short-K sequential forward kernel
     (1, 3, 10, 256, 256, 1, 1, 0),
-    (2, 3, 9, 128, 64, 1, 1, 0),    # dgrad over a single 64-deep stage
+    (2, 3, 9, 128, 64, 1, 1, 0),    # dgrad over a single 64-deep stage: the one-stage kernel
+    (2, 3, 9, 256, 128, 1, 1, 0),   # dgrad K = 128: the short-K sequential data gradient
 ]
 
 

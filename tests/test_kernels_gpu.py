@@ -30,7 +30,8 @@ CONV_CASES = [
     (2, 2, 4, 512, 2048, 1, 1, 0),
     (3, 2, 5, 64, 256, 1, 1, 0),
     (2, 3, 9, 64, 256, 1, 1, 0),     # 1x1 forwards with K <= 256 on 128 x 128 tiles: the
-    (1, 3, 10, 256, 128, 1, 1, 0),   # split kernel's short-K (SEQ) variant
+    (1, 3, 10, 256, 128, 1, 1, 0),   # split kernel's short-K (SEQ) variant (dgrad: K = 128)
+    (2, 3, 9, 128, 64, 1, 1, 0),     # SEQ data gradient over K = 64
 ]
 
 
