@@ -94,6 +94,12 @@ int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strides, const
  * mode -1 queries.  Returns the previous mode, or < 0 for an invalid mode. */
 int mauv_set_f32_math(int mode);
 
+/* 3x3 / stride-1 / pad-1 16-bit forwards over 64 -> 64 channels (every bottleneck's layer-1
+ * conv2) through an LDS image of the input rows each block's pixels touch (conv_halo16.hip;
+ * bit-identical to the implicit GEMM): 1 (default, or MAUV_HALO3=0 at load) routes them there,
+ * 0 to the implicit GEMM, -1 queries.  Returns the previous setting. */
+int mauv_set_halo3(int on);
+
 /* ---- 16-bit implicit-GEMM convs (conv_gemm16.hip) -----------------------------------------
  * Same three GEMM views on v_mfma_f32_32x32x16_{bf16,f16}: dtype 0 = bf16 (BASELINE configs[2]
  * training), 1 = f16 (the reference predictor's torch.amp.autocast on a GPU,

@@ -59,8 +59,13 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
   const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
   float* red = (float*)smem;  // LDS is free: the main loop ended with a barrier
   if (MODE == FWD && a.st_mean) {
-    // per-tile BN statistics of y from the fp32 accumulators (tile mean, then M2 around it)
-    const int nvalid = min(BM, a.M - m0);
+    // per-tile BN statistics of y from the fp32 accumulators (tile mean, then M2 around it),
+    // one partial per SR = min(BM, 128) rows (the granularity the host sizes them with): a
+    // 256-row tile (conv_halo16.hip) writes two, from the waves wm / WPS of each half
+    constexpr int SR = BM > 128 ? 128 : BM, SUB = BM / SR, WPS = WGM / SUB;
+    static_assert(WGM % SUB == 0, "whole waves per statistics sub-tile");
+    const int sub = wm / WPS;
+    const int nvalid = min(SR, a.M - (m0 + sub * SR));
     const int tcol = wn * WN + li;
     float s1[NI], s2[NI], mean[NI];
 #pragma unroll
@@ -85,8 +90,8 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
     for (int ni = 0; ni < NI; ++ni) {
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < WGM; ++w) t += red[w * BN + tcol + ni * 32];
-      mean[ni] = t / (float)nvalid;
+      for (int w = 0; w < WPS; ++w) t += red[(sub * WPS + w) * BN + tcol + ni * 32];
+      mean[ni] = t / (float)(nvalid > 0 ? nvalid : 1);
     }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
@@ -107,17 +112,21 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
       for (int ni = 0; ni < NI; ++ni) red[WGM * BN + wm * BN + tcol + ni * 32] = s2[ni];
     }
     __syncthreads();
-    if (tid < BN && n0 + tid < a.N) {
+    const int col = tid % BN, sb = tid / BN, nv = min(SR, a.M - (m0 + sb * SR));
+    if (tid < SUB * BN && n0 + col < a.N && nv > 0) {
       float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-      for (int w = 0; w < WGM; ++w) { t1 += red[w * BN + tid]; t2 += red[WGM * BN + w * BN + tid]; }
-      const int mt = m0 / BM;
-      const int col = n0 + tid;
-      const int gc = a.cpg ? col / a.cpg : g, cc = a.cpg ? col % a.cpg : col;
+      for (int w = 0; w < WPS; ++w) {
+        t1 += red[(sb * WPS + w) * BN + col];
+        t2 += red[WGM * BN + (sb * WPS + w) * BN + col];
+      }
+      const int mt = m0 / SR + sb;
+      const int cn = n0 + col;
+      const int gc = a.cpg ? cn / a.cpg : g, cc = a.cpg ? cn % a.cpg : cn;
       const long long so = ((long long)gc * a.st_nblk + a.st_base + mt) * (a.cpg ? a.cpg : a.N) + cc;
-      a.st_mean[so] = t1 / (float)nvalid;
+      a.st_mean[so] = t1 / (float)nv;
       a.st_m2[so] = t2;
-      if (cc == 0) a.st_cnt[(long long)gc * a.st_nblk + a.st_base + mt] = (float)nvalid;
+      if (cc == 0) a.st_cnt[(long long)gc * a.st_nblk + a.st_base + mt] = (float)nv;
     }
     __syncthreads();  // red is overwritten by the staged store below
   }

@@ -444,10 +444,12 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
       return true;
     }
     if (a.Cin % 64 || !xs8 || (a.xsc && a.Cin > kMaxXbn16)) return false;
+    if (conv_halo16_launch(FWD, dt, a, st)) return true;
     if (a.xsc) pipe16_dt<FWD, true>(dt, a, st);
     else pipe16_dt<FWD, false>(dt, a, st);
   } else if (mode == DGRAD) {
     if (a.Cout % 64 || a.Cin % 8) return false;
+    if (conv_halo16_launch(DGRAD, dt, a, st)) return true;
     pipe16_dt<DGRAD, false>(dt, a, st);
   } else {
     if (a.Cout % 8 || a.Cin % 8 || !xs8 || a.kchunk % 64) return false;

@@ -17,40 +17,55 @@ using namespace mauv;
 
 namespace mauv {
 
-// one thread per (row m, 8 consecutive k): gathers the taps from the NCHW fp32 images
+// one thread per (row m, 8 consecutive k): gathers the taps from the NCHW fp32 images.  The
+// k -> (c, r, s) decomposition is a per-block LDS table of input offsets (c*H*W + r*W + s) and
+// taps; the row index is split with 32-bit arithmetic (host-checked M * Kp/8 < 2^31): the 64-bit
+// divisions per element of the first version made this a 1 TB/s integer-bound pass
+constexpr int kMaxStemK = 2048;  // C*R*S of a stem (7x7: up to 41 input channels)
 template <int DT>
 __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ x, int C, int H,
                                                      int W, int R, int S, int stride, int pad,
                                                      int Ho, int Wo, int K, int Kp, long long M,
                                                      void* __restrict__ out) {
+  __shared__ int tab_off[kMaxStemK], tab_rs[kMaxStemK];
+  const int RS = R * S;
+  for (int k = threadIdx.x; k < Kp; k += 256) {
+    if (k < K) {
+      const int c = k / RS, rs = k - c * RS, r = rs / S, q = rs - r * S;
+      tab_off[k] = (c * H + r) * W + q;
+      tab_rs[k] = (r << 16) | q;
+    } else {
+      tab_off[k] = 0;
+      tab_rs[k] = -1;   // zero padding of K
+    }
+  }
+  __syncthreads();
   const int kc = Kp / 8;
-  const long long total = M * kc;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const long long m = i / kc;
-    const int k0 = 8 * (int)(i - m * kc);
-    const int HW = Ho * Wo;
-    const int b = (int)(m / HW), rem = (int)(m - (long long)b * HW);
-    const int oh = rem / Wo, ow = rem - oh * Wo;
+  const unsigned total = (unsigned)(M * kc);
+  const unsigned HW = (unsigned)(Ho * Wo);
+  const long long CHW = (long long)C * H * W;
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const unsigned m = i / (unsigned)kc;
+    const int k0 = 8 * (int)(i - m * (unsigned)kc);
+    const unsigned b = m / HW, rem = m - b * HW;
+    const int oh = (int)(rem / (unsigned)Wo), ow = (int)rem - oh * Wo;
+    const int ih0 = oh * stride - pad, iw0 = ow * stride - pad;
+    const float* xb = x + (long long)b * CHW + (long long)ih0 * W + iw0;
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int k = k0 + e;
-      float t = 0.f;
-      if (k < K) {
-        const int c = k / (R * S), rs = k - c * (R * S), r = rs / S, s = rs - r * S;
-        const int ih = oh * stride - pad + r, iw = ow * stride - pad + s;
-        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-          t = x[(((long long)b * C + c) * H + ih) * W + iw];
-      }
-      v[e] = t;
+      const int rs = tab_rs[k0 + e];
+      const int ih = ih0 + (rs >> 16), iw = iw0 + (rs & 0xffff);
+      v[e] = (rs >= 0 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+                 ? xb[tab_off[k0 + e]] : 0.f;
     }
     if constexpr (DT < 0) {
-      float* o = (float*)out + m * Kp + k0;
+      float* o = (float*)out + (long long)m * Kp + k0;
       *(floatx4*)o = floatx4{v[0], v[1], v[2], v[3]};
       *(floatx4*)(o + 4) = floatx4{v[4], v[5], v[6], v[7]};
     } else {
       const floatx8 f = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
-      *(u32x4*)((u16*)out + m * Kp + k0) = pack8<DT>(f);   // RNE, as every 16-bit store
+      *(u32x4*)((u16*)out + (long long)m * Kp + k0) = pack8<DT>(f);   // RNE, as every 16-bit store
     }
   }
 }
@@ -70,6 +85,10 @@ MAUV_API int mauv_stem_im2col(int dtype, const float* x, int B, int C, int H, in
   const long long M = (long long)B * Ho * Wo;
   if (Ho <= 0 || Wo <= 0) { set_error("stem_im2col: empty output"); return kErrArg; }
   const long long n = M * (Kp / 8);
+  if (n >= (1LL << 31) || Kp > kMaxStemK || S > 0xffff) {
+    set_error("stem_im2col: more than 2^31 row chunks or Kp > 2048");
+    return kErrArg;
+  }
   long long nb = (n + 255) / 256;
   if (nb > 16384) nb = 16384;
   const dim3 grid((unsigned)nb);

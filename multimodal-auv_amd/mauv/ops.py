@@ -104,6 +104,14 @@ def set_f32_math(mode):
     return _F32_NAMES[rc]
 
 
+def set_halo3(on):
+    """Route the 16-bit 3x3 / stride-1 64 -> 64 forwards through the LDS-row-image kernel
+    (True, default) or the implicit GEMM (False); returns the previous setting."""
+    rc = lib.mauv_set_halo3(1 if on else 0)
+    check(0 if rc >= 0 else rc, "set_halo3")
+    return bool(rc)
+
+
 def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_strides=None,
                x_bn=None, stats=None, alg_cin=None):
     """y[G][B*Ho*Wo][Cout] = conv(x'[g], w[g]) (+ bias[g]); w: [G][Cout][R][R][Cin].
