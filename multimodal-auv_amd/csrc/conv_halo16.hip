@@ -106,7 +106,11 @@ void conv_halo16(const ConvArgs a) {
   // channel co, its 64 input channels n in place (a column image)
   const int wn_ = tid >> 3, wq = tid & 7;
   const u16* wrow = wg + (long long)wn_ * 9 * C + 8 * wq;
-  u32x4 wv = *(const u32x4*)wrow;
+  // all nine taps' slices are fetched here, beside the input rows: the tap loop then issues no
+  // global loads (an L2 round trip per tap had sat in front of every tap's barrier)
+  u32x4 wv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wv[t] = *(const u32x4*)(wrow + t * C);
   if constexpr (XBN) __syncthreads();  // xbn staged
   const unsigned rfloor = a.xrelu ? 0u : 0x80008000u;
 #pragma unroll
@@ -129,7 +133,7 @@ void conv_halo16(const ConvArgs a) {
     const int hr = q >> 4, side = (q >> 3) & 1, cq = q & 7;
     *(u32x4*)(halo + hslot(hr * W2 + side * (W + 1), cq)) = u32x4{0u, 0u, 0u, 0u};
   }
-  *(u32x4*)(wbuf + wn_ * WLD + 8 * wq) = wv;
+  *(u32x4*)(wbuf + wn_ * WLD + 8 * wq) = wv[0];
 
   // ---- this lane's output pixel (row li of its wave's 32-pixel fragment) ----
   const int m = m0 + wm * 32 + li;
@@ -149,7 +153,6 @@ void conv_halo16(const ConvArgs a) {
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const int r = MODE == FWD ? t / 3 : 2 - t / 3, s = MODE == FWD ? t % 3 : 2 - t % 3;
-    if (t < 8) wv = *(const u32x4*)(wrow + (t + 1) * C);
     const u16* wb = wbuf + (t & 1) * WB;
     const int pix = (mok & ((unsigned)(oh + r - 1) < (unsigned)H)) ? hb + r * W2 + s : 0;
     const u16* ap = halo + pix * 64;
@@ -165,7 +168,7 @@ void conv_halo16(const ConvArgs a) {
         acc[ni] = H16<DT>::mfma(af, bq, acc[ni]);
       }
     }
-    if (t < 8) *(u32x4*)(wbuf + ((t + 1) & 1) * WB + wn_ * WLD + 8 * wq) = wv;
+    if (t < 8) *(u32x4*)(wbuf + ((t + 1) & 1) * WB + wn_ * WLD + 8 * wq) = wv[t + 1];
     __syncthreads();
   }
 
