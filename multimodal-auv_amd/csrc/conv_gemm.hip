@@ -775,11 +775,31 @@ MAUV_API int mauv_conv2d_wgrad_splits(int G, int B, int H, int W, int Cin, int C
   // fewest splits whose last round is filled within 5 % of the best fill (fewer splits: fewer
   // fp32 slab bytes).  MAUV_WGRAD_SPLITS=0 restores the round-1 rule.
   static int mode = -1;
-  if (mode < 0) { const char* e = getenv("MAUV_WGRAD_SPLITS"); mode = e ? atoi(e) : 1; }
+  if (mode < 0) { const char* e = getenv("MAUV_WGRAD_SPLITS"); mode = e ? atoi(e) : 2; }
   if (mode == 0) {
     long long splits = (1024 + tiles - 1) / tiles;
     if (splits > maxs) splits = maxs;
     return (int)(splits < 1 ? 1 : splits);
+  }
+  if (mode == 2) {
+    // Every split writes a full fp32 slab of its tiles that mauv_reparam_bwd reads back: at the
+    // layer-3/4 shapes the fill rule below chose 19 splits (1520 blocks, 11 GB of slabs per bf16
+    // step).  Price both: block rounds x the per-block MFMA time of its pixel chunk, plus the
+    // slab bytes (written and read back) at HBM rate, and take the cheapest split count.
+    const double tile_m = Cout <= 64 ? 64.0 : 128.0, tile_n = N <= 64 ? 64.0 : 128.0;
+    const double blk_flops = 480e12 / 512.0;       // sustained 16-bit MFMA rate per resident block
+    const double hbm = 5.0e12;                     // bytes/s a streaming pass sustains
+    const double ovh = 2.0e-6;                     // per-block prologue / epilogue (s)
+    long long best = 1;
+    double tbest = 1e30;
+    for (long long s = 1; s <= maxs; ++s) {
+      const long long nb = tiles * s, rounds = (nb + 511) / 512;
+      const long long kch = ((P + s - 1) / s + 31) / 32 * 32;
+      const double t = (double)rounds * ((double)kch * 2.0 * tile_m * tile_n / blk_flops + ovh) +
+                       (double)nb * tile_m * tile_n * 4.0 * 2.0 / hbm;
+      if (t < tbest * 0.995) { tbest = t; best = s; }
+    }
+    return (int)best;
   }
   const long long slots = 512;
   const long long lo = tiles * maxs < slots ? maxs : (slots + tiles - 1) / tiles;
