@@ -157,6 +157,12 @@ int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride, long lon
                      unsigned long long seed, unsigned long long sample0, unsigned int layer,
                      int G, int Cout, int Cin, int RS, int dw_cin, float* dmu, float* drho,
                      long long fixed_sample, hipStream_t stream);
+/* Kernel forms of the two calls above (process-wide; defaults 1, or MAUV_SAMPLE_BLK /
+ * MAUV_REPARAM_BWD4 = 0 at load): bit 0 = sampling by (output channel, channel range) blocks
+ * with vector KRSC stores (bit-identical to the per-element kernel), bit 1 = the backward with
+ * 16-byte slab loads (deterministic; a different fixed sum order).  -1 queries.  Returns the
+ * previous mask. */
+int mauv_set_reparam_kernels(int mask);
 /* 16-bit sampled weights (dtype 0 = bf16, 1 = f16) for the 16-bit convs: KRSC with cin_pad
  * (>= Cin) input channels; pad channels are not written (zero-fill them once).  The sampling
  * arithmetic is fp32, only the stored weight is rounded.  out_gstride 0 = Cout*RS*cin_pad. */

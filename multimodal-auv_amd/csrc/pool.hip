@@ -95,20 +95,27 @@ static void launch_maxpool_fwd(const typename S::T* x, int N, int H, int W, int 
                                typename S::T* y, unsigned char* idx, const float* scale,
                                const float* shift, int npg, hipStream_t stream);
 
-template <class S>
+// dx of the 3x3 / stride-2 / pad-1 max-pool as a gather: input pixel (ih, iw) collects dy of the
+// (at most 2 x 2) windows whose stored argmax tap is it.  V channels per thread (8 for 16-bit
+// storage: 16-byte dx stores, 8-byte argmax loads; 4 for fp32), index arithmetic in I (32-bit
+// whenever the element count allows: the 64-bit divisions had held this pass to ~2 TB/s).
+// The per-channel sum order over windows (oh, then ow, ascending) is the same for every V.
+template <class S, int V, typename I>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const typename S::T* __restrict__ dy,
                                                           const unsigned char* __restrict__ idx,
                                                           int N, int H, int W, int C, int Ho,
                                                           int Wo, typename S::T* __restrict__ dx) {
-  const int C4 = C / 4;
-  const long long total = (long long)N * H * W * C4;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c = 4 * (int)(i % C4);
-    long long p = i / C4;
-    const int iw = (int)(p % W); p /= W;
-    const int ih = (int)(p % H);
-    const int n = (int)(p / H);
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  typedef float vf __attribute__((ext_vector_type(V)));
+  const I CV = (I)(C / V);
+  const I total = (I)N * (I)H * (I)W * CV;
+  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
+    I p = i / CV;
+    const int c = V * (int)(i - p * CV);
+    I q = p / (I)W;
+    const int iw = (int)(p - q * (I)W);
+    const I n = q / (I)H;
+    const int ih = (int)(q - n * (I)H);
+    vf acc = (vf)(0.f);
     const int oh_lo = max(0, ih / 2), oh_hi = min(Ho - 1, (ih + 1) / 2);
     const int ow_lo = max(0, iw / 2), ow_hi = min(Wo - 1, (iw + 1) / 2);
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
@@ -117,17 +124,28 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const typename S::T* _
       for (int ow = ow_lo; ow <= ow_hi; ++ow) {
         const int s = iw - (ow * 2 - 1);
         if (s < 0 || s > 2) continue;
-        const long long o = (((long long)n * Ho + oh) * Wo + ow) * C + c;
-        const uchar4 k = *(const uchar4*)(idx + o);
-        const floatx4 g = S::ld4(dy + o);
-        const int t = r * 3 + s;
-        if (k.x == t) acc[0] += g[0];
-        if (k.y == t) acc[1] += g[1];
-        if (k.z == t) acc[2] += g[2];
-        if (k.w == t) acc[3] += g[3];
+        const I o = ((n * (I)Ho + (I)oh) * (I)Wo + (I)ow) * (I)C + (I)c;
+        const unsigned char t = (unsigned char)(r * 3 + s);
+        if constexpr (V == 8) {
+          const uint2 kk = *(const uint2*)(idx + o);
+          const floatx8 g = S::ld8(dy + o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const unsigned char k = (unsigned char)(((e < 4 ? kk.x : kk.y) >> (8 * (e & 3))) & 0xff);
+            if (k == t) acc[e] += g[e];
+          }
+        } else {
+          const uchar4 k = *(const uchar4*)(idx + o);
+          const floatx4 g = S::ld4(dy + o);
+          if (k.x == t) acc[0] += g[0];
+          if (k.y == t) acc[1] += g[1];
+          if (k.z == t) acc[2] += g[2];
+          if (k.w == t) acc[3] += g[3];
+        }
       }
     }
-    S::st4(dx + 4 * i, acc);
+    if constexpr (V == 8) S::st8(dx + (I)V * i, acc);
+    else S::st4(dx + (I)V * i, acc);
   }
 }
 
@@ -180,6 +198,18 @@ static int grid1(long long n) {
   return (int)(b < 1 ? 1 : b);
 }
 
+template <class S, int V>
+static void launch_maxpool_bwd(const typename S::T* dy, const unsigned char* idx, int N, int H,
+                               int W, int C, int Ho, int Wo, typename S::T* dx, hipStream_t stream) {
+  const long long total = (long long)N * H * W * (C / V);
+  if (total + (long long)8192 * 256 < (1LL << 31))
+    hipLaunchKernelGGL((maxpool_bwd_kernel<S, V, unsigned>), dim3(grid1(total)), dim3(256), 0, stream,
+                       dy, idx, N, H, W, C, Ho, Wo, dx);
+  else
+    hipLaunchKernelGGL((maxpool_bwd_kernel<S, V, long long>), dim3(grid1(total)), dim3(256), 0,
+                       stream, dy, idx, N, H, W, C, Ho, Wo, dx);
+}
+
 template <class S>
 static void launch_maxpool_fwd(const typename S::T* x, int N, int H, int W, int C, int Ho, int Wo,
                                typename S::T* y, unsigned char* idx, const float* scale,
@@ -216,8 +246,7 @@ MAUV_API int mauv_maxpool_bwd(const float* dy, const unsigned char* idx, int N, 
                               int C, float* dx, hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   if (C % 4) { set_error("maxpool_bwd: C % 4 != 0"); return kErrArg; }
-  hipLaunchKernelGGL(maxpool_bwd_kernel<SF32>, dim3(grid1((long long)N * H * W * C / 4)), dim3(256),
-                     0, stream, dy, idx, N, H, W, C, Ho, Wo, dx);
+  launch_maxpool_bwd<SF32, 4>(dy, idx, N, H, W, C, Ho, Wo, dx, stream);
   return check_launch("maxpool_bwd");
 }
 
@@ -263,8 +292,10 @@ MAUV_API int mauv_maxpool_bwd_h16(int dtype, const void* dy, const unsigned char
                                   int H, int W, int C, void* dx, hipStream_t stream) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   if (C % 4) { set_error("maxpool_bwd_h16: C % 4 != 0"); return kErrArg; }
-#define L(D) hipLaunchKernelGGL(maxpool_bwd_kernel<S16<D>>, dim3(grid1((long long)N * H * W * C / 4)), \
-                                dim3(256), 0, stream, (const u16*)dy, idx, N, H, W, C, Ho, Wo, (u16*)dx);
+#define L(D) if (C % 8 == 0) launch_maxpool_bwd<S16<D>, 8>((const u16*)dy, idx, N, H, W, C, Ho, Wo, \
+                                                          (u16*)dx, stream);                     \
+             else launch_maxpool_bwd<S16<D>, 4>((const u16*)dy, idx, N, H, W, C, Ho, Wo, (u16*)dx, \
+                                                stream);
   MAUV_DT_DISPATCH(dtype, "maxpool_bwd_h16", L)
 #undef L
   return check_launch("maxpool_bwd_h16");

@@ -65,6 +65,75 @@ __global__ __launch_bounds__(256) void reparam_sample_kernel(
   }
 }
 
+// Block form of the sampling (round 3): the kernel above computes a KRSC destination per element
+// with 64-bit divisions and stores 2-4 B scattered by cin_pad across the taps (bf16 step: 189
+// launches, 2.3 ms, 0.4-1.2 TB/s).  Here a block owns one output channel o and CB input channels
+// — ONE contiguous OIHW interval, read once (mu, softplus(rho) kept in registers) — and per sample
+// g draws the interval's Philox quads into an LDS image, then writes it in KRSC order as 4-channel
+// vector stores (8 B 16-bit, 16 B fp32).  Same normals (counter = (sample, layer, OIHW quad)),
+// same fp32 arithmetic: bit-identical output.  CB * RS <= 1024 (one quad or two per thread).
+// Needs Cin, cin_pad, out_gs % 4 == 0 and an aligned out (host checks).
+template <class S>
+__global__ __launch_bounds__(256) void reparam_sample_blk(
+    const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
+    uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS, int cin_pad,
+    typename S::T* __restrict__ out, long long out_gs, const unsigned long long* __restrict__ base,
+    int CB) {
+  __shared__ float sv[1024];
+  if (base) sample0 += *base;
+  const int o = blockIdx.x, tid = threadIdx.x;
+  const int c0 = blockIdx.y * CB, cb = min(CB, Cin - c0), len = cb * RS;
+  const long long numel = (long long)Cout * Cin * RS;
+  const long long i0 = ((long long)o * Cin + c0) * RS;
+  const long long q0 = i0 >> 2;
+  const int nq = (int)(((i0 + len - 1) >> 2) - q0 + 1);   // <= 257
+  float m[2][4], sg[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int qi = tid + 256 * j;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long i = 4 * (q0 + qi) + e;
+      const bool in = qi < nq && i >= i0 && i < i0 + len;
+      m[j][e] = in ? mu[i] : 0.f;
+      sg[j][e] = in ? softplus(rho[i]) : 0.f;
+    }
+  }
+  for (int g = blockIdx.z; g < G; g += gridDim.z) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int qi = tid + 256 * j;
+      if (qi < nq) {
+        const long long q = q0 + qi;
+        floatx4 ep;
+        if (eps) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const long long i = 4 * q + e;
+            ep[e] = (i >= i0 && i < i0 + len) ? eps[(long long)g * numel + i] : 0.f;
+          }
+        } else {
+          ep = normal4(seed, sample0 + g, layer, (uint32_t)q);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const long long i = 4 * q + e;
+          if (i >= i0 && i < i0 + len) sv[(int)(i - i0)] = m[j][e] + sg[j][e] * ep[e];
+        }
+      }
+    }
+    __syncthreads();
+    typename S::T* og = out + (long long)g * out_gs + (long long)o * RS * cin_pad + c0;
+    for (int k = 4 * tid; k < len; k += 1024) {   // KRSC order inside the block: rs-major
+      const int rs = k / cb, c = k - rs * cb;
+      const floatx4 v = {sv[c * RS + rs], sv[(c + 1) * RS + rs], sv[(c + 2) * RS + rs],
+                         sv[(c + 3) * RS + rs]};
+      S::st4(og + (long long)rs * cin_pad + c, v);
+    }
+    __syncthreads();
+  }
+}
+
 // One block per (output channel o, range of CB input channels): that range's parameters are
 // ONE contiguous OIHW interval [(o*Cin + c0)*RS, (o*Cin + c0 + cb)*RS) and, per tap rs, a
 // contiguous KRSC run of cb channels — so the block
@@ -131,6 +200,97 @@ __global__ __launch_bounds__(256) void reparam_bwd_kernel(
     __syncthreads();
     const long long esample = fixed >= 0 ? fixed : pass;
     for (long long q = q0 + tid; q <= q1; q += 256) {
+      floatx4 ep;
+      if (eps) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const long long i = 4 * q + e;
+          ep[e] = (i < numel) ? eps[esample * numel + i] : 0.f;
+        }
+      } else {
+        ep = normal4(seed, sample0 + esample, layer, (uint32_t)q);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long long i = 4 * q + e;
+        if (i < i0 || i >= i0 + len) continue;
+        const float d = sd[(int)(i - i0)];
+        dmu[i] += d;
+        drho[i] += d * ep[e] * sigmoidf_(rho[i]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// The same reduction with 16-byte slab loads (round 3).  The kernel above moves 4 B per lane per
+// load with one division per term and ran at 0.7-2.8 TB/s (bf16 step: 189 launches, 4.5 ms).
+// Here a lane owns a QUAD of consecutive KRSC channels (float4 loads); the block's NT threads are
+// QW quad lanes x NG term groups (QW = the quads of one pass, up to 64, so a small 1x1 layer with
+// 16 quads per block still keeps every lane busy); the term offsets s*dw_ss + g*dw_gs are tabled
+// once per block in LDS; each lane keeps four loads in flight.  Per element the terms are summed
+// in a fixed order (group grp takes t = grp + j*NG, four interleaved accumulators, then the
+// groups in order), so the result is deterministic (not bit-equal to the kernel above).
+// Phase B (chain rule over OIHW quads) is the same.  Needs cin_pad, c0, both strides % 4 == 0,
+// a 16-B aligned slab, G*splits <= RB4_TERMS and int32 term offsets (host checks).
+constexpr int RB4_TERMS = 2048;
+
+template <int NT>
+__global__ __launch_bounds__(NT) void reparam_bwd4_kernel(
+    const float* __restrict__ dw, int splits, long long dw_gs, long long dw_ss,
+    const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
+    uint64_t seed, uint64_t sample0, uint32_t layer, int G, int Cout, int Cin, int RS, int cin_pad,
+    float* __restrict__ dmu, float* __restrict__ drho, long long fixed, int CB, int QW) {
+  __shared__ int toff[RB4_TERMS];
+  __shared__ floatx4 red[NT];
+  __shared__ float sd[16 * 49];   // [cb][RS]
+  const int o = blockIdx.x, tid = threadIdx.x;
+  const int c0 = blockIdx.y * CB, cb = min(CB, Cin - c0);
+  const int len = cb * RS;
+  const int cq = cb >> 2, lenq = RS * cq;
+  const int NG = NT / QW, lq = tid & (QW - 1), grp = tid / QW;
+  const long long numel = (long long)Cout * Cin * RS;
+  const long long i0 = ((long long)o * Cin + c0) * RS;
+  const long long q0 = i0 >> 2, q1 = (i0 + len - 1) >> 2;
+  const int npass = fixed >= 0 ? 1 : G;
+  const int ng = fixed >= 0 ? G : 1;
+  const int nt = ng * splits;
+  for (int t = tid; t < nt; t += NT) {
+    const int g = t / splits;
+    toff[t] = (int)((t - g * splits) * dw_ss + g * dw_gs);
+  }
+  __syncthreads();
+  for (int pass = 0; pass < npass; ++pass) {
+    const int g0 = fixed >= 0 ? 0 : pass;
+    for (int kb = 0; kb < lenq; kb += QW) {
+      const int kq = kb + lq;
+      floatx4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+      int rs = 0, c4 = 0;
+      if (kq < lenq) {
+        rs = kq / cq;
+        c4 = kq - rs * cq;
+        const float* src = dw + ((long long)o * RS + rs) * cin_pad + c0 + 4 * c4 + g0 * dw_gs;
+        int t = grp;
+        for (; t + 3 * NG < nt; t += 4 * NG) {
+          a0 += *(const floatx4*)(src + toff[t]);
+          a1 += *(const floatx4*)(src + toff[t + NG]);
+          a2 += *(const floatx4*)(src + toff[t + 2 * NG]);
+          a3 += *(const floatx4*)(src + toff[t + 3 * NG]);
+        }
+        for (; t < nt; t += NG) a0 += *(const floatx4*)(src + toff[t]);
+      }
+      red[tid] = (a0 + a1) + (a2 + a3);
+      __syncthreads();
+      if (grp == 0 && kq < lenq) {
+        floatx4 r = red[lq];
+        for (int j = 1; j < NG; ++j) r += red[j * QW + lq];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sd[(4 * c4 + e) * RS + rs] = r[e];
+      }
+      __syncthreads();
+    }
+    const long long esample = fixed >= 0 ? fixed : pass;
+    for (long long q = q0 + tid; q <= q1; q += NT) {
       floatx4 ep;
       if (eps) {
 #pragma unroll
@@ -226,6 +386,39 @@ static dim3 sample_grid(long long nq, int G) {
   return dim3(bx, (unsigned)(gy < 1 ? 1 : gy));
 }
 
+// Kernel forms (MAUV_SAMPLE_BLK / MAUV_REPARAM_BWD4, default 1 each; mauv_set_reparam_kernels):
+// bit 0 = block-form sampling, bit 1 = 16-byte reparam_bwd.
+static int g_sample_blk = -1, g_bwd4 = -1;
+static int env_flag(int& v, const char* name) {
+  if (v < 0) { const char* e = getenv(name); v = e ? (atoi(e) != 0) : 1; }
+  return v;
+}
+
+// The block form when its layout conditions hold, else the element kernel.
+template <class S>
+static void launch_sample(const float* mu, const float* rho, const float* eps,
+                          unsigned long long seed, unsigned long long sample0,
+                          const unsigned long long* base, unsigned int layer, int G, int Cout,
+                          int Cin, int RS, int cin_pad, typename S::T* out, long long gs,
+                          hipStream_t stream) {
+  const int blk = env_flag(g_sample_blk, "MAUV_SAMPLE_BLK");
+  const int align = (int)sizeof(typename S::T) * 4;
+  if (blk && Cin % 4 == 0 && cin_pad % 4 == 0 && gs % 4 == 0 && RS <= 256 &&
+      ((uintptr_t)out % align) == 0) {
+    const int CB = RS == 1 ? 1024 : (1024 / RS) / 4 * 4;
+    const long long nb = (long long)Cout * ceil_div(Cin, CB);
+    long long gz = (1024 + nb - 1) / nb;
+    if (gz > G) gz = G;
+    hipLaunchKernelGGL(reparam_sample_blk<S>, dim3(Cout, ceil_div(Cin, CB), (unsigned)gz),
+                       dim3(256), 0, stream, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS,
+                       cin_pad, out, gs, base, CB);
+    return;
+  }
+  const long long nq = ((long long)Cout * Cin * RS + 3) / 4;
+  hipLaunchKernelGGL(reparam_sample_kernel<S>, sample_grid(nq, G), dim3(256), 0, stream, mu, rho,
+                     eps, seed, sample0, layer, G, Cout, Cin, RS, cin_pad, out, gs, base);
+}
+
 }  // namespace mauv
 
 // Sample G weight sets: out[g] (KRSC) = mu + softplus(rho) * eps_g.  mu/rho in OIHW
@@ -238,9 +431,9 @@ MAUV_API int mauv_reparam_sample(const float* mu, const float* rho, const float*
                                  float* out, long long out_gstride, hipStream_t stream) {
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
-  hipLaunchKernelGGL(reparam_sample_kernel<SF32>, sample_grid(nq, G), dim3(256), 0, stream, mu,
-                     rho, eps, seed, sample0, layer, G, Cout, Cin, RS, Cin, out,
-                     out_gstride ? out_gstride : numel);
+  (void)nq;
+  launch_sample<SF32>(mu, rho, eps, seed, sample0, nullptr, layer, G, Cout, Cin, RS, Cin, out,
+                      out_gstride ? out_gstride : numel, stream);
   return check_launch("reparam_sample");
 }
 
@@ -254,9 +447,9 @@ MAUV_API int mauv_reparam_sample_padded(const float* mu, const float* rho, const
   if (cin_pad < Cin) { set_error("reparam_sample_padded: cin_pad < Cin"); return kErrArg; }
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
-  hipLaunchKernelGGL(reparam_sample_kernel<SF32>, sample_grid(nq, G), dim3(256), 0, stream, mu,
-                     rho, eps, seed, sample0, layer, G, Cout, Cin, RS, cin_pad, out,
-                     out_gstride ? out_gstride : (long long)Cout * RS * cin_pad);
+  (void)nq;
+  launch_sample<SF32>(mu, rho, eps, seed, sample0, nullptr, layer, G, Cout, Cin, RS, cin_pad, out,
+                      out_gstride ? out_gstride : (long long)Cout * RS * cin_pad, stream);
   return check_launch("reparam_sample_padded");
 }
 
@@ -272,9 +465,9 @@ MAUV_API int mauv_reparam_sample_h16(int dtype, const float* mu, const float* rh
   const long long numel = (long long)Cout * Cin * RS;
   const long long nq = (numel + 3) / 4;
   const long long gs = out_gstride ? out_gstride : (long long)Cout * RS * cin_pad;
-#define L(D) hipLaunchKernelGGL(reparam_sample_kernel<S16<D>>, sample_grid(nq, G), dim3(256), 0, \
-                                stream, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS,   \
-                                cin_pad, (u16*)out, gs);
+  (void)nq;
+#define L(D) launch_sample<S16<D>>(mu, rho, eps, seed, sample0, nullptr, layer, G, Cout, Cin, RS, \
+                                   cin_pad, (u16*)out, gs, stream);
   MAUV_DT_DISPATCH(dtype, "reparam_sample_h16", L)
 #undef L
   return check_launch("reparam_sample_h16");
@@ -294,14 +487,13 @@ MAUV_API int mauv_reparam_sample_ex(int dtype, const float* mu, const float* rho
   const long long nq = (numel + 3) / 4;
   const long long gs = out_gstride ? out_gstride : (long long)Cout * RS * cin_pad;
   if (dtype < 0) {
-    hipLaunchKernelGGL(reparam_sample_kernel<SF32>, sample_grid(nq, G), dim3(256), 0, stream, mu,
-                       rho, eps, seed, sample0, layer, G, Cout, Cin, RS, cin_pad, (float*)out, gs,
-                       sample_base);
+    launch_sample<SF32>(mu, rho, eps, seed, sample0, sample_base, layer, G, Cout, Cin, RS, cin_pad,
+                        (float*)out, gs, stream);
     return check_launch("reparam_sample_ex");
   }
-#define L(D) hipLaunchKernelGGL(reparam_sample_kernel<S16<D>>, sample_grid(nq, G), dim3(256), 0, \
-                                stream, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS,   \
-                                cin_pad, (u16*)out, gs, sample_base);
+  (void)nq;
+#define L(D) launch_sample<S16<D>>(mu, rho, eps, seed, sample0, sample_base, layer, G, Cout, Cin, \
+                                   RS, cin_pad, (u16*)out, gs, stream);
   MAUV_DT_DISPATCH(dtype, "reparam_sample_ex", L)
 #undef L
   return check_launch("reparam_sample_ex");
@@ -328,6 +520,29 @@ MAUV_API int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride,
   const long long ss = dw_sstride ? dw_sstride : gs * G;
   if (RS > 49) { set_error("reparam_bwd: R*S > 49"); return kErrArg; }
   (void)nq;
+  const int nt = (fixed_sample >= 0 ? G : 1) * splits;
+  const int v4 = env_flag(mauv::g_bwd4, "MAUV_REPARAM_BWD4");
+  if (v4 && Cin % 4 == 0 && dw_cin % 4 == 0 && gs % 4 == 0 && ss % 4 == 0 &&
+      ((uintptr_t)dw & 15) == 0 && nt <= RB4_TERMS &&
+      (long long)(splits - 1) * ss + (long long)(G - 1) * gs + (long long)Cout * RS * dw_cin <
+          (1LL << 31)) {
+    // 1x1: up to 256 channels per block (64 quads: one full pass of QW = 64 lanes); 3x3: the
+    // rule above (16 or 64 channels, <= 16*49 parameters per block)
+    const int cb = RS == 1 ? (Cin >= 256 ? 256 : (Cin + 3) / 4 * 4) : rb_cb(Cout, Cin, RS);
+    const int lenq = RS * (cb / 4);
+    int qw = 1;
+    while (qw < lenq && qw < 64) qw *= 2;
+    const long long xs = fixed_sample >= 0 ? (long long)(fixed_sample - (long long)sample0) : -1LL;
+    if (nt >= 32)
+      hipLaunchKernelGGL(reparam_bwd4_kernel<1024>, dim3(Cout, ceil_div(Cin, cb)), dim3(1024), 0,
+                         stream, dw, splits, gs, ss, mu, rho, eps, seed, sample0, layer, G, Cout,
+                         Cin, RS, dw_cin, dmu, drho, xs, cb, qw);
+    else
+      hipLaunchKernelGGL(reparam_bwd4_kernel<256>, dim3(Cout, ceil_div(Cin, cb)), dim3(256), 0,
+                         stream, dw, splits, gs, ss, mu, rho, eps, seed, sample0, layer, G, Cout,
+                         Cin, RS, dw_cin, dmu, drho, xs, cb, qw);
+    return check_launch("reparam_bwd");
+  }
   const int cb = rb_cb(Cout, Cin, RS);
   hipLaunchKernelGGL(reparam_bwd_kernel, dim3(Cout, ceil_div(Cin, cb)), dim3(256), 0, stream, dw, splits,
                      gs, ss, mu, rho, eps, seed, sample0, layer, G, Cout, Cin, RS, dw_cin, dmu, drho,
@@ -361,4 +576,20 @@ MAUV_API int mauv_philox_raw(unsigned long long seed, unsigned long long sample,
   hipLaunchKernelGGL(philox_raw_kernel, dim3((nq + 255) / 256), dim3(256), 0, stream, seed,
                      sample, layer, nq, (uint4*)out_u32x4, (floatx4*)out_normal4);
   return check_launch("philox_raw");
+}
+
+// Select the sampling / reparameterisation-backward kernel forms: bit 0 = block-form sampling
+// (reparam_sample_blk), bit 1 = 16-byte backward (reparam_bwd4); -1 queries.  Returns the
+// previous mask.  Sampling is bit-identical either way; the backward's sum order differs.
+MAUV_API int mauv_set_reparam_kernels(int mask) {
+  const int prev = mauv::env_flag(mauv::g_sample_blk, "MAUV_SAMPLE_BLK") |
+                   (mauv::env_flag(mauv::g_bwd4, "MAUV_REPARAM_BWD4") << 1);
+  if (mask >= 0 && mask <= 3) {
+    mauv::g_sample_blk = mask & 1;
+    mauv::g_bwd4 = (mask >> 1) & 1;
+  } else if (mask != -1) {
+    mauv::set_error("set_reparam_kernels: mask 0..3 or -1 (query)");
+    return mauv::kErrArg;
+  }
+  return prev;
 }

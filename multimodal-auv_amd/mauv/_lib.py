@@ -43,6 +43,7 @@ SIGNATURES = {
     # reparam.hip
     "mauv_reparam_sample": [P, P, P, U64, U64, U32, I, I, I, I, P, LL, P],
     "mauv_reparam_bwd": [P, I, LL, LL, P, P, P, U64, U64, U32, I, I, I, I, I, P, P, LL, P],
+    "mauv_set_reparam_kernels": [I],
     "mauv_reparam_sample_h16": [I, P, P, P, U64, U64, U32, I, I, I, I, I, P, LL, P],
     "mauv_reparam_sample_padded": [P, P, P, U64, U64, U32, I, I, I, I, I, P, LL, P],
     "mauv_kl_workspace_bytes": [I],

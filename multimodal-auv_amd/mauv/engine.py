@@ -122,6 +122,15 @@ class RootState:
         # device int64 [1] added to every sampled MC index while a forward is being captured
         # into a HIP graph (mauv.predict): the replay draws fresh samples after it is updated
         self.sample_base = None
+        # parameter lists the entry points walk every call (named_parameters over 696 tensors:
+        # ~1.3 ms of host time per step ahead of the first kernel); built once, like self.params
+        self._plists = {}
+
+    def plist(self, key, build):
+        got = self._plists.get(key)
+        if got is None:
+            got = self._plists[key] = build()
+        return got
 
     def trunk_dtype(self):
         if self.precision is not None:
@@ -831,7 +840,7 @@ def run_trunk_mc(trunk, x, num_mc, state=None, sample0=None, join=None):
     if dev.type != "cuda":
         raise RuntimeError("mauv: the model must be on a ROCm device (model.to('cuda'))")
     s0 = st.next_samples(num_mc) if sample0 is None else sample0
-    params = list(trunk.parameters())
+    params = st.plist(("trunk", id(trunk)), lambda: list(trunk.parameters()))
     save = needs_grad(params)
     runner = TrunkRunner(trunk, st, num_mc, s0, save, st.trunk_dtype(), join)
     x = _to_device(x, dev)
@@ -847,7 +856,8 @@ def run_multimodal_mc(model, inputs, bathy, sss, num_mc):
         _check_trunk(trunk)
     dev = model.fc.mu_weight.device
     s0 = st.next_samples(num_mc)
-    head_params = [p for n, p in model.named_parameters() if not n.split(".")[0].endswith("_feat")]
+    head_params = st.plist("head", lambda: [p for n, p in model.named_parameters()
+                                            if not n.split(".")[0].endswith("_feat")])
     trunks = (model.image_model_feat, model.bathy_model_feat, model.sss_model_feat)
     xs = (inputs, bathy, sss)
     # Training only: concurrent trunks need the fusion head's backward to set up the gradient

@@ -30,6 +30,7 @@ class KLTable:
     def __init__(self, modules):
         self.entries = _entries(modules)
         self.n = len(self.entries)
+        self.nmod = len(modules)
         self._fwd = None
         self._fwd_key = None
         self._bwd = None
@@ -110,7 +111,7 @@ def kl_of_modules(modules, root=None):
     owner_mod = root if root is not None else modules[0]
     key = "_mauv_kltab"
     tab = owner_mod.__dict__.get(key)
-    if tab is None or tab.n != len(_entries(modules)):
+    if tab is None or tab.nmod != len(modules):
         tab = KLTable(modules)
         owner_mod.__dict__[key] = tab
     st = root_state(owner_mod)
@@ -131,7 +132,9 @@ def unwrap(model):
 def get_kl_loss(m):
     """Sum of every Bayesian layer's KL (bayesian-torch ``get_kl_loss`` semantics)."""
     m = unwrap(m)
-    bayes = [x for x in m.modules() if is_bayesian(x)]
+    st = m.__dict__.get("_mauv_state")   # an engine model: its Bayesian layer list, built once
+    bayes = st.plist("bayes", lambda: [x for x in m.modules() if is_bayesian(x)]) if st \
+        else [x for x in m.modules() if is_bayesian(x)]
     if bayes:
         return kl_of_modules(bayes, root=m)
     kl = None  # foreign modules exposing kl_loss(): reference behaviour

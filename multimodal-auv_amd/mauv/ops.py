@@ -112,6 +112,18 @@ def set_halo3(on):
     return bool(rc)
 
 
+def set_reparam_kernels(sample_blk=None, bwd4=None):
+    """Kernel forms of reparam_sample (block form, bit-identical) and reparam_bwd (16-byte slab
+    loads); None keeps a setting.  Returns the previous (sample_blk, bwd4)."""
+    prev = lib.mauv_set_reparam_kernels(-1)
+    check(0 if prev >= 0 else prev, "set_reparam_kernels")
+    sb = (prev & 1) if sample_blk is None else int(bool(sample_blk))
+    b4 = (prev >> 1) & 1 if bwd4 is None else int(bool(bwd4))
+    rc = lib.mauv_set_reparam_kernels(sb | (b4 << 1))
+    check(0 if rc >= 0 else rc, "set_reparam_kernels")
+    return bool(prev & 1), bool(prev & 2)
+
+
 def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_strides=None,
                x_bn=None, stats=None, alg_cin=None):
     """y[G][B*Ho*Wo][Cout] = conv(x'[g], w[g]) (+ bias[g]); w: [G][Cout][R][R][Cin].

@@ -207,6 +207,34 @@ def test_bn16_apply_bwd_matches_fp32_kernels(dt, C, relu, res, lazy):
 
 
 @pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
+@pytest.mark.parametrize("N,H,C", [(2, 10, 12), (5, 16, 64), (1, 7, 8)])
+def test_maxpool16_bwd_shapes(dt, N, H, C):
+    """8-channel gather (C % 8 == 0) and the 4-channel one (C = 12), even / odd sizes: the max-pool
+    backward equals autograd of F.max_pool2d on the same argmax (no ties: distinct values)."""
+    from mauv import ops
+    torch.manual_seed(16 + C)
+    x = (torch.randperm(N * H * H * C).float() / 64.0).reshape(N, H, H, C).to(dt)
+    Ho = ops.out_hw(H, 3, 2, 1)
+    xr = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    yr, flat = F.max_pool2d(xr, 3, 2, 1, return_indices=True)
+    # the argmax as the kernels store it: tap r*3 + s of the window at (2*oh - 1, 2*ow - 1)
+    oh = torch.arange(Ho).view(1, 1, Ho, 1)
+    ow = torch.arange(Ho).view(1, 1, 1, Ho)
+    tap = (flat // H - (2 * oh - 1)) * 3 + (flat % H - (2 * ow - 1))
+    idx_ref = tap.permute(0, 2, 3, 1).to(torch.uint8).contiguous()
+    if C % 8 == 0:   # the 16-bit forward (8-channel chunks) writes the same argmax bytes
+        y = torch.empty(N, Ho, Ho, C, device=dev, dtype=dt)
+        idx = torch.empty(N, Ho, Ho, C, dtype=torch.uint8, device=dev)
+        ops.maxpool_fwd(x.to(dev), N, H, H, C, y, idx)
+        assert torch.equal(idx.cpu(), idx_ref)
+    dy = torch.randn(N, Ho, Ho, C).to(dt)
+    yr.backward(dy.double().permute(0, 3, 1, 2))
+    dx = torch.empty(N, H, H, C, device=dev, dtype=dt)
+    ops.maxpool_bwd(dy.to(dev), idx_ref.to(dev), N, H, H, C, dx)
+    close(dx, xr.grad.permute(0, 2, 3, 1), 2 * ULP[dt])
+
+
+@pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
 def test_pools16_and_stem_pack(dt):
     from mauv import ops
     N, H, C = 3, 9, 64

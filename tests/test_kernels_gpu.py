@@ -421,15 +421,18 @@ def test_reparam_and_kl():
         assert torch.equal(o1[0], outb[g])
 
 
-@pytest.mark.parametrize("G,Cout,Cin,R,fixed", [(11, 24, 20, 3, -1), (11, 8, 70, 1, -1),
-                                                  (5, 24, 20, 3, 2), (12, 16, 64, 3, -1)])
-def test_reparam_bwd_sample_batches(G, Cout, Cin, R, fixed):
+@pytest.mark.parametrize("G,Cout,Cin,R,fixed,splits", [
+    (11, 24, 20, 3, -1, 3), (11, 8, 70, 1, -1, 3), (5, 24, 20, 3, 2, 3), (12, 16, 64, 3, -1, 3),
+    # 16-byte kernel (reparam_bwd4): 1x1 with a ragged 256-channel block and 1024 threads,
+    # 16 quads per block in exact mode (256 threads), 3x3 with 16-channel blocks
+    (5, 16, 300, 1, 2, 20), (3, 8, 64, 1, -1, 7), (5, 32, 128, 3, 4, 9), (2, 4, 12, 1, 1, 1)])
+def test_reparam_bwd_sample_batches(G, Cout, Cin, R, fixed, splits):
     """reparam_bwd with more MC samples than one LDS batch (RB_GC = 8): the per-sample terms
     are added in sample order onto nonzero accumulated gradients; ragged channel blocks
-    (Cin % 16, Cin % 64), 1x1 and 3x3, and bayesian-torch's fixed-sample mode."""
+    (Cin % 16, Cin % 64, Cin % 256), 1x1 and 3x3, 1 to 20 split-K slabs, both kernels (Cin % 4
+    selects the 16-byte one), and bayesian-torch's fixed-sample mode."""
     from mauv import ops
     torch.manual_seed(9)
-    splits = 3
     mu = torch.randn(Cout, Cin, R, R) * 0.1
     rho = torch.randn(Cout, Cin, R, R) - 3
     eps = torch.randn(G, Cout * Cin * R * R)
@@ -574,6 +577,45 @@ def test_fused_adam_matches_torch_adam():
         close(ob2.state[q]["exp_avg_sq"], oa.state[p]["exp_avg_sq"], rtol=1e-6, atol=1e-12)
 
 
+def test_fused_adam_fast_path_matches_torch_adam():
+    """Persistent gradient tensors (the engine's arena views): from the second step FusedAdam
+    takes its cached path (one table, one shared step buffer) — still == torch.optim.Adam over 5
+    steps, state["step"] readable per parameter, and a state_dict round trip (torch Adam ->
+    FusedAdam) continues identically."""
+    from mauv.optim import FusedAdam
+    torch.manual_seed(12)
+    shapes = [(64, 3, 7, 7), (7,), (300, 20), (5, 3)]
+    pa = [torch.randn(s, device=dev, requires_grad=True) for s in shapes]
+    pb = [p.detach().clone().requires_grad_(True) for p in pa]
+    for p, q in zip(pa, pb):
+        p.grad, q.grad = torch.empty_like(p), torch.empty_like(q)
+    oa = FusedAdam(pa, lr=5e-3, weight_decay=1e-5)
+    ob = torch.optim.Adam(pb, lr=5e-3, weight_decay=1e-5)
+    for _ in range(5):
+        for p, q in zip(pa, pb):
+            g = torch.randn_like(p)
+            p.grad.copy_(g)
+            q.grad.copy_(g)
+        oa.step()
+        ob.step()
+    assert 0 in oa._fast and all(float(oa.state[p]["step"]) == 5.0 for p in pa)
+    for p, q in zip(pa, pb):
+        close(p, q, rtol=1e-6, atol=1e-7)
+    import copy
+    oa2 = FusedAdam(pa, lr=5e-3, weight_decay=1e-5)
+    # a copy: torch's load_state_dict keeps the very "step" tensors it is given (no copy), so
+    # two optimizers loaded from one dict would bump each other's counts
+    oa2.load_state_dict(copy.deepcopy(ob.state_dict()))
+    for p, q in zip(pa, pb):
+        g = torch.randn_like(p)
+        p.grad.copy_(g)
+        q.grad.copy_(g)
+    oa2.step()
+    ob.step()
+    for p, q in zip(pa, pb):
+        close(p, q, rtol=1e-6, atol=1e-7)
+
+
 @pytest.mark.parametrize("nblk", [37, 1500])
 def test_bn_stats_finalize_segmented(nblk):
     """Per-128-row partials (count, mean, M2) merged into batch statistics: one launch up to
@@ -692,3 +734,56 @@ def test_bn_relu_mask_path_matches_output_path(dt, C, M, res_bn):
         res.append((dy, dres, dg, db))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16],
+                         ids=["fp32", "bf16", "f16"])
+@pytest.mark.parametrize("G,Cout,Cin,R,cin_pad,explicit", [
+    (5, 64, 64, 3, None, False), (5, 48, 1028, 1, None, False), (3, 7, 2048, 1, None, True),
+    (4, 33, 20, 3, 24, True), (2, 16, 12, 7, None, False), (5, 8, 6, 3, None, False)])
+def test_reparam_sample_block_form_bit_identical(dt, G, Cout, Cin, R, cin_pad, explicit):
+    """The block-form sampling (one output channel x channel range per block, LDS image, vector
+    KRSC stores; mauv_set_reparam_kernels bit 0) writes the per-element kernel's values: Philox
+    and explicit eps, 1x1 / 3x3 / 7x7, ragged channel ranges (1028 = 1024 + 4), padded KRSC rows
+    (pad channels untouched), the device sample counter; Cin % 4 != 0 falls back.  Its 16-bit
+    weights are the fp32 sample rounded once more (the reference's fp32 weight cast by autocast)
+    — bit-exact for every dtype; the per-element f16 kernel instead rounds mu + sigma*eps to f16
+    in one step (hipcc contracts it to v_fma_mix), which differs by 1 ulp on rare elements."""
+    from mauv import ops
+    torch.manual_seed(21)
+    RS = R * R
+    mu = (torch.randn(Cout, Cin, R, R) * 0.1).to(dev)
+    rho = (torch.randn(Cout, Cin, R, R) - 3).to(dev)
+    eps = torch.randn(G, Cout * Cin * RS, device=dev) if explicit else None
+    cp = cin_pad or Cin
+    base = torch.tensor([3], dtype=torch.int64, device=dev)
+    outs = []
+    prev = ops.set_reparam_kernels(sample_blk=False)
+    try:
+        for blk in (False, True):
+            ops.set_reparam_kernels(sample_blk=blk)
+            o = torch.full((G, Cout, R, R, cp), 7.0, device=dev).to(dt)
+            ops.reparam_sample(mu, rho, o, G, 99, 11, 5, Cout, Cin, RS, eps=eps,
+                               cin_pad=cin_pad)
+            o2 = torch.full((G, Cout, R, R, cp), 7.0, device=dev).to(dt)
+            ops.reparam_sample_ex(mu, rho, o2, G, 99, 11, base, 5, Cout, Cin, RS, eps=eps,
+                                  cin_pad=cin_pad)
+            outs.append((o, o2))
+    finally:
+        ops.set_reparam_kernels(sample_blk=prev[0])
+    f32 = torch.full((G, Cout, R, R, cp), 7.0, device=dev)
+    ops.reparam_sample(mu, rho, f32, G, 99, 11, 5, Cout, Cin, RS, eps=eps, cin_pad=cin_pad)
+    torch.cuda.synchronize()
+    blk_on = Cin % 4 == 0
+    if blk_on or dt != torch.float16:
+        assert torch.equal(outs[1][0], f32.to(dt))
+    if dt == torch.float16:
+        for a, b in ((outs[0][0], outs[1][0]), (outs[0][1], outs[1][1])):
+            d = (a.view(torch.int16).int() - b.view(torch.int16).int()).abs()
+            assert d.max() <= 1 and (d > 0).float().mean() < 1e-3
+    else:
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    if cin_pad:
+        assert (outs[1][0][..., Cin:].float() == 7.0).all()
+    if not explicit:   # the device counter shifts the sample index by 3
+        assert not torch.equal(outs[1][0], outs[1][1])
