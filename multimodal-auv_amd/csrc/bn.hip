@@ -165,7 +165,10 @@ __global__ __launch_bounds__(1024) void bn_stats_final(
 // channel) are merged in two launches: stage 2a reduces segments of SEG partials per channel
 // exactly as above (two passes, double) into (count, mean, M2), stage 2b Chan-merges the
 // segments in order.  One segment (nblk <= SEG) keeps the single-launch path above.
-constexpr int SEG = 512;
+#ifndef MAUV_STAT_SEG
+#define MAUV_STAT_SEG 512
+#endif
+constexpr int SEG = MAUV_STAT_SEG;
 static inline int stat_segs(int nblk) { return (nblk + SEG - 1) / SEG; }
 
 __global__ __launch_bounds__(1024) void bn_stats_seg(int nblk, int C,
@@ -658,7 +661,10 @@ static void bwd_geometry(long long M, int C, int& nblk, int& rpb) {
   const int rp = 256 / (C / 8);
   long long r = (long long)rp * rpt;
   long long n = (M + r - 1) / r;
-  if (n > 1024) { n = 1024; r = (M + n - 1) / n; }
+#ifndef MAUV_BWD_NBLK_CAP
+#define MAUV_BWD_NBLK_CAP 1024
+#endif
+  if (n > MAUV_BWD_NBLK_CAP) { n = MAUV_BWD_NBLK_CAP; r = (M + n - 1) / n; }
   if (r < rp) r = rp;
   rpb = (int)r;
   nblk = (int)((M + r - 1) / r);
