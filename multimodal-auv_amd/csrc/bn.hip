@@ -164,14 +164,18 @@ __global__ __launch_bounds__(1024) void bn_stats_final(
 // Large partial counts (an MC-batched inference chunk: tens of thousands of 128-row partials per
 // channel) are merged in two launches: stage 2a reduces segments of SEG partials per channel
 // exactly as above (two passes, double) into (count, mean, M2), stage 2b Chan-merges the
-// segments in order.  One segment (nblk <= SEG) keeps the single-launch path above.
-#ifndef MAUV_STAT_SEG
-#define MAUV_STAT_SEG 512
-#endif
-constexpr int SEG = MAUV_STAT_SEG;
-static inline int stat_segs(int nblk) { return (nblk + SEG - 1) / SEG; }
+// segments in order.  One segment keeps the single-launch path above.  Segment length: 128
+// partials up to 64 segments (a training step's layers: 4x more finalize blocks and 4x shorter
+// chains than 512 — bn_stats_final + seg + merge 3.14 -> 2.09 ms per bf16 step,
+// profiles/round3/bn_finalize_geometry_ab.txt), 512 beyond (an inference chunk's hundreds of
+// thousands of partials: the in-order merge walks one segment list per channel).
+static inline int stat_seg_len(int nblk) { return nblk <= 128 * 64 ? 128 : 512; }
+static inline int stat_segs(int nblk) {
+  const int L = stat_seg_len(nblk);
+  return (nblk + L - 1) / L;
+}
 
-__global__ __launch_bounds__(1024) void bn_stats_seg(int nblk, int C,
+__global__ __launch_bounds__(1024) void bn_stats_seg(int nblk, int C, int SEG,
                                                      const float* __restrict__ pmean,
                                                      const float* __restrict__ pm2,
                                                      const float* __restrict__ pcnt,
@@ -246,7 +250,7 @@ static void stats_final(int G, int nblk, int C, const float* pmean, const float*
   }
   double* seg = (double*)(((uintptr_t)(ws + (long long)G * C) + 7) & ~(uintptr_t)7);
   hipLaunchKernelGGL(bn_stats_seg, dim3((C + 63) / 64, G, S), dim3(1024), 0, stream, nblk, C,
-                     pmean, pm2, pcnt, seg);
+                     stat_seg_len(nblk), pmean, pm2, pcnt, seg);
   hipLaunchKernelGGL(bn_stats_merge, dim3((C + 255) / 256, G), dim3(256), 0, stream, G, S, C, seg,
                      gamma, beta, eps, mean, invstd, scale, shift, ws);
 }
@@ -661,10 +665,9 @@ static void bwd_geometry(long long M, int C, int& nblk, int& rpb) {
   const int rp = 256 / (C / 8);
   long long r = (long long)rp * rpt;
   long long n = (M + r - 1) / r;
-#ifndef MAUV_BWD_NBLK_CAP
-#define MAUV_BWD_NBLK_CAP 1024
-#endif
-  if (n > MAUV_BWD_NBLK_CAP) { n = MAUV_BWD_NBLK_CAP; r = (M + n - 1) / n; }
+  // at most 256 partial blocks per group (was 1024: bn_bwd_final walks 4x fewer partials,
+  // 1.53 -> 1.01 ms per bf16 step, and the partial pass itself 11.35 -> 11.23 ms)
+  if (n > 256) { n = 256; r = (M + n - 1) / n; }
   if (r < rp) r = rp;
   rpb = (int)r;
   nblk = (int)((M + r - 1) / r);
