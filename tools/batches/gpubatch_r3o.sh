@@ -1,3 +1,4 @@
+# RECORD ONLY: the switches / experimental libraries this script A/Bs were removed after the measurement (profiles/round3/*_ab.txt); it no longer runs against the current library
 # round 3: block order of the BN row passes (MAUV_BN_REV bits: 1 = backward partial pass reversed,
 # 2 = backward apply reversed, 4 = forward apply reversed) — a pass that walks its tensors in the
 # opposite order of the pass before starts on the rows the memory-side cache still holds.

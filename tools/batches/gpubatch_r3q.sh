@@ -1,3 +1,4 @@
+# RECORD ONLY: the switches / experimental libraries this script A/Bs were removed after the measurement (profiles/round3/*_ab.txt); it no longer runs against the current library
 # round 3: gradient arena attached during the forward (host work off the loss-check -> backward
 # critical path), and the BN backward partial pass with U rows' loads issued together
 # (MAUV_BN_PUNROLL = 1 / 2 / 4): model, drop-in and BN tests; serial kernel statistics per U;

@@ -1,3 +1,4 @@
+# RECORD ONLY: the switches / experimental libraries this script A/Bs were removed after the measurement (profiles/round3/*_ab.txt); it no longer runs against the current library
 # round 3: BN finalize geometry, experimental libraries (MAUV_LIB): v1 = backward partial blocks
 # capped at 256 per group (was 1024: the finalize walks 4x fewer partials), v2 = forward statistics
 # segments of 128 partials (was 512: 4x more finalize blocks, shorter chains), v3 = both.
