@@ -1,1 +1,5 @@
-"""Multimodal_AUV.train (mauv drop-in)."""
+"""Multimodal_AUV.train (mauv drop-in); the reference's other train modules resolve through
+MAUV_REFERENCE_PKG (see the top package)."""
+from .. import _extend_path
+
+__path__ = _extend_path(__path__, "train")
