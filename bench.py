@@ -330,6 +330,7 @@ def main():
     from mauv.models import define_models, DEFAULT_PRIOR
     from mauv.train import mc_train_step
     from mauv.predict import mc_statistics, mc_chunk
+    from mauv.engine import root_state
 
     torch.manual_seed(0)
     model = define_models(None, 7, DEFAULT_PRIOR)["multimodal_model"].to(dev)
@@ -349,6 +350,20 @@ def main():
     def step():
         return mc_train_step(model, (x, b, s), y, crit, opt, args.num_mc, args.batch, kl_w)
 
+    # world > 1: the gradient exchange's caller-stream time (waits on the trunk slices issued
+    # during the backward + the rest of the arena + the 1/world scale) = exposed all-reduce
+    comm_events = []
+    if world > 1:
+        _allreduce = model.allreduce_grads
+
+        def allreduce_timed():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _allreduce()
+            e1.record()
+            comm_events.append((e0, e1))
+        model.allreduce_grads = allreduce_timed
+
     def barrier():
         if world > 1:
             dist.barrier()
@@ -357,6 +372,8 @@ def main():
         step()
     barrier()
     torch.cuda.synchronize()
+    comm_events.clear()
+    c0 = (model.n_buckets, model.n_overlapped, model.elems_reduced) if world > 1 else None
     t0 = time.perf_counter()
     for i in range(args.steps):
         step()
@@ -365,10 +382,29 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    comm = None
     if world > 1:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
+        per_rank = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(per_rank, torch.tensor([dt], dtype=torch.float64, device=dev))
+        per_rank = [float(t.item()) for t in per_rank]
+        dt = max(per_rank)
+        nb, no, ne = (model.n_buckets - c0[0], model.n_overlapped - c0[1],
+                      model.elems_reduced - c0[2])
+        esz = 2 if args.grad_exchange == "bf16" else 4
+        exposed = [a.elapsed_time(b) for a, b in comm_events]
+        comm = {"backend": args.backend + (" (RCCL)" if args.backend == "nccl" else ""),
+                "exchange_dtype": args.grad_exchange,
+                "grad_bytes_per_step": int(ne * esz / args.steps),
+                "arena_values": int(root_state(model.module).arena.numel),
+                "buckets_per_step": round(nb / args.steps, 2),
+                "bucket_bytes": int(model.bucket_elems * esz),
+                "overlapped_trunk_slices_per_step": round(no / args.steps, 2),
+                "exposed_allreduce_ms_per_step": round(sum(exposed) / max(len(exposed), 1), 3),
+                "step_ms_per_rank_min": round(min(per_rank) / args.steps * 1e3, 2),
+                "step_ms_per_rank_max": round(max(per_rank) / args.steps * 1e3, 2),
+                "note": "exposed = caller-stream time of allreduce_grads (waits on the trunk "
+                        "slices all-reduced during the backward, the remaining buckets, the "
+                        "1/world scale), HIP events over the timed steps"}
     triplets_s = args.batch * world * args.steps / dt
     from mauv import ops
     f32_math = ops.f32_math()
@@ -435,11 +471,19 @@ def main():
         # headline does not cover, and main.py:310's num_mc=12 at the headline shape; same
         # model, optimiser and trunk precision as the headline.  Each leg reports its peak
         # HBM; a leg that does not fit is reported, not fatal.
+        # BASELINE.md row 5 states configs[4] in bf16: its two sonar legs also run with bf16
+        # trunks (the headline precision's legs stay beside them)
+        from mauv.engine import set_precision
         sweep = {}
-        legs = [(f"sonar{S}", args.sweep_batch, S, args.num_mc) for S in (128, 512)]
-        legs.append(("num_mc12", args.batch, args.sonar, 12))
-        for name, Bs, S, nmc in legs:
+        legs = [(f"sonar{S}", args.sweep_batch, S, args.num_mc, args.dtype) for S in (128, 512)]
+        legs.append(("num_mc12", args.batch, args.sonar, 12, args.dtype))
+        if args.dtype != "bf16":
+            legs += [(f"sonar{S}_bf16", args.sweep_batch, S, args.num_mc, "bf16")
+                     for S in (128, 512)]
+        core = model.module if world > 1 else model
+        for name, Bs, S, nmc, ldt in legs:
             progress(f"train_sweep {name}")
+            set_precision(core, torch.bfloat16 if ldt == "bf16" else None)
             opt.zero_grad(set_to_none=True)
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
@@ -457,12 +501,13 @@ def main():
                                "ms_per_step": round(ts / args.leg_steps * 1e3, 2),
                                "steps": args.leg_steps,
                                "batch_per_gpu": Bs, "sonar_px": S, "optical_px": args.optical,
-                               "num_mc": nmc, "dtype": args.dtype,
+                               "num_mc": nmc, "dtype": ldt,
                                "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)}
             except torch.OutOfMemoryError as e:
                 sweep[name] = {"error": "out of memory", "detail": str(e)[:200]}
             finally:
                 xs_ = bs_ = ss_ = ys_ = None
+        set_precision(core, torch.bfloat16 if args.dtype == "bf16" else None)
         opt.zero_grad(set_to_none=True)
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
@@ -577,7 +622,7 @@ def main():
             "f32_math": f32_math if args.dtype == "fp32" else None,
             "fp32_exact_mfma": exact,
             "inference": infer, "infer_sweep": infer_sweep, "bf16_train": bf16,
-            "train_sweep": sweep, "roofline": roof,
+            "train_sweep": sweep, "roofline": roof, "comm": comm,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

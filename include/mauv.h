@@ -222,6 +222,21 @@ typedef struct MauvAdamEntry {
 } MauvAdamEntry;
 int mauv_adam_step(const MauvAdamEntry* table, int n, float lr, float beta1, float beta2,
                    float eps, float weight_decay, long long step, hipStream_t stream);
+/* The step decision of train/multimodal.py:133-145 (skip on a non-finite loss; skip the step
+ * AND the zero_grad on non-finite gradients; otherwise step + zero_grad) taken on the device, so
+ * a training step has no host round trip.  64-byte device struct; the caller zero-initialises
+ * it, writes ok_loss (1 = the loss is finite on every rank) before the backward and counts
+ * the gradient arena's non-finite elements into `nonfinite` after it.  mode / step_size /
+ * bc2_sqrt are written by mauv_adam_step_gated; step is the Adam step count (bias correction);
+ * poisoned = the arena still holds a skipped step's non-finite gradients. */
+typedef struct MauvStepGate {
+  int ok_loss, nonfinite, poisoned, mode;
+  int step, stepped, skipped_loss, skipped_grad;
+  float step_size, bc2_sqrt;
+  int reserved[6];
+} MauvStepGate;
+int mauv_adam_step_gated(const MauvAdamEntry* table, int n, float lr, float beta1, float beta2,
+                         float eps, float weight_decay, MauvStepGate* gate, hipStream_t stream);
 
 /* ---- BatchNorm2d (training mode, per MC group) + residual + ReLU (bn.hip) ---------------
  * torchvision Bottleneck bn1..3 / downsample.1 / stem bn1 in .train() for every MC pass

@@ -52,6 +52,7 @@ SIGNATURES = {
     "mauv_philox_raw": [U64, U64, U32, I, P, P, P],
     # adam.hip
     "mauv_adam_step": [P, I, F, F, F, F, F, LL, P],
+    "mauv_adam_step_gated": [P, I, F, F, F, F, F, P, P],
     # bn.hip
     "mauv_bn_workspace_floats": [I, LL, I],
     "mauv_bn_fwd_train": [P, I, LL, I, P, P, P, P, F, F, P, P, P, P, P, P, I, P, P],

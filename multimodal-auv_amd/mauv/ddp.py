@@ -58,6 +58,8 @@ class DistributedMC(nn.Module):
         self._done = []         # [start, end) arena ranges they cover
         self._kl_mark = 0
         self.n_overlapped = 0   # trunk slices all-reduced from the backward hook (cumulative)
+        self.n_buckets = 0      # all-reduce calls of the gradient exchange (cumulative)
+        self.elems_reduced = 0  # arena values exchanged (cumulative)
         if overlap and self.world > 1:
             st.grad_ready_hook = self._trunk_ready
 
@@ -98,7 +100,9 @@ class DistributedMC(nn.Module):
             buf[start:end].copy_(flat[start:end])     # round to bf16 on the current stream
             self._lp_ranges.append((start, end))
         works = []
+        self.elems_reduced += end - start
         for off in range(start, end, self.bucket_elems):
+            self.n_buckets += 1
             w = dist.all_reduce(buf[off:min(end, off + self.bucket_elems)], group=self.group,
                                 async_op=async_op)
             if async_op:
@@ -138,6 +142,12 @@ class DistributedMC(nn.Module):
         t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
         return bool(t.item())
+
+    def all_ranks_device(self, flag):
+        """In-place MIN of a device int32 flag over the group, stream-ordered (no host sync):
+        the device-gated training step (mauv.train.mc_train_step) skips on every rank or none."""
+        if self.world > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
 
     def sum_ranks(self, values):
         """Element-wise sum of a list of floats over the ranks (one float64 all-reduce)."""

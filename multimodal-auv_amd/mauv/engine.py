@@ -219,6 +219,9 @@ class _Runner:
         key = (id(m), name)
         if key not in cache:
             cache[key] = fn(m, name, self.G)
+            # the layer's latest draw, for a reference-mode rho-gradient of an EARLIER forward
+            # (sequential grad-enabled calls before one backward, the noise Examples' loop)
+            self.st.__dict__.setdefault("eps_last", {})[key] = (self.s0, cache[key])
         return cache[key]
 
     # ---- Bayesian parameter sampling (mauv_reparam_sample) ----
@@ -239,8 +242,13 @@ class _Runner:
         if not mu.requires_grad:
             return
         fixed = self.st.offset - 1 if self.st.rho_grad == "reference" else -1
-        ops.reparam_bwd(dw, splits, mu, rho, mu.grad, rho.grad, self.G, self.st.seed, self.s0,
-                        self.st.layer_id(m, bias), Cout, Cin, RS, eps=self._eps(m, name),
+        eps, s0 = self._eps(m, name), self.s0
+        if eps is not None and fixed >= 0 and not s0 <= fixed < s0 + self.G:
+            # explicit epsilons whose last draw belongs to a later forward: its rows
+            ls0, leps = self.st.eps_last[(id(m), name)]
+            eps, s0 = leps[fixed - ls0:fixed - ls0 + 1], fixed
+        ops.reparam_bwd(dw, splits, mu, rho, mu.grad, rho.grad, self.G, self.st.seed, s0,
+                        self.st.layer_id(m, bias), Cout, Cin, RS, eps=eps,
                         dw_gstride=dw_gstride, dw_sstride=dw_sstride, fixed_sample=fixed,
                         dw_cin=dw_cin)
 
@@ -406,6 +414,16 @@ class TrunkRunner(_Runner):
                        x_bn=x_bn, stats=None if part is None else part[:3], alg_cin=Cin)
         rec = (conv, x, x_strides, x_bn, w, B, H, W) if self.save else None
         return y, rec, part
+
+    @staticmethod
+    def _masked_addend_ok(rec):
+        """A 16-bit identity block's conv1 data gradient takes its residual addend under the
+        block output's ReLU bits only in the pipelined kernel: Cout % 64 == 0 and every operand
+        within its 31-bit buffer offsets (conv_pipe16_launch); otherwise dres is materialised."""
+        conv, B, H, W = rec[0], rec[5], rec[6], rec[7]
+        lim = 0x7fff0000 // 2
+        return conv.out_channels % 64 == 0 and \
+            B * H * W * max(conv.in_channels, conv.out_channels) <= lim
 
     def _conv_bwd(self, rec, dy, need_dx=True, addend=None, dx=None, accumulate=False,
                   addend_mask=None):
@@ -631,7 +649,7 @@ class TrunkRunner(_Runner):
             r1, s1, r2, s2, r3, s3, rd, sd = self.recs.pop()
             # the residual gradient: dres = da * mask3, kept implicit when bn3 has mask bits
             rmask = s3.mask if RES_MASK and s3.mask is not None and \
-                (rd is not None or self.dt == torch.float32 or r1[0].out_channels % 64 == 0) \
+                (rd is not None or self.dt == torch.float32 or self._masked_addend_ok(r1)) \
                 else None
             dy3, dres = self._bn_bwd(s3, da, want_dres=rmask is None)
             if rmask is not None:

@@ -13,6 +13,7 @@ Numerics: like the reference (predictors.py:55) the MC passes run under
 (activations and sampled weights 16-bit, fp32 accumulation and BN statistics); the fusion head
 and every reduction stay fp32/fp64.
 """
+import collections
 import csv
 import logging
 import math
@@ -101,9 +102,33 @@ class _GraphedChunk:
         return self.out
 
 
+_GRAPH_CACHE_MAX = 2   # captured chunk graphs kept per model (each holds a private pool)
+
+
+def _graph_state_key(base, st):
+    """What a capture bakes in besides the input shapes: the Philox seed (a kernel scalar), the
+    BN mode / momentum / eps of every BatchNorm (batch statistics + running-stat updates vs
+    eval parameters) and the storage of every parameter and buffer (a ``p.data = ...`` rebind,
+    bayesian-torch's MOPED idiom, leaves a replay reading freed memory)."""
+    bns = st.plist("graph_bns", lambda: [m for m in base.modules()
+                                         if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)])
+    tensors = st.plist("graph_tensors", lambda: list(base.parameters()) + list(base.buffers()))
+    return (st.seed, base.training, tuple((m.training, m.momentum, m.eps) for m in bns),
+            hash(tuple(t.data_ptr() for t in tensors)))
+
+
+def drop_graphs(model):
+    """Release the captured inference graphs of ``model`` (and their memory pools)."""
+    base = unwrap(model)
+    base.__dict__.pop("_mauv_graphs", None)
+    base.__dict__.pop("_mauv_graph_seen", None)
+
+
 def _chunk_forward(core, inputs, G):
     """core.mc_forward(*inputs, G), through a captured HIP graph for small chunks once a shape
-    has run eagerly (the first run also loads every kernel the capture records)."""
+    has run eagerly (the first run also loads every kernel the capture records).  The cache is
+    keyed on the shapes and on everything the capture fixes (``_graph_state_key``) and keeps the
+    ``_GRAPH_CACHE_MAX`` most recently used graphs."""
     if not GRAPH_INFER or torch.is_grad_enabled() or not inputs[0].is_cuda:
         return core.mc_forward(*inputs, G)
     base = unwrap(core)
@@ -116,15 +141,18 @@ def _chunk_forward(core, inputs, G):
     if per * G > _GRAPH_MAX_BYTES:
         return base.mc_forward(*inputs, G)
     key = (tuple(tuple(t.shape) for t in inputs), tuple(t.dtype for t in inputs), G, dt,
-           inputs[0].device)
-    cache = base.__dict__.setdefault("_mauv_graphs", {})
+           inputs[0].device, _graph_state_key(base, st))
+    cache = base.__dict__.setdefault("_mauv_graphs", collections.OrderedDict())
     g = cache.get(key)
     if g is None:
-        if key in base.__dict__.setdefault("_mauv_graph_seen", set()):
-            g = cache[key] = _GraphedChunk(base, inputs, G)
-        else:
-            base.__dict__["_mauv_graph_seen"].add(key)
+        seen = base.__dict__.setdefault("_mauv_graph_seen", set())
+        if key not in seen:
+            seen.add(key)
             return base.mc_forward(*inputs, G)
+        while len(cache) >= _GRAPH_CACHE_MAX:
+            cache.popitem(last=False)
+        g = cache[key] = _GraphedChunk(base, inputs, G)
+    cache.move_to_end(key)
     return g(inputs)
 
 

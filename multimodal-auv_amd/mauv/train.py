@@ -105,11 +105,77 @@ def mc_loss(model, inputs_tuple, labels, criterion, num_mc, batch_size, kl_w):
     return ce + scaled_kl, output, predicted, ce, scaled_kl
 
 
+def _step_gate(model, optimizer, loss):
+    """The device MauvStepGate when the batch can be decided on the device: a mauv engine model
+    whose gradients live in its arena, stepped by FusedAdam over exactly its parameters."""
+    from .optim import FusedAdam
+    if not isinstance(optimizer, FusedAdam) or not loss.is_cuda:
+        return None
+    st = unwrap(model).__dict__.get("_mauv_state")
+    if st is None or not all(p.requires_grad for p in st.params):
+        return None
+    return optimizer.gate(st.params, loss.device)
+
+
+def _count_nonfinite(model, counter):
+    """Add the number of non-finite gradient blocks of the arena into the device ``counter``
+    (the fused form of multimodal.py:141's per-tensor isnan/isinf scan, no host sync)."""
+    st = unwrap(model).__dict__["_mauv_state"]
+    from . import ops
+    ops.nonfinite_count(st.arena.flat, counter)
+
+
+_MAX_STEPS_AHEAD = 2
+
+
+def _throttle(model):
+    """With no host round trip in a step the host could enqueue steps without bound; it stays
+    at most ``_MAX_STEPS_AHEAD`` steps ahead of the GPU (it waits for the end of the step
+    before the previous one, so the GPU always has a whole queued step while the host works)."""
+    st = unwrap(model).__dict__.get("_mauv_state")
+    if st is None or not torch.cuda.is_available():
+        return None
+    q = st.__dict__.setdefault("step_events", [])
+    while len(q) >= _MAX_STEPS_AHEAD:
+        q.pop(0).synchronize()
+    return q
+
+
 def mc_train_step(model, inputs_tuple, labels, criterion, optimizer, num_mc, batch_size, kl_w):
     """One reference training batch (multimodal.py:104-146): MC forward, KL, CE, NaN/Inf loss
-    skip, backward, NaN/Inf gradient guard, optimizer step + zero_grad."""
+    skip, backward, NaN/Inf gradient guard, optimizer step + zero_grad.
+
+    For a mauv model stepped by FusedAdam the two skip decisions are taken on the device
+    (``MauvStepGate``, adam.hip): the finite-loss flag is written (and MIN-reduced over the
+    ranks of a DistributedMC job) before the backward, the gradient arena's non-finite count
+    after it, and the Adam kernel steps + zeroes the gradients, takes the batch's gradients
+    back out (non-finite loss: the reference never ran that backward), or leaves the arena
+    alone (non-finite gradients: no zero_grad, multimodal.py:141-145).  Nothing here waits on
+    the GPU; ``ok_loss`` / ``stepped`` come back as device tensors.  Other models and
+    optimizers take the host-decided path (None for a skipped batch)."""
+    inflight = _throttle(model)
     loss, output, predicted, ce, scaled_kl = mc_loss(model, inputs_tuple, labels, criterion,
                                                      num_mc, batch_size, kl_w)
+    gate = _step_gate(model, optimizer, loss)
+    if gate is not None:
+        from .optim import G_OK_LOSS, G_NONFINITE, G_STEPPED
+        ok = gate[G_OK_LOSS:G_OK_LOSS + 1]
+        ok.copy_(torch.isfinite(loss.detach()).reshape(1))
+        if hasattr(model, "all_ranks_device"):
+            model.all_ranks_device(ok)
+        loss.backward()
+        if hasattr(model, "allreduce_grads"):  # mauv.ddp.DistributedMC: RCCL all-reduce
+            model.allreduce_grads()
+        _count_nonfinite(model, gate[G_NONFINITE:G_NONFINITE + 1])
+        optimizer.step_gated(gate)
+        flags = gate[:G_STEPPED + 1].clone() != 0   # this batch's decisions (device)
+        if inflight is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            inflight.append(ev)
+        return dict(loss=loss.detach(), output=output, predicted=predicted, ce=ce.detach(),
+                    scaled_kl=scaled_kl.detach(), ok_loss=flags[G_OK_LOSS],
+                    stepped=flags[G_STEPPED])
     if not _all_ranks(model, bool(torch.isfinite(loss).item())):
         logging.warning(f"Skipping batch due to NaN/Inf loss: {loss}")
         return None
@@ -124,6 +190,49 @@ def mc_train_step(model, inputs_tuple, labels, criterion, optimizer, num_mc, bat
         logging.warning("Skipping optimizer step due to NaN/Inf gradients")
     return dict(loss=loss.detach(), output=output, predicted=predicted, ce=ce.detach(),
                 scaled_kl=scaled_kl.detach(), stepped=stepped)
+
+
+class _TrainEpoch:
+    """Per-batch bookkeeping of train_multimodal_model (multimodal.py:133-166) without a host
+    round trip on the batch just issued: a batch's loss, correct count and skip decisions are
+    read when the NEXT batch has been issued (the GPU is then still busy), so the host never
+    idles the GPU.  Batches whose loss was non-finite are not counted or logged, exactly as the
+    reference's ``continue``; the running figures, TensorBoard scalars and log lines come out in
+    the reference's order and values."""
+
+    def __init__(self, epoch, sum_writer):
+        self.epoch, self.writer = epoch, sum_writer
+        self.total_loss, self.correct, self.total = 0.0, 0, 0
+        self.last = None
+        self.pending = []
+
+    def add(self, i, r, labels):
+        keep = ("loss", "ce", "scaled_kl", "ok_loss", "stepped")
+        r = dict({k: r[k] for k in keep if k in r},
+                 n_correct=(r["predicted"] == labels).sum(), n=labels.size(0))
+        self.pending.append((i, r))
+        if len(self.pending) > 1:
+            self._settle(self.pending.pop(0))
+
+    def flush(self):
+        while self.pending:
+            self._settle(self.pending.pop(0))
+
+    def _settle(self, item):
+        i, r = item
+        if "ok_loss" in r and not bool(r["ok_loss"]):
+            logging.warning(f"Skipping batch {i} due to NaN/Inf loss: {r['loss']}")
+            return
+        if not bool(r["stepped"]):
+            logging.warning("Skipping optimizer step due to NaN/Inf gradients")
+        lv = r["loss"].item()
+        self.total_loss += lv
+        self.correct += int(r["n_correct"].item())
+        self.total += r["n"]
+        self.last = r
+        self.writer.add_scalar("Loss/train", lv, i)
+        logging.info(f"[Epoch {self.epoch} | Batch {i}] Loss: {lv:.4f}, "
+                     f"Accuracy: {self.correct / max(self.total, 1):.4f}")
 
 
 def loop_device(model, device):
@@ -212,23 +321,16 @@ def train_multimodal_model(multimodal_model, dataloader, criterion, optimizer, e
                 w.writerow(["Epoch", "Model type", "Loss", "Accuracy", "lr", "kl loss",
                             "cross entropy loss", "SSS Patch Type", "Channel Patch Type"])
             kl_w = kl_weight_for(epoch, total_num_epochs)
-            total_loss, correct, total = 0.0, 0, 0
-            last = None
+            ep = _TrainEpoch(epoch, sum_writer)
             for i, batch in enumerate(dataloader):
                 inputs, labels, bathy, sss = _batch_to(batch, device, bathy_patch_type,
                                                        sss_patch_type)
                 r = mc_train_step(multimodal_model, (inputs, bathy, sss), labels, criterion,
                                   optimizer, num_mc, dataloader.batch_size, kl_w)
-                if r is None:
-                    continue
-                last = r
-                lv = r["loss"].item()
-                total_loss += lv
-                correct += int((r["predicted"] == labels).sum().item())
-                total += labels.size(0)
-                sum_writer.add_scalar("Loss/train", lv, i)
-                logging.info(f"[Epoch {epoch} | Batch {i}] Loss: {lv:.4f}, "
-                             f"Accuracy: {correct / max(total, 1):.4f}")
+                if r is not None:
+                    ep.add(i, r, labels)
+            ep.flush()
+            total_loss, correct, total, last = ep.total_loss, ep.correct, ep.total, ep.last
             # DistributedMC: the epoch's figures over every rank's batches
             total_loss, correct, total = sum_ranks(multimodal_model, [total_loss, correct, total])
             train_accuracy = correct / total

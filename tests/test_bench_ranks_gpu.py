@@ -41,7 +41,13 @@ def test_bench_world2_gloo_one_gpu():
     assert d["config"]["parallelism"] == "dp2" and d["value"] > 0
     assert d["bf16_train"]["value"] > 0
     assert d["inference"]["sharding"] == "mc" and d["inference"]["value"] > 0
-    for leg in ("sonar128", "sonar512", "num_mc12"):
+    c = d["comm"]                                      # the multi-rank line explains itself
+    assert c["exchange_dtype"] == "fp32" and c["buckets_per_step"] >= 1
+    assert c["grad_bytes_per_step"] == 4 * c["arena_values"]
+    assert c["overlapped_trunk_slices_per_step"] >= 1
+    assert c["exposed_allreduce_ms_per_step"] > 0
+    assert 0 < c["step_ms_per_rank_min"] <= c["step_ms_per_rank_max"] == d["ms_per_step"]
+    for leg in ("sonar128", "sonar512", "num_mc12", "sonar128_bf16", "sonar512_bf16"):
         assert d["train_sweep"][leg]["value"] > 0, d["train_sweep"]
     for leg in ("sonar128", "sonar512", "main_py_b8_mc12"):
         assert d["infer_sweep"][leg]["sharding"] == "mc" and d["infer_sweep"][leg]["value"] > 0

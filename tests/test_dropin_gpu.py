@@ -209,8 +209,10 @@ def test_g6_evaluate_and_predict(tmp_path, monkeypatch):
 def test_g6_predict_under_autocast(tmp_path):
     """The drop-in predictor autocasts like predictors.py:55 (f16 trunks on the GPU): classes
     equal to the reference's fp32 golden, aleatoric entropy within SURVEY §8c's 16-bit row
-    (1e-2), MC variance within 1e-4 absolute (the golden values are ~1e-6: f16 rounding of
-    the trunk activations is visible there, so only its scale is checked)."""
+    (1e-2), and the MC variance (golden values ~1e-6, where f16 rounding of the trunk
+    activations is visible) as close to the fp32 golden as the reference's own scheme gets:
+    the oracle under torch.autocast(f16) on the GPU with the same weights and epsilons —
+    max |HIP - golden| <= 2x max |autocast - golden| (+1e-9)."""
     import Multimodal_AUV.inference.predictors as pr
     from Multimodal_AUV.models.model_utils import define_models
     o = _oracle_trained_g5()
@@ -239,8 +241,26 @@ def test_g6_predict_under_autocast(tmp_path):
     rows = list(csv.reader(open(csvp)))
     for got, want in zip(rows[1:], G["g6_predict_csv"][1:]):
         assert got[0] == want[0] and int(got[1]) == int(want[1])
-        assert abs(float(got[2]) - float(want[2])) <= 1e-4
         assert abs(float(got[3]) - float(want[3])) <= 1e-2
+    # the reference's scheme on the same weights / epsilon stream: oracle under f16 autocast
+    from oracle import bayes_ref
+    oc = copy.deepcopy(o).cuda()
+    bayes_ref.set_eps_source(eps_generator_source(SEED_EPS + 3))
+    try:
+        with torch.autocast("cuda", dtype=torch.float16):
+            var_ac = torch.cat([loops_ref.predict_batch(oc, b["main_image"].cuda(),
+                                                        b["bathy_image"].cuda(),
+                                                        b["sss_image"].cuda(), 4)[1].cpu()
+                                for b in batches]).double()
+    finally:
+        bayes_ref.set_eps_source(None)
+    var_gold = torch.tensor([float(r[2]) for r in G["g6_predict_csv"][1:]], dtype=torch.float64)
+    var_hip = torch.tensor([float(r[2]) for r in rows[1:]], dtype=torch.float64)
+    dh = (var_hip - var_gold).abs().max().item()
+    da = (var_ac - var_gold).abs().max().item()
+    print(f"\nf16 predictor variance vs fp32 golden (|golden| max {var_gold.abs().max():.3e}): "
+          f"HIP {dh:.3e}, torch-autocast {da:.3e}")
+    assert dh <= 2 * da + 1e-9, (dh, da)
 
 
 def test_g7_train_unimodal_model(tmp_path):

@@ -178,17 +178,81 @@ def test_mc_batched_equals_sequential():
     assert not torch.equal(batched[0], batched[1])  # samples differ
 
 
-def test_unimodal_resnet50custom_parity():
+@pytest.mark.parametrize("S_opt,S_son,B,N", [(64, 64, 2, 3), (224, 256, 2, 2)])
+def test_noise_examples_sequential_grad_pattern(S_opt, S_son, B, N):
+    """The noise Examples' fork of the training loop (Example training with image noise.py:
+    282-302): N grad-enabled ``model(x, b, s)`` calls, ``get_kl_loss`` after each, the mean of
+    the stacked logits and KLs, ``optimizer.zero_grad()``, ONE backward over the N graphs.  On
+    the drop-in every call is a separate single-sample engine forward; the N graphs' gradients
+    (with bayesian-torch's aliased rho-gradient: every pass sees the LAST draw) must match the
+    oracle's as the batched path's do."""
+    from mauv.engine import root_state
+    from mauv.kl import get_kl_loss
+    o, m = build_pair()
+    o_pre = copy.deepcopy(o)
+    batch = make_batches(SEED_DATA + 2, 1, B=B, S_opt=S_opt, S_son=S_son)[0]
+    x, b, s, y = batch["main_image"], batch["bathy_image"], batch["sss_image"], batch["label"]
+    kl_w = 0.5
+
+    def script_loss(model, kl_fn, xs, dt=None):
+        outs, kls = [], []
+        for _ in range(N):
+            outs.append(model(*xs))
+            kls.append(kl_fn(model))
+        output = torch.mean(torch.stack(outs), dim=0)
+        scaled_kl = torch.mean(torch.stack(kls), dim=0) / B * kl_w
+        loss = F.cross_entropy(output, y.to(output.device)) + scaled_kl
+        for p in model.parameters():      # optimizer.zero_grad() (:301)
+            p.grad = None
+        loss.backward()
+        return torch.stack(outs), loss
+
+    bridge = EpsBridge(o, m, 31)
+    with bridge:
+        o_logits, loss_o = script_loss(o, bayes_ref.get_kl_loss, (x, b, s))
+    bridge.collect()
+    o64, _ = oracle64(o_pre, bridge.store, lambda mm: script_loss(
+        mm, bayes_ref.get_kl_loss, (x.double(), b.double(), s.double())))
+    root_state(m).eps_provider = _SequentialProvider(bridge)
+    logits, loss = script_loss(m, get_kl_loss, _cuda(x, b, s))
+    _assert_close(logits, o_logits)
+    assert abs(loss.item() - loss_o.item()) <= 1e-4 * abs(loss_o.item())
+    _assert_grads_as_accurate(list(m.parameters()), list(o.parameters()), list(o64.parameters()))
+
+
+class _SequentialProvider:
+    """EpsBridge's epsilons served one pass per engine call (sequential single-sample
+    forwards consume the oracle's passes in order)."""
+
+    def __init__(self, bridge):
+        self.bridge, self.used = bridge, {}
+
+    def __call__(self, module, name, G):
+        key = (self.bridge.m_names[id(module)], name)
+        i = self.used.get(key, 0)
+        self.used[key] = i + G
+        return torch.stack(self.bridge.store[key][i:i + G]).cuda().contiguous()
+
+
+@pytest.mark.parametrize("S,B,N", [
+    (64, 2, 2),
+    (224, 8, 5),    # BASELINE configs[0] at its own shape (train/unimodal.py:127-146)
+])
+def test_unimodal_resnet50custom_parity(S, B, N):
+    """Bayesian ResNet50Custom(3, 7) (configs[0]'s model): one MC training step — logits,
+    loss, gradients against the float64 oracle — at 64 px and at configs[0]'s 224 px, B=8,
+    num_mc=5."""
     from mauv.engine import root_state
     from mauv.kl import get_kl_loss
     from mauv import mchead
     o, m = build_pair(key="image_model")
-    batch = make_batches(SEED_DATA, 1, B=2, S_opt=64, S_son=64)[0]
+    o_pre = copy.deepcopy(o)
+    batch = make_batches(SEED_DATA, 1, B=B, S_opt=S, S_son=64)[0]
     x, y = batch["main_image"], batch["label"]
 
     def oracle_loss(model, dt=torch.float32):
-        lg = torch.stack([model(x.to(dt)) for _ in range(2)])
-        loss = F.cross_entropy(lg.mean(0), y) + 0.25 * bayes_ref.get_kl_loss(model) / 2
+        lg = torch.stack([model(x.to(dt)) for _ in range(N)])
+        loss = F.cross_entropy(lg.mean(0), y) + 0.25 * bayes_ref.get_kl_loss(model) / B
         loss.backward()
         return lg, loss
 
@@ -196,12 +260,12 @@ def test_unimodal_resnet50custom_parity():
     with bridge:
         o_logits, loss_o = oracle_loss(o)
     bridge.collect()
-    o64, _ = oracle64(o, bridge.store, lambda mm: oracle_loss(mm, torch.float64))
+    o64, _ = oracle64(o_pre, bridge.store, lambda mm: oracle_loss(mm, torch.float64))
     root_state(m).eps_provider = bridge.provider
-    logits = m.mc_forward(x.cuda(), 2)
+    logits = m.mc_forward(x.cuda(), N)
     _assert_close(logits, o_logits)
     ce, _, _ = mchead.mc_mean_ce(logits, y.cuda())
-    loss = ce + 0.25 * get_kl_loss(m) / 2
+    loss = ce + 0.25 * get_kl_loss(m) / B
     assert abs(loss.item() - loss_o.item()) <= 1e-4 * abs(loss_o.item())
     loss.backward()
     _assert_grads_as_accurate(list(m.parameters()), list(o.parameters()), list(o64.parameters()))
@@ -411,3 +475,49 @@ def test_graphed_small_chunk_inference_equals_eager():
         for k in e:
             assert torch.equal(e[k], gr[k]), k
     assert not torch.equal(runs[True][2]["var"], runs[True][3]["var"])   # fresh samples
+
+
+def test_graphed_chunk_follows_seed_mode_and_rebinds():
+    """A captured chunk bakes in the Philox seed, the BN mode and the parameter storage
+    (ADVICE r3): changing any of them between replays re-captures, so the graphed statistics
+    stay equal to the eager ones of the same state; the cache keeps at most two graphs."""
+    from mauv import predict
+    from mauv.engine import root_state
+    from mauv.predict import mc_statistics
+    _, m = build_pair()
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(8, 3, 64, 64, generator=g).cuda()
+    b = torch.rand(8, 3, 64, 64, generator=g).cuda()
+    s = torch.rand(8, 1, 64, 64, generator=g).cuda()
+    st = root_state(m)
+    prev = predict.GRAPH_INFER
+
+    def run(graph, seed, train):
+        predict.GRAPH_INFER = graph
+        st.seed, st.offset = seed, 0
+        m.train(train)
+        with torch.no_grad(), torch.autocast("cuda"):
+            return [{k: v.clone() for k, v in mc_statistics(m, x, b, s, 12).items()}
+                    for _ in range(3)]
+
+    try:
+        snap = {k: v.clone() for k, v in m.state_dict().items()}
+        states = [(11, True), (12, True), (12, False), (11, True)]
+        for i, (seed, train) in enumerate(states):
+            if i == 3:   # MOPED-style storage rebind of one parameter between replays
+                p = m.fc2.mu_weight
+                p.data = p.data.clone()
+                snap = {k: v.clone() for k, v in m.state_dict().items()}
+            m.load_state_dict(snap)
+            eager = run(False, seed, train)
+            m.load_state_dict(snap)
+            graphed = run(True, seed, train)
+            for e, gr in zip(eager, graphed):
+                for k in e:
+                    assert torch.equal(e[k], gr[k]), (seed, train, k)
+            assert len(m.__dict__["_mauv_graphs"]) <= 2
+    finally:
+        predict.GRAPH_INFER = prev
+        m.train()
+        predict.drop_graphs(m)
+    assert "_mauv_graphs" not in m.__dict__

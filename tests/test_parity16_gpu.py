@@ -18,7 +18,7 @@ predictor's statistics) as that scheme, within a stated margin.
       head's: HIP >= autocast - COS_MARGIN;
     - logits: max |HIP - fp64| <= 2x max |autocast - fp64|.
 * f16 predictor (the drop-in default path, ``multimodal_predict_and_save``'s maths) at B=64,
-  N=8 after a few training steps on the batch (``fit_model``: the class then depends on the
+  N=8 (64 / 128 px) and B=16, N=8 at 224 / 256 px after a few training steps on the batch (``fit_model``: the class then depends on the
   input; at random init every golden item is class 4): predictive variance and aleatoric uncertainty deviate from
   the fp32 oracle by at most 2x what torch-autocast deviates (max over items), and the class
   agrees with the fp32 oracle on >= 99 % of the items.
@@ -132,14 +132,17 @@ def test_train_step16_grads_vs_torch_autocast(dt, S_opt, S_son, B, N):
     assert dh <= max(2 * da, 1e-3)
 
 
-@pytest.mark.parametrize("S", [64, 128], ids=["64px", "128px"])
-def test_predictor_f16_vs_torch_autocast(S):
-    """The drop-in predictor's default path (f16 trunks under autocast, predictors.py:55)."""
+@pytest.mark.parametrize("S_opt,S_son,B,N", [(64, 64, 64, 8), (128, 128, 64, 8),
+                                              (224, 256, 16, 8)],
+                         ids=["64px", "128px", "224-256px"])
+def test_predictor_f16_vs_torch_autocast(S_opt, S_son, B, N):
+    """The drop-in predictor's default path (f16 trunks under autocast, predictors.py:55),
+    also at the configs[3] tile sizes (224 optical / 256 sonar)."""
     from mauv.engine import root_state
     from mauv.predict import mc_statistics
     o, m = build_pair()
-    B, N = 64, 8
-    batch = make_batches(SEED_DATA + 1, 1, B=B, S_opt=S, S_son=S)[0]
+    S = f"{S_opt}/{S_son}"
+    batch = make_batches(SEED_DATA + 1, 1, B=B, S_opt=S_opt, S_son=S_son)[0]
     x, b, s = batch["main_image"], batch["bathy_image"], batch["sss_image"]
     # train the model a few steps on this batch (random labels) so that its class depends on
     # the input, then give the oracle the trained state

@@ -1,0 +1,216 @@
+"""The training step's skip decisions taken on the device (adam.hip
+``MauvStepGate``): a non-finite loss skips the batch (multimodal.py:133-135), non-finite
+gradients skip the optimizer step AND the zero_grad (multimodal.py:141-145, so the arena keeps
+them), otherwise Adam steps and the gradients are zeroed.  The gated path (FusedAdam) is held
+against the host-decided reference path (torch.optim.Adam, the reference's own optimizer, with
+``.item()`` decisions) over a sequence with an injected NaN loss and an injected NaN gradient,
+single-rank and with two gloo ranks on one GPU; the steady-state gated step is checked to make
+no synchronising call (torch.cuda sync-debug mode)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+# batch kinds: "ok", "nan_loss" (one input pixel NaN), "nan_grad" (a NaN written into the
+# gradient arena after the backward, before the scan)
+SEQ = ["ok", "ok", "nan_loss", "ok", "nan_grad", "ok"]
+
+
+def _model(seed=0):
+    from mauv.models import define_models, DEFAULT_PRIOR
+    torch.manual_seed(seed)
+    m = define_models(None, 7, DEFAULT_PRIOR)["multimodal_model"].cuda()
+    return m
+
+
+def _batch(seed, kind, B=2, S=64):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, 3, S, S, generator=g)
+    b = torch.rand(B, 3, S, S, generator=g)
+    s = torch.rand(B, 1, S, S, generator=g)
+    y = torch.randint(0, 7, (B,), generator=g)
+    if kind == "nan_loss":
+        x[0, 0, 3, 3] = float("nan")
+    return x.cuda(), b.cuda(), s.cuda(), y.cuda()
+
+
+def _nan_into_head_grad(model):
+    """A NaN in the fusion head's last gradient (the arena slice DistributedMC reduces in
+    allreduce_grads, after the backward)."""
+    from mauv.engine import root_state
+    from mauv.kl import unwrap
+    ar = root_state(unwrap(model)).arena
+    ar.flat.narrow(0, ar.offsets[-1], 1).fill_(float("nan"))   # a kernel, no host copy
+
+
+class _InjectNaNGrad:
+    """Write a NaN into the arena between the backward and the non-finite scan, in both the
+    gated (``_count_nonfinite``) and the host-decided (``_grads_finite``) path — or, for a
+    DistributedMC model, before its all-reduce (so it reaches every rank, as a real one would)."""
+
+    def __init__(self, ddp=None):
+        import mauv.train as T
+        self.T, self.on, self.ddp = T, False, ddp
+        self.orig_count, self.orig_finite = T._count_nonfinite, T._grads_finite
+        if ddp is not None:
+            orig = ddp.allreduce_grads
+
+            def allreduce():
+                if self.on:
+                    _nan_into_head_grad(ddp)
+                return orig()
+            ddp.allreduce_grads = allreduce
+            return
+
+        def count(model, counter):
+            if self.on:
+                _nan_into_head_grad(model)
+            return self.orig_count(model, counter)
+
+        def finite(model):
+            if self.on:
+                _nan_into_head_grad(model)
+            return self.orig_finite(model)
+        T._count_nonfinite, T._grads_finite = count, finite
+
+    def close(self):
+        self.T._count_nonfinite, self.T._grads_finite = self.orig_count, self.orig_finite
+
+
+def _run(model, opt, seq, seed0, inject, sync_check_from=None):
+    from mauv.engine import root_state
+    from mauv.kl import unwrap
+    from mauv.train import mc_train_step
+    crit = torch.nn.CrossEntropyLoss()
+    st = root_state(unwrap(model))
+    flags = []
+    for i, kind in enumerate(seq):
+        x, b, s, y = _batch(seed0 + i, kind)
+        st.offset = 1000 * i          # same MC samples in both arms
+        inject.on = kind == "nan_grad"
+        if sync_check_from is not None and i >= sync_check_from:
+            torch.cuda.synchronize()
+            torch.cuda.set_sync_debug_mode("error")
+        try:
+            r = mc_train_step(model, (x, b, s), y, crit, opt, 2, 2, 1e-3)
+        finally:
+            torch.cuda.set_sync_debug_mode(0)
+        inject.on = False
+        if r is None:
+            flags.append((False, False))
+        else:
+            flags.append((bool(r.get("ok_loss", True)), bool(r["stepped"])))
+    torch.cuda.synchronize()
+    return flags
+
+
+def test_gated_step_matches_host_decided_reference():
+    from mauv.optim import FusedAdam, G_POISONED, G_STEP, G_SKIP_LOSS, G_SKIP_GRAD
+    from mauv.engine import root_state
+    inject = _InjectNaNGrad()
+    try:
+        ref = _model()
+        gat = _model()
+        root_state(gat).seed = root_state(ref).seed
+        opt_ref = torch.optim.Adam(ref.parameters(), lr=1e-3, weight_decay=1e-5)
+        opt_gat = FusedAdam(gat.parameters(), lr=1e-3, weight_decay=1e-5)
+        # steady-state gated steps (from the second one on) make no synchronising call
+        f_gat = _run(gat, opt_gat, SEQ, 10, inject, sync_check_from=1)
+        f_ref = _run(ref, opt_ref, SEQ, 10, inject)
+    finally:
+        inject.close()
+    want = [(True, True), (True, True), (False, False), (True, True), (True, False),
+            (True, False)]   # after the NaN gradient the arena stays poisoned (no zero_grad)
+    assert f_gat == want, f_gat
+    assert [s for _, s in f_ref] == [s for _, s in want]
+    for (n, p), q in zip(ref.named_parameters(), gat.parameters()):
+        d = (p.detach() - q.detach()).abs().max().item()
+        assert d <= 1e-6 + 1e-5 * p.detach().abs().max().item(), n
+    # the reference keeps the skipped step's non-finite gradients; so does the arena
+    assert not torch.isfinite(root_state(gat).arena.flat).all()
+    assert not all(torch.isfinite(p.grad).all() for p in ref.parameters())
+    gate = opt_gat._gate.cpu()
+    assert int(gate[G_STEP]) == 3 and int(gate[G_POISONED]) == 1
+    assert int(gate[G_SKIP_LOSS]) == 1 and int(gate[G_SKIP_GRAD]) == 2
+    # the optimizer's state_dict carries the device step count, torch.optim.Adam-compatible
+    sd = opt_gat.state_dict()
+    assert {float(v["step"]) for v in sd["state"].values()} == {3.0}
+    opt_ref.load_state_dict(sd)
+
+
+def test_nan_loss_batch_leaves_clean_arena_and_counts():
+    """A non-finite loss on a clean arena: the batch's gradients are taken back out (the
+    reference never ran that backward) and the drop-in loop does not count or log the batch."""
+    from mauv.optim import FusedAdam
+    from mauv.engine import root_state
+    from mauv.train import train_multimodal_model
+    from tests.helpers import ListLoader, NullWriter
+    m = _model(1)
+    opt = FusedAdam(m.parameters(), lr=1e-4)
+    batches = []
+    for i, kind in enumerate(["ok", "nan_loss", "ok"]):
+        x, b, s, y = _batch(40 + i, kind)
+        batches.append({"main_image": x.cpu(), "bathy_image": b.cpu(), "sss_image": s.cpu(),
+                        "label": y.cpu(), "patch_bathy": {}, "patch_sss": {}})
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        loss, acc = train_multimodal_model(m, ListLoader(batches, 2), torch.nn.CrossEntropyLoss(),
+                                           opt, 1, "cuda", "multimodal", 2, 2, NullWriter(),
+                                           csv_path=os.path.join(d, "t.csv"))
+    assert loss > 0 and 0.0 <= acc <= 1.0
+    assert torch.isfinite(root_state(m).arena.flat).all()
+    assert (root_state(m).arena.flat == 0).all()          # zeroed after the last step
+    assert int(opt._gate[4].item()) == 2                   # two steps taken
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "multimodal-auv_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from mauv.ddp import DistributedMC
+    from mauv.optim import FusedAdam
+    from mauv.engine import root_state
+    model = _model()
+    ddp = DistributedMC(model)
+    opt = FusedAdam(model.parameters(), lr=1e-3)
+    inject = _InjectNaNGrad(ddp)
+    # rank 0 alone sees the NaN loss (batch 2) and the NaN gradient (batch 4): every rank
+    # must skip both, and the ranks stay identical
+    seq = SEQ if rank == 0 else ["ok"] * len(SEQ)
+    try:
+        flags = _run(ddp, opt, seq, 10 + 100 * rank, inject)
+    finally:
+        inject.close()
+    flat = torch.cat([p.detach().flatten() for p in model.parameters()]).cpu()
+    torch.save((flags, flat, int(opt._gate[4].item())), os.path.join(q, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_gated_step_two_ranks_agree():
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        res = [torch.load(os.path.join(d, f"r{r}.pt")) for r in range(2)]
+    want = [(True, True), (True, True), (False, False), (True, True), (True, False),
+            (True, False)]
+    for flags, _, step in res:
+        assert flags == want, flags
+        assert step == 3
+    assert torch.equal(res[0][1], res[1][1])
