@@ -636,13 +636,7 @@ static void rows_geometry(long long M, int C, int& nblk, int& rpb) {
   nblk = (int)((M + r - 1) / r);
 }
 
-static bool use_rows(int C) {
-  static const int on = [] {
-    const char* e = getenv("MAUV_BN_ROWS");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  return on && C % 8 == 0 && C <= 2048;
-}
+static bool use_rows(int C) { return C % 8 == 0 && C <= 2048; }
 
 template <class S>
 static void launch_apply(const typename S::T* y, const float* scale, const float* shift,

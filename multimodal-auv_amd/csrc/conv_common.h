@@ -57,7 +57,8 @@ struct ConvArgs {
   // column n belongs to group n / cpg, channel n % cpg; outputs and BN statistics go to that
   // group's tensors ([G][M][cpg], [G][nblk][cpg]).  0 = off.
   int cpg;
-  // block order over the whole grid (1, default) or over blockIdx.x only (0): see conv_block_tile
+  // block order over the whole grid (1, what every launch sets) or over blockIdx.x only (0): see
+// conv_block_tile
   int xcd_grid;
 };
 
@@ -91,10 +92,6 @@ __device__ __forceinline__ void conv_block_tile(const ConvArgs& a, int& m0, int&
   n0 = __builtin_amdgcn_readfirstlane((L - (L / nN) * nN) * BN);
 }
 
-// MAUV_XCD_GRID (default 1): conv_block_tile's order
-int conv_xcd_grid();
-// MAUV_DGRAD_SHORT (default 1): short-K kernels for the data gradients (conv_pipe16.hip)
-int dgrad_short();
 
 // output element (row, col) of a FWD/DGRAD epilogue, relative to the block's group base
 __device__ __forceinline__ long long conv_out_index(const ConvArgs& a, long long orow, int col) {
@@ -156,7 +153,7 @@ bool conv_split_launch(int mode, const ConvArgs& a, int oneacc, hipStream_t st);
 // (DT_BF16 / DT_F16), WGRAD out stays fp32 slabs; false: shape not covered
 bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
 // 3x3 / stride-1 forwards and data gradients over 64 -> 64 channels through an LDS image of the
-// input rows (conv_halo16.hip); false: shape not covered (or MAUV_HALO3=0)
+// input rows (conv_halo16.hip); false: shape not covered (or mauv_set_halo3(0))
 bool conv_halo16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
 
 __device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int relu) {

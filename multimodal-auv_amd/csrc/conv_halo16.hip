@@ -178,12 +178,9 @@ void conv_halo16(const ConvArgs a) {
   epilogue16<MODE, DT, BM, BN, 1, NI, WGM, WGN, (HALO + 2 * WB) * 2>(a, acc2, smem, m0, n0, g);
 }
 
-// MAUV_HALO3 (default 1) / mauv_set_halo3: the 3x3 C = 64 forwards take this kernel
-static int g_halo3 = -1;
-static int halo3() {
-  if (g_halo3 < 0) { const char* e = getenv("MAUV_HALO3"); g_halo3 = e ? (atoi(e) != 0) : 1; }
-  return g_halo3;
-}
+// mauv_set_halo3 (default on): the 3x3 C = 64 forwards take this kernel
+static int g_halo3 = 1;
+static int halo3() { return g_halo3; }
 
 // rows of the flattened B*H image rows a BM-pixel tile touches, at most
 static int halo_rows(int BM, int W) { return BM % W == 0 ? BM / W : BM / W + 2; }

@@ -375,23 +375,9 @@ static void launch_pipe16(const ConvArgs& a, hipStream_t st) {
                      dim3(Waves16<BM, BN>::T), 0, st, a);
 }
 
-// forward launches with K <= MAUV_P16_SHORT_K (default 256; 0 = off) take the short-K kernels
-// (measured, tools/gpubatch_r2y.sh: f16 inference 11.03k -> 11.52k MC-samples/s, bf16
-// training 563 -> 582 triplets/s; K <= 64 alone: 11.30k / 585)
-static int short_k() {
-  static int k = -1;
-  if (k < 0) { const char* e = getenv("MAUV_P16_SHORT_K"); k = e ? atoi(e) : 256; }
-  return k;
-}
-
-
-// data-gradient launches take the short-K kernels when MAUV_DGRAD_SHORT is not 0 (default 1;
-// both conv families)
-int dgrad_short() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("MAUV_DGRAD_SHORT"); v = e ? atoi(e) : 1; }
-  return v;
-}
+// forward and data-gradient launches with K <= 256 take the short-K kernels (DESIGN.md §2.8b,
+// §2.15: f16 inference 11.03k -> 11.52k MC-samples/s, bf16 training 563 -> 582 triplets/s)
+constexpr int kShortK = 256;
 
 template <int MODE, int DT, bool XBN, bool STEM>
 static void pipe16_tiles(const ConvArgs& a, hipStream_t st) {
@@ -408,13 +394,13 @@ static void pipe16_tiles(const ConvArgs& a, hipStream_t st) {
   // short-K kernels: forwards, and data gradients without the BN-partials epilogue (K = the
   // parity class's taps x Cout)
   constexpr bool SHORT_OK = (MODE == FWD || MODE == DGRAD) && !STEM;
-  const bool use = MODE == FWD || dgrad_short();
+  constexpr bool use = true;
   if (bm == 64 && bn == 64) launch_pipe16<MODE, DT, 64, 64, XBN, STEM>(a, st);
   else if (bm == 64) launch_pipe16<MODE, DT, 64, 128, XBN, STEM>(a, st);
   else if (bn == 64) launch_pipe16<MODE, DT, 128, 64, XBN, STEM>(a, st);
-  else if (SHORT_OK && use && a.K == 64 && short_k() >= 64)
+  else if (SHORT_OK && use && a.K == 64)
     launch_pipe16<MODE, DT, 128, 128, XBN, STEM, SHORT_OK ? 1 : 0>(a, st);
-  else if (SHORT_OK && use && a.K > 0 && a.K <= short_k())
+  else if (SHORT_OK && use && a.K > 0 && a.K <= kShortK)
     launch_pipe16<MODE, DT, 128, 128, XBN, STEM, SHORT_OK ? 2 : 0>(a, st);
   else launch_pipe16<MODE, DT, 128, 128, XBN, STEM>(a, st);
 }
@@ -436,7 +422,7 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
   if (nx > lim || (mode != FWD && ny > lim) || a0.ws_g > lim) return false;
   const bool xs8 = a0.xs_w % 8 == 0 && a0.xs_h % 8 == 0 && a0.xs_b % 8 == 0 && a0.xs_g % 8 == 0;
   ConvArgs a = a0;
-  a.xcd_grid = conv_xcd_grid();
+  a.xcd_grid = 1;
   if (mode == FWD) {
     if (a.Cin == 8 && a.S <= 8 && a.xs_w == 8 && !a.xsc && a.xs_h % 8 == 0 && a.xs_b % 8 == 0 &&
         a.xs_g % 8 == 0) {  // the stems: 7x7 taps over 8 zero-padded input channels

@@ -419,18 +419,8 @@ static void launch_split(const ConvArgs& a, int oneacc, hipStream_t st) {
   }
 }
 
-int conv_xcd_grid() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("MAUV_XCD_GRID"); v = e ? atoi(e) : 1; }
-  return v;
-}
-
-// forward launches with K <= MAUV_SPLIT_SHORT_K (default 256; 0 = off) take the SEQ kernel
-static int split_short_k() {
-  static int k = -1;
-  if (k < 0) { const char* e = getenv("MAUV_SPLIT_SHORT_K"); k = e ? atoi(e) : 256; }
-  return k;
-}
+// forward launches with K <= 256 take the SEQ kernel
+constexpr int kSplitShortK = 256;
 
 template <int MODE, bool XBN>
 static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
@@ -448,10 +438,9 @@ static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
   // 64 x 128 as waves of 32 x 32 — measured 200 vs 235 ms of convs per bench step over four
   // waves.  256-wide tiles (225 vs 229 ms of convs per step against two co-resident 128 x 128
   // blocks) were measured and removed.  The short-K (SEQ) kernel serves the forwards and the
-  // data gradients without the BN-partials epilogue (MAUV_DGRAD_SHORT=0: forwards only).
+  // data gradients without the BN-partials epilogue.
   if constexpr (MODE == FWD || MODE == DGRAD) {
-    if (bm == 128 && bn == 128 && a.K > 0 && a.K <= split_short_k() &&
-        (MODE == FWD || dgrad_short())) {
+    if (bm == 128 && bn == 128 && a.K > 0 && a.K <= kSplitShortK) {
       launch_split<MODE, 128, 128, XBN, 8, false, true>(a, oneacc, st);
       return;
     }
@@ -472,7 +461,7 @@ bool conv_split_launch(int mode, const ConvArgs& a0, int oneacc, hipStream_t st)
   // (the FWD output is stored through plain pointers: only dgrad / wgrad read y by rsrc)
   if (nx > lim || (mode != FWD && ny > lim) || a0.ws_g > lim) return false;
   ConvArgs a = a0;
-  a.xcd_grid = conv_xcd_grid();
+  a.xcd_grid = 1;
   if (mode == FWD && a.Cin == 4 && a.S <= 8 && a.xs_c == 1 && a.xs_w == 4 && !a.xsc &&
       a.xs_h % 4 == 0 && a.xs_b % 4 == 0 && a.xs_g % 4 == 0 && a.N == 64) {
     // the stems over 4 zero-padded input channels (mauv_pack_nchw_f32)

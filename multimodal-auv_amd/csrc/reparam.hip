@@ -386,13 +386,9 @@ static dim3 sample_grid(long long nq, int G) {
   return dim3(bx, (unsigned)(gy < 1 ? 1 : gy));
 }
 
-// Kernel forms (MAUV_SAMPLE_BLK / MAUV_REPARAM_BWD4, default 1 each; mauv_set_reparam_kernels):
-// bit 0 = block-form sampling, bit 1 = 16-byte reparam_bwd.
-static int g_sample_blk = -1, g_bwd4 = -1;
-static int env_flag(int& v, const char* name) {
-  if (v < 0) { const char* e = getenv(name); v = e ? (atoi(e) != 0) : 1; }
-  return v;
-}
+// Kernel forms (default 1 each; mauv_set_reparam_kernels): bit 0 = block-form sampling,
+// bit 1 = 16-byte reparam_bwd.
+static int g_sample_blk = 1, g_bwd4 = 1;
 
 // The block form when its layout conditions hold, else the element kernel.
 template <class S>
@@ -401,7 +397,7 @@ static void launch_sample(const float* mu, const float* rho, const float* eps,
                           const unsigned long long* base, unsigned int layer, int G, int Cout,
                           int Cin, int RS, int cin_pad, typename S::T* out, long long gs,
                           hipStream_t stream) {
-  const int blk = env_flag(g_sample_blk, "MAUV_SAMPLE_BLK");
+  const int blk = g_sample_blk;
   const int align = (int)sizeof(typename S::T) * 4;
   if (blk && Cin % 4 == 0 && cin_pad % 4 == 0 && gs % 4 == 0 && RS <= 256 &&
       ((uintptr_t)out % align) == 0) {
@@ -521,7 +517,7 @@ MAUV_API int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride,
   if (RS > 49) { set_error("reparam_bwd: R*S > 49"); return kErrArg; }
   (void)nq;
   const int nt = (fixed_sample >= 0 ? G : 1) * splits;
-  const int v4 = env_flag(mauv::g_bwd4, "MAUV_REPARAM_BWD4");
+  const int v4 = mauv::g_bwd4;
   if (v4 && Cin % 4 == 0 && dw_cin % 4 == 0 && gs % 4 == 0 && ss % 4 == 0 &&
       ((uintptr_t)dw & 15) == 0 && nt <= RB4_TERMS &&
       (long long)(splits - 1) * ss + (long long)(G - 1) * gs + (long long)Cout * RS * dw_cin <
@@ -582,8 +578,8 @@ MAUV_API int mauv_philox_raw(unsigned long long seed, unsigned long long sample,
 // (reparam_sample_blk), bit 1 = 16-byte backward (reparam_bwd4); -1 queries.  Returns the
 // previous mask.  Sampling is bit-identical either way; the backward's sum order differs.
 MAUV_API int mauv_set_reparam_kernels(int mask) {
-  const int prev = mauv::env_flag(mauv::g_sample_blk, "MAUV_SAMPLE_BLK") |
-                   (mauv::env_flag(mauv::g_bwd4, "MAUV_REPARAM_BWD4") << 1);
+  const int prev = mauv::g_sample_blk |
+                   (mauv::g_bwd4 << 1);
   if (mask >= 0 && mask <= 3) {
     mauv::g_sample_blk = mask & 1;
     mauv::g_bwd4 = (mask >> 1) & 1;

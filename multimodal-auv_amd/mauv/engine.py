@@ -25,26 +25,17 @@ from . import ops
 from .layers import is_bayesian, LinearReparameterization
 
 
-# fp32 stems on an NHWC copy of the images with 4 zero-padded channels (the pipelined split
-# kernel's STEM mode) instead of strided NCHW loads on the generic kernel
-F32_STEM_PACK = os.environ.get("MAUV_F32_STEM_PACK", "1") == "1"
 # The three trunks of MultiModalModel are independent until the fusion head: each runs its
 # forward and (autograd replays the forward's stream) its backward on a stream of its own, so
-# one trunk's memory-bound BN passes overlap another's MFMA-bound convs.
+# one trunk's memory-bound BN passes overlap another's MFMA-bound convs (MAUV_TRUNK_STREAMS=0:
+# one stream, for serial kernel traces).
 TRUNK_STREAMS = os.environ.get("MAUV_TRUNK_STREAMS", "1") == "1"
-# The stem's bn1 + ReLU applied on load inside the max-pool (the 112x112 BN output, the largest
-# activation of the trunk, is never written; its backward recomputes the ReLU mask from y).
-FUSED_STEM_POOL = os.environ.get("MAUV_FUSED_STEM_POOL", "1") == "1"
-# Training block outputs (bn3 + residual + ReLU) also write 1-bit ReLU masks, and their
-# backward reads those instead of the 2-4 B stored output (MAUV_BN_RELU_MASK=0: read the output).
-BN_RELU_MASK = os.environ.get("MAUV_BN_RELU_MASK", "1") == "1"
-# The stems as ONE GEMM over im2col rows shared by the G samples, the G weight sets stacked
-# along N (stem.hip), instead of G implicit GEMMs over channel-padded pixels.
-STEM_GEMM = os.environ.get("MAUV_STEM_GEMM", "1") == "1"
-# Training: a block output's residual gradient dres = dout * relu-mask is never written — the
-# conv1 data gradient adds dout where the block output's mask bit is set (identity blocks), the
-# downsample BN's backward reads dout with that mask (MAUV_RES_MASK=0: write dres).
-RES_MASK = os.environ.get("MAUV_RES_MASK", "1") == "1"
+# Measured-positive schedule choices whose predecessors were removed (DESIGN.md §2.3, §2.8,
+# §2.13): the stems run as ONE GEMM over im2col rows shared by the G samples (stem.hip) and their
+# bn1 + ReLU is applied inside the max-pool's loads; training block outputs (bn3 + residual +
+# ReLU) write 1-bit ReLU masks that their backward reads instead of the stored output; a block
+# output's residual gradient dres = dout * mask is never written (the conv1 data gradient adds
+# dout under the mask bits, the downsample BN's backward reads dout with them).
 _STREAMS = {}
 
 
@@ -386,11 +377,9 @@ class TrunkRunner(_Runner):
         self.dt = dtype   # activation / sampled-weight storage (fp32, bf16 or f16)
 
     def _cin_pad(self, Cin):
-        """The convs move 16-byte channel chunks: the stems' 1/3 input channels pad to 8
-        (16-bit) or 4 (fp32; MAUV_F32_STEM_PACK=0 keeps the fp32 stems on strided NCHW loads)."""
+        """The convs move 16-byte channel chunks: input channels pad to 8 (16-bit) or 4 (fp32)
+        (every conv after the stems has Cin % 64 == 0)."""
         q = 4 if self.dt == torch.float32 else 8
-        if self.dt == torch.float32 and not F32_STEM_PACK:
-            q = 1
         return Cin if Cin % q == 0 else (Cin + q - 1) // q * q
 
     # ---- conv / bn units ----
@@ -517,7 +506,7 @@ class TrunkRunner(_Runner):
         out = mask = None
         if materialize:
             out = torch.empty_like(y)
-            if BN_RELU_MASK and relu and self.save and C <= 2048:
+            if relu and self.save and C <= 2048:
                 mask = torch.empty(G * M * C // 8, dtype=torch.uint8, device=y.device)
                 ops.bn_apply_mask(y, scale, shift, res, out, mask, G, M, C, res_bn=res_bn)
             else:
@@ -570,30 +559,16 @@ class TrunkRunner(_Runner):
             raise ValueError(f"trunk expects {t.conv1.in_channels} input channels, got {Cin}")
         self.B = B
         recs = self.recs = []
-        if STEM_GEMM:
-            y, rc, part = self._stem(t.conv1, x, B, H, W)
-        else:
-            cp = self._cin_pad(Cin)
-            if self.dt == torch.float32 and cp == Cin:   # the stem reads the NCHW images in place
-                xs = (0, Cin * H * W, W, 1, H * W)
-            else:           # NHWC copy, channels zero-padded to 8 (16-bit) / 4 (fp32)
-                xh = torch.empty(B, H, W, cp, device=x.device, dtype=self.dt)
-                ops.pack_nchw(x, B, Cin, H, W, cp, xh)
-                x, xs = xh, (0, H * W * cp, W * cp, cp, 1)
-            y, rc, part = self._conv(t.conv1, x, B, H, W, x_strides=xs)
+        y, rc, part = self._stem(t.conv1, x, B, H, W)
         H, W = y.shape[2], y.shape[3]
         Hp, Wp = ops.out_hw(H, 3, 2, 1), ops.out_hw(W, 3, 2, 1)
         p = torch.empty(G, B, Hp, Wp, 64, device=x.device, dtype=self.dt)
         idx = torch.empty(G, B, Hp, Wp, 64, dtype=torch.uint8, device=x.device) \
             if self.save else None
-        if FUSED_STEM_POOL:   # bn1 + relu applied inside the max-pool's loads
-            _, rb = self._bn(t.bn1, y, part, relu=True, materialize=False)
-            scale, shift, _ = self.last_lazy
-            ops.maxpool_fwd(y, G * B, H, W, 64, p, idx, bn=(scale, shift, G))
-        else:
-            a, rb = self._bn(t.bn1, y, part, relu=True)
-            ops.maxpool_fwd(a, G * B, H, W, 64, p, idx)
-            del a
+        # bn1 + relu applied inside the max-pool's loads
+        _, rb = self._bn(t.bn1, y, part, relu=True, materialize=False)
+        scale, shift, _ = self.last_lazy
+        ops.maxpool_fwd(y, G * B, H, W, 64, p, idx, bn=(scale, shift, G))
         del y, part
         self.stem = (rc, rb, idx, (H, W)) if self.save else None
         del idx
@@ -648,7 +623,7 @@ class TrunkRunner(_Runner):
         while self.recs:
             r1, s1, r2, s2, r3, s3, rd, sd = self.recs.pop()
             # the residual gradient: dres = da * mask3, kept implicit when bn3 has mask bits
-            rmask = s3.mask if RES_MASK and s3.mask is not None and \
+            rmask = s3.mask if s3.mask is not None and \
                 (rd is not None or self.dt == torch.float32 or self._masked_addend_ok(r1)) \
                 else None
             dy3, dres = self._bn_bwd(s3, da, want_dres=rmask is None)
@@ -681,10 +656,7 @@ class TrunkRunner(_Runner):
         del da, idx
         dy0, _ = self._bn_bwd(rb, da0)
         del da0
-        if rc[0] == "stem":
-            self._stem_bwd(rc, dy0)
-        else:
-            self._conv_bwd(rc, dy0, need_dx=False)
+        self._stem_bwd(rc, dy0)
         if self.st.grad_ready_hook is not None:
             self.st.grad_ready_hook(self.trunk)
         if self.join is not None:   # the caller's stream (optimizer, all-reduce) waits for us
