@@ -96,9 +96,15 @@ int mauv_set_f32_math(int mode);
 
 /* 3x3 / stride-1 / pad-1 16-bit forwards over 64 -> 64 channels (every bottleneck's layer-1
  * conv2) through an LDS image of the input rows each block's pixels touch (conv_halo16.hip;
- * bit-identical to the implicit GEMM): 1 (default, or MAUV_HALO3=0 at load) routes them there,
- * 0 to the implicit GEMM, -1 queries.  Returns the previous setting. */
+ * bit-identical to the implicit GEMM): 1 (default) routes them there, 0 to the implicit GEMM,
+ * -1 queries.  Returns the previous setting. */
 int mauv_set_halo3(int on);
+/* 16-bit forwards on 256-row block tiles with LDS-DMA operands (conv_big16.hip; same operands
+ * and k order as the implicit GEMM, bit-identical outputs): mode 1 (default) routes the shapes
+ * where it measured faster (1x1, no pending BN, K >= 512, N >= 256, >= 512 tiles), 2 every
+ * forward it covers with K = R*S*Cin >= min_k, 0 none; -1 keeps; min_k <= 0 keeps the
+ * threshold (512).  Returns the previous mode. */
+int mauv_set_big16(int mode, int min_k);
 
 /* ---- 16-bit implicit-GEMM convs (conv_gemm16.hip) -----------------------------------------
  * Same three GEMM views on v_mfma_f32_32x32x16_{bf16,f16}: dtype 0 = bf16 (BASELINE configs[2]
@@ -233,7 +239,7 @@ typedef struct MauvStepGate {
   int ok_loss, nonfinite, poisoned, mode;
   int step, stepped, skipped_loss, skipped_grad;
   float step_size, bc2_sqrt;
-  int reserved[6];
+  int reserved[6];   /* untouched by the library (mauv.train counts non-finite inputs in [5]) */
 } MauvStepGate;
 int mauv_adam_step_gated(const MauvAdamEntry* table, int n, float lr, float beta1, float beta2,
                          float eps, float weight_decay, MauvStepGate* gate, hipStream_t stream);

@@ -1,0 +1,230 @@
+// 16-bit implicit-GEMM forward on 256-row block tiles whose operands reach LDS by LDS-DMA
+// (buffer_load ... lds): the long-K forwards of the trunks (layer-2..4 3x3 convs, the 1x1 convs
+// over >= 512 channels) in bf16 training (BASELINE configs[2]) and in the f16 MC inference the
+// reference predictor runs under torch.amp.autocast (inference/predictors.py:55).
+//
+// conv_pipe16's 128 x 128 tiles stage operands through registers (load, BN-on-load VALU,
+// ds_write) and give each wave 8 MFMAs per barrier (latency-bound, MFMA busy
+// <= 0.33).  Here one block of 8 waves owns a 256 x BN tile (BN = 256: waves of 128 x 64, 32
+// MFMAs per 64-deep stage; BN = 128: 64 x 64), the DMA of stage t+1 is in flight while stage t
+// computes, and the operands never pass through VGPRs:
+//  * LDS images of 64-k rows (128 B), chunk c of row r in slot c ^ ((r >> 1) & 7) (every
+//    ds_read_b128 fragment of v_mfma_f32_32x32x16 conflict-free); the DMA writes each wave
+//    instruction's 1 KiB linearly, so each lane fetches the chunk its slot holds;
+//  * A = the im2col rows of x for tap (r, s), channels c0..c0+63 (zero outside the image and
+//    past M: the buffer offset is past the descriptor), B = the KRSC weight rows;
+//  * the producing layer's pending BN(+ReLU) (XBN) is applied to the landed A tile in place
+//    (bn_relu8, the implicit GEMM's transform: identical operands), one extra barrier;
+//  * the epilogue is conv_pipe16's (epilogue16: BN statistics from the fp32 accumulators in
+//    128-row partials, 16-bit rows through LDS).
+// Accumulation order over k is the implicit GEMM's; outputs match it to accumulation order.
+#include "conv_common.h"
+#include "conv_epi16.h"
+
+namespace mauv {
+
+namespace {
+
+constexpr int BK = 64;
+constexpr unsigned kOOBb = 0x7ffffff0u;
+constexpr int kMaxXbnB = 512;  // pending-BN input channels staged in LDS
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                           voff, 0, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void block_sync() {  // LDS-only barrier: DMAs stay in flight
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrcb(const void* p, long long nelem) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(nelem * 2), 0x00020000);
+}
+
+template <int BM, int BN>
+struct WavesB {
+  static constexpr int M = BN == 256 ? 2 : 4, N = 8 / M;
+};
+
+}  // namespace
+
+template <int DT, int BM, int BN, bool XBN>
+__global__ __launch_bounds__(512, 2) void conv_big16(const ConvArgs a) {
+  constexpr int NT = 512, NW = 8;
+  constexpr int WGM = WavesB<BM, BN>::M, WGN = WavesB<BM, BN>::N;
+  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
+  constexpr int A_B = BM * 128, B_B = BN * 128, STG = A_B + B_B;  // bytes
+  constexpr int RA = BM / NW, RB = BN / NW, JA = RA / 8, JB = RB / 8, J = JA + JB;
+  constexpr int XOFF = 2 * STG, XB = XBN ? 2 * kMaxXbnB * 4 : 0;
+  constexpr int PR = BM / WGM, EPI = PR * (BN + 4) * 4;  // epilogue16's per-pass staging
+  constexpr int LDSB = XOFF + XB > EPI ? XOFF + XB : EPI;
+  constexpr int TCH = BM * 8 / NT;  // A chunks each thread transforms per stage (XBN)
+  // ONE shared array (a second __shared__ object makes hipcc wait vmcnt(0) before ds_reads)
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDSB];
+  float* xbn = (float*)(smem + XOFF);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
+  int m0, n0, g;
+  conv_block_tile<BM, BN>(a, m0, n0, g);
+  const u16* xg = (const u16*)a.x + (long long)g * a.xs_g;
+  const u16* wg = (const u16*)a.w + (long long)g * a.ws_g;
+  const __amdgpu_buffer_rsrc_t ra = rsrcb(xg, (long long)a.B * a.xs_b);
+  const __amdgpu_buffer_rsrc_t rb = rsrcb(wg, a.ws_g);
+  const int xs_h = (int)a.xs_h, xs_w = (int)a.xs_w, xs_b = (int)a.xs_b;
+  const int HW = a.Ho * a.Wo;
+
+  // DMA lanes: row r = wave * R + 8 j + (lane >> 3) of the tile, slot lane & 7 holds chunk
+  // c = (lane & 7) ^ ((r >> 1) & 7)
+  unsigned abase[JA];
+  int ap0[JA], ap1[JA];
+#pragma unroll
+  for (int j = 0; j < JA; ++j) {
+    const int r = wave * RA + 8 * j + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
+    const int m = m0 + r, mm = m < a.M ? m : 0;
+    const int b = mm / HW, rem = mm - b * HW, oh = rem / a.Wo, ow = rem - oh * a.Wo;
+    const int p0 = oh * a.stride - a.pad, p1 = ow * a.stride - a.pad;
+    abase[j] = (unsigned)((b * xs_b + p0 * xs_h + p1 * xs_w + 8 * c) * 2);
+    ap0[j] = m < a.M ? p0 : -(1 << 28);
+    ap1[j] = p1;
+  }
+  unsigned bbase[JB];
+#pragma unroll
+  for (int j = 0; j < JB; ++j) {
+    const int r = wave * RB + 8 * j + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
+    bbase[j] = n0 + r < a.N ? (unsigned)(((n0 + r) * a.K + 8 * c) * 2) : kOOBb;
+  }
+  // XBN transform: this thread's rows (tid >> 3) + 64 i and their input pixel origins
+  int tp0[XBN ? TCH : 1], tp1[XBN ? TCH : 1];
+  if constexpr (XBN) {
+#pragma unroll
+    for (int i = 0; i < TCH; ++i) {
+      const int m = m0 + (tid >> 3) + (NT / 8) * i, mm = m < a.M ? m : 0;
+      const int b = mm / HW, rem = mm - b * HW, oh = rem / a.Wo, ow = rem - oh * a.Wo;
+      tp0[i] = m < a.M ? oh * a.stride - a.pad : -(1 << 28);
+      tp1[i] = ow * a.stride - a.pad;
+    }
+    for (int i = tid; i < a.Cin; i += NT) {
+      xbn[i] = a.xsc[g * a.Cin + i];
+      xbn[kMaxXbnB + i] = a.xsh[g * a.Cin + i];
+    }
+  }
+
+  const int nt = a.K / BK;
+  int t_r = 0, t_s = 0, t_c = 0;  // k position of the next stage to issue
+  auto issue = [&](int t) {
+    unsigned char* As = smem + (t & 1) * STG;
+    unsigned char* Bs = As + A_B;
+    const unsigned soff = (unsigned)((t_r * xs_h + t_s * xs_w + t_c) * 2);
+#pragma unroll
+    for (int j = 0; j < JA; ++j) {
+      const bool ok = ((unsigned)(ap0[j] + t_r) < (unsigned)a.H) &
+                      ((unsigned)(ap1[j] + t_s) < (unsigned)a.W);
+      dma16(ra, As + (wave * RA + 8 * j) * 128, sel_off(ok, abase[j] + soff, kOOBb));
+    }
+    const unsigned koff = (unsigned)(t * BK * 2);
+#pragma unroll
+    for (int j = 0; j < JB; ++j) dma16(rb, Bs + (wave * RB + 8 * j) * 128, bbase[j] + koff);
+    t_c += BK;
+    if (t_c >= a.Cin) { t_c = 0; if (++t_s == a.S) { t_s = 0; ++t_r; } }
+  };
+
+  floatx16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  auto frag = [&](const unsigned char* img, int row, int chunk) -> u32x4 {
+    return *(const u32x4*)(img + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
+  };
+  // fragments of k-step s + 1 are read while the MFMAs of k-step s run
+  auto compute = [&](int t) {
+    const unsigned char* As = smem + (t & 1) * STG;
+    const unsigned char* Bs = As + A_B;
+    u32x4 af[2][MI], bq[2][NI];
+    auto rd = [&](int s, int q) {
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) af[q][mi] = frag(As, wm * WM + mi * 32 + li, 2 * s + lh);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) bq[q][ni] = frag(Bs, wn * WN + ni * 32 + li, 2 * s + lh);
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      if (s + 1 < BK / 16) rd(s + 1, (s + 1) & 1);
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = H16<DT>::mfma(af[s & 1][mi], bq[s & 1][ni], acc[mi][ni]);
+    }
+  };
+
+  const unsigned rfloor = a.xrelu ? 0u : 0x80008000u;
+  int x_r = 0, x_s = 0, x_c = 0;  // k position of the stage being transformed
+  issue(0);
+  if constexpr (XBN) block_sync();  // xbn staged
+  for (int t = 0; t < nt; ++t) {
+    // tile t + 1 goes to the buffer tile t - 1 was read from (free since the barrier ending t - 1)
+    if (t + 1 < nt) {
+      issue(t + 1);
+      wait_vm<J>();   // this wave's DMAs of tile t have landed
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();  // every wave's DMAs of tile t have landed
+    asm volatile("" ::: "memory");
+    if constexpr (XBN) {
+      unsigned char* As = smem + (t & 1) * STG;
+#pragma unroll
+      for (int i = 0; i < TCH; ++i) {
+        const int idx = tid + NT * i, row = idx >> 3;
+        const int c = (idx & 7) ^ ((row >> 1) & 7), ch = x_c + 8 * c;
+        const bool ok = ((unsigned)(tp0[i] + x_r) < (unsigned)a.H) &
+                        ((unsigned)(tp1[i] + x_s) < (unsigned)a.W);
+        u32x4* p = (u32x4*)(As + idx * 16);
+        *p = bn_relu8<DT>(*p, ldf8(xbn + ch), ldf8(xbn + kMaxXbnB + ch), rfloor, ok);
+      }
+      x_c += BK;
+      if (x_c >= a.Cin) { x_c = 0; if (++x_s == a.S) { x_s = 0; ++x_r; } }
+      block_sync();
+    }
+    compute(t);
+    block_sync();  // tile t's buffer is free for the DMA issued next
+  }
+  epilogue16<FWD, DT, BM, BN, MI, NI, WGM, WGN, 2 * STG>(a, acc, smem, m0, n0, g);
+}
+
+// true: launched (a = conv_pipe16_launch's prepared FWD arguments)
+bool conv_big16_launch(int dt, const ConvArgs& a, hipStream_t st) {
+  if (a.cpg || a.Cin % 64 || a.K != a.R * a.S * a.Cin || a.xs_c != 1 || a.xs_w % 8 ||
+      a.xs_h % 8 || a.xs_b % 8 || a.xs_g % 8 || (a.xsc && a.Cin > kMaxXbnB))
+    return false;
+  if ((long long)a.B * a.xs_b * 2 > 0x7fff0000LL || a.ws_g * 2 > 0x7fff0000LL) return false;
+  if (a.M <= 64) return false;  // the statistics partials are 128-row (conv_tile_rows)
+  const bool xb = a.xsc != nullptr;
+  const int BN = a.N >= 256 ? 256 : 128;
+  const dim3 grid(ceil_div(a.M, 256) * ceil_div(a.N, BN), a.G);
+#define MAUV_BIG_LAUNCH(D, N_, X) \
+  hipLaunchKernelGGL((conv_big16<D, 256, N_, X>), grid, dim3(512), 0, st, a)
+#define MAUV_BIG_DT(D)                                                             \
+  do {                                                                             \
+    if (BN == 256) { if (xb) MAUV_BIG_LAUNCH(D, 256, true); else MAUV_BIG_LAUNCH(D, 256, false); } \
+    else { if (xb) MAUV_BIG_LAUNCH(D, 128, true); else MAUV_BIG_LAUNCH(D, 128, false); }          \
+  } while (0)
+  if (dt == DT_BF16) MAUV_BIG_DT(DT_BF16);
+  else MAUV_BIG_DT(DT_F16);
+#undef MAUV_BIG_DT
+#undef MAUV_BIG_LAUNCH
+  return true;
+}
+
+}  // namespace mauv

@@ -152,6 +152,8 @@ bool conv_split_launch(int mode, const ConvArgs& a, int oneacc, hipStream_t st);
 // pipelined 16-bit kernels (conv_pipe16.hip); x/w/dy/out/addend hold 16-bit data of type dt
 // (DT_BF16 / DT_F16), WGRAD out stays fp32 slabs; false: shape not covered
 bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
+// 16-bit forwards on 256-row tiles with LDS-DMA operands (conv_big16.hip); false: not covered
+bool conv_big16_launch(int dt, const ConvArgs& a, hipStream_t st);
 // 3x3 / stride-1 forwards and data gradients over 64 -> 64 channels through an LDS image of the
 // input rows (conv_halo16.hip); false: shape not covered (or mauv_set_halo3(0))
 bool conv_halo16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);

@@ -41,8 +41,13 @@ __device__ __forceinline__ u32x4 bn_relu8(u32x4 v, const floatx8& sc, const floa
       lo = (float)__builtin_bit_cast(_Float16, (u16)(v[i] & 0xffffu));
       hi = (float)__builtin_bit_cast(_Float16, (u16)(v[i] >> 16));
     }
-    unsigned p = pk2<DT>(__builtin_fmaf(lo, sc[2 * i], sh[2 * i]),
-                         __builtin_fmaf(hi, sc[2 * i + 1], sh[2 * i + 1]));
+    // the fp32 result is pinned before the conversion: one fp32 fma, then one rounding to the
+    // 16-bit format (the reference's fp32 BN output cast by autocast) — without the pin hipcc
+    // may contract f16 paths into v_fma_mix (one rounding straight to f16), kernel by kernel
+    float f0 = __builtin_fmaf(lo, sc[2 * i], sh[2 * i]);
+    float f1 = __builtin_fmaf(hi, sc[2 * i + 1], sh[2 * i + 1]);
+    asm("" : "+v"(f0), "+v"(f1));
+    unsigned p = pk2<DT>(f0, f1);
     asm("" : "+v"(p));  // keeps one v_cvt_pk per pair (else: two single conversions + v_perm)
     const s2 m = __builtin_elementwise_max(__builtin_bit_cast(s2, p), __builtin_bit_cast(s2, floor));
     o[i] = ok ? __builtin_bit_cast(unsigned, m) : 0u;

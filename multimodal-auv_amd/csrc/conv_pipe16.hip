@@ -411,6 +411,20 @@ static void pipe16_dt(int dt, const ConvArgs& a, hipStream_t st) {
   else pipe16_tiles<MODE, DT_F16, XBN, STEM>(a, st);
 }
 
+// mauv_set_big16: 1 (default) = the forwards where the 256-row LDS-DMA kernel (conv_big16.hip)
+// measured faster take it; 2 = every forward it covers with K >= g_big16_k; 0 = none
+int g_big16 = 1, g_big16_k = 512;
+static int big16() { return g_big16; }
+static int big16_min_k() { return g_big16_k; }
+// measured (tools/fwd_ab.py): faster only on 1x1 forwards without a pending
+// BN over K >= 512 input channels into N >= 256 outputs with enough 256 x 256 tiles for two
+// rounds of the chip; the 3x3s and the 128-column / few-tile shapes of the training slice ran
+// 5-70 % slower than the implicit GEMM
+static bool big16_wins(const ConvArgs& a) {
+  const long long tiles = (long long)ceil_div(a.M, 256) * ceil_div(a.N, 256) * a.G;
+  return a.R == 1 && a.S == 1 && !a.xsc && a.K >= 512 && a.N >= 256 && tiles >= 512;
+}
+
 bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
   const long long lim = 0x7fff0000LL / 2;  // elements addressable by a 31-bit byte offset
   const long long nx = (long long)a0.B * a0.xs_b, ny = (long long)a0.B * a0.Ho * a0.Wo * a0.Cout;
@@ -431,6 +445,9 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
     }
     if (a.Cin % 64 || !xs8 || (a.xsc && a.Cin > kMaxXbn16)) return false;
     if (conv_halo16_launch(FWD, dt, a, st)) return true;
+    if (big16() && a.K >= big16_min_k() && (big16() == 2 || big16_wins(a)) &&
+        conv_big16_launch(dt, a, st))
+      return true;
     if (a.xsc) pipe16_dt<FWD, true>(dt, a, st);
     else pipe16_dt<FWD, false>(dt, a, st);
   } else if (mode == DGRAD) {
@@ -451,3 +468,17 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
 }
 
 }  // namespace mauv
+
+// Route 16-bit forwards through conv_big16: mode 1 (default) where it measured faster, 2 every
+// forward it covers with K >= min_k, 0 none; mode -1 / min_k <= 0 query / keep.  Returns the
+// previous mode.
+MAUV_API int mauv_set_big16(int mode, int min_k) {
+  const int prev = mauv::g_big16;
+  if (mode >= 0 && mode <= 2) mauv::g_big16 = mode;
+  else if (mode != -1) {
+    mauv::set_error("set_big16: mode 0, 1, 2 or -1 (query)");
+    return mauv::kErrArg;
+  }
+  if (min_k > 0) mauv::g_big16_k = min_k;
+  return prev;
+}

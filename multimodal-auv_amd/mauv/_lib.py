@@ -33,6 +33,7 @@ SIGNATURES = {
     "mauv_conv2d_bwd_weight_f32": [P, P, P, P, I, P, P] + [I] * 11 + [P],
     "mauv_set_f32_math": [I],
     "mauv_set_halo3": [I],
+    "mauv_set_big16": [I, I],
     # conv_gemm16.hip
     "mauv_conv2d_fwd_h16": [I, P, P, P, P, I, P, P] + [I] * 10 + [P, P, P, P],
     "mauv_conv2d_bwd_data_h16": [I, P, P, P, P, I] + [I] * 10 + [P],

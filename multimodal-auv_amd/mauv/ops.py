@@ -112,6 +112,16 @@ def set_halo3(on):
     return bool(rc)
 
 
+def set_big16(mode=None, min_k=0):
+    """Route 16-bit forwards through the 256-row LDS-DMA kernel: 1 (default) where it measured
+    faster, 2 (or True) every forward it covers with K >= min_k, 0 (or False) none; None /
+    min_k=0 keep.  Returns the previous mode (0 / 1 / 2)."""
+    m = -1 if mode is None else (2 if mode is True else (0 if mode is False else int(mode)))
+    rc = lib.mauv_set_big16(m, int(min_k))
+    check(0 if rc >= 0 else rc, "set_big16")
+    return rc
+
+
 def set_reparam_kernels(sample_blk=None, bwd4=None):
     """Kernel forms of reparam_sample (block form, bit-identical) and reparam_bwd (16-byte slab
     loads); None keeps a setting.  Returns the previous (sample_blk, bwd4)."""

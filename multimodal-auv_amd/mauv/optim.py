@@ -23,6 +23,7 @@ from ._lib import lib, check
 
 GATE_WORDS = 16          # sizeof(MauvStepGate) / 4 (include/mauv.h)
 G_OK_LOSS, G_NONFINITE, G_POISONED, G_MODE, G_STEP, G_STEPPED, G_SKIP_LOSS, G_SKIP_GRAD = range(8)
+G_SCRATCH = 15           # a reserved word the training step counts non-finite inputs in
 
 
 class FusedAdam(torch.optim.Optimizer):

@@ -117,6 +117,27 @@ def _step_gate(model, optimizer, loss):
     return optimizer.gate(st.params, loss.device)
 
 
+def _batch_finite(loss, inputs_tuple, counter=None):
+    """Device bool: the reference would see a finite loss (multimodal.py:133).  Besides the
+    loss itself, any non-finite input pixel counts: with BatchNorm in train mode one NaN / Inf
+    pixel makes every logit of the reference's batch NaN (torch's ReLU propagates NaN), while
+    the fused kernels' ReLU (x > 0 ? x : 0) would zero a NaN channel and hand back a finite
+    loss over non-finite gradients.  ``counter``: int32 device scratch word."""
+    from . import ops
+    ok = torch.isfinite(loss.detach()).reshape(1)
+    ins = [t for t in inputs_tuple if t.is_cuda and t.dtype == torch.float32 and
+           t.is_contiguous()]
+    if not ins:
+        return ok
+    if counter is None:
+        counter = torch.zeros(1, dtype=torch.int32, device=loss.device)
+    else:
+        counter.zero_()
+    for t in ins:
+        ops.nonfinite_count(t, counter)
+    return ok & (counter == 0)
+
+
 def _count_nonfinite(model, counter):
     """Add the number of non-finite gradient blocks of the arena into the device ``counter``
     (the fused form of multimodal.py:141's per-tensor isnan/isinf scan, no host sync)."""
@@ -158,9 +179,9 @@ def mc_train_step(model, inputs_tuple, labels, criterion, optimizer, num_mc, bat
                                                      num_mc, batch_size, kl_w)
     gate = _step_gate(model, optimizer, loss)
     if gate is not None:
-        from .optim import G_OK_LOSS, G_NONFINITE, G_STEPPED
+        from .optim import G_OK_LOSS, G_NONFINITE, G_STEPPED, G_SCRATCH
         ok = gate[G_OK_LOSS:G_OK_LOSS + 1]
-        ok.copy_(torch.isfinite(loss.detach()).reshape(1))
+        ok.copy_(_batch_finite(loss, inputs_tuple, gate[G_SCRATCH:G_SCRATCH + 1]))
         if hasattr(model, "all_ranks_device"):
             model.all_ranks_device(ok)
         loss.backward()
@@ -176,7 +197,7 @@ def mc_train_step(model, inputs_tuple, labels, criterion, optimizer, num_mc, bat
         return dict(loss=loss.detach(), output=output, predicted=predicted, ce=ce.detach(),
                     scaled_kl=scaled_kl.detach(), ok_loss=flags[G_OK_LOSS],
                     stepped=flags[G_STEPPED])
-    if not _all_ranks(model, bool(torch.isfinite(loss).item())):
+    if not _all_ranks(model, bool(_batch_finite(loss, inputs_tuple).item())):
         logging.warning(f"Skipping batch due to NaN/Inf loss: {loss}")
         return None
     loss.backward()

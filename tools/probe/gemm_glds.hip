@@ -24,7 +24,7 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // NBUF LDS stages; STAGES_AHEAD tiles in flight while computing
-template <int BM, int BN, int WGM, int WGN, int DT, int NBUF>
+template <int BM, int BN, int WGM, int WGN, int DT, int NBUF, bool XT = false>
 __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN + 3) / 4) void gemm_glds(const ConvArgs a) {
   constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
@@ -121,6 +121,21 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN + 3) / 4) void gemm_glds
     }
     __builtin_amdgcn_s_barrier();  // every wave's DMAs of tile t have landed
     asm volatile("" ::: "memory");
+    if constexpr (XT) {
+      // the producing layer's pending BN + ReLU on the landed A tile, in place in LDS
+      unsigned char* As = smem + (t % NBUF) * STG;
+#pragma unroll
+      for (int j = 0; j < BM * 8 / NT; ++j) {
+        const int idx = tid + NT * j, row = idx >> 3, slot = idx & 7;
+        const int c = slot ^ ((row >> 1) & 7), ch = t * BK + 8 * c;
+        u32x4* p = (u32x4*)(As + idx * 16);
+        const floatx8 sc = ldf8(a.xsc + (long long)g * K + ch), sh = ldf8(a.xsh + (long long)g * K + ch);
+        *p = bn_relu8<DT>(*p, sc, sh, 0u, m0 + row < M);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
     compute(t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // tile t's buffer is free for the DMA issued next
@@ -129,20 +144,22 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN + 3) / 4) void gemm_glds
   epilogue16<FWD, DT, BM, BN, MI, NI, WGM, WGN, NBUF * STG>(a, acc, smem, m0, n0, g);
 }
 
-template <int BM, int BN, int WGM, int WGN, int NBUF>
+template <int BM, int BN, int WGM, int WGN, int NBUF, bool XT = false>
 void launch(const ConvArgs& a, hipStream_t st) {
   dim3 grid(((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN), a.G);
-  hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, DT_BF16, NBUF>), grid, dim3(64 * WGM * WGN), 0,
-                     st, a);
+  hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, DT_BF16, NBUF, XT>), grid, dim3(64 * WGM * WGN),
+                     0, st, a);
 }
 
 }  // namespace
 
 // variant: 0 = 256x256 (2x4 waves of 128x64), 2 LDS stages; 1 = 256x128 (4x2 waves of 64x64),
-// 2 stages; 2 = 256x128, 3 stages; 3 = 128x128 (2x2 waves... 4 waves of 64x64), 2 stages
+// 2 stages; 2 = 256x128, 3 stages; 3 = 128x128 (4 waves of 64x64), 2 stages; 4 / 5 = 1 / 0 with
+// the pending BN + ReLU applied to the landed A tile in LDS (xsc / xsh [G][K])
 extern "C" int probe_gemm_glds(int variant, const void* A, const void* B, void* C, int M, int N,
-                               int K, int G, hipStream_t st) {
+                               int K, int G, const float* xsc, const float* xsh, hipStream_t st) {
   ConvArgs a = {};
+  a.xsc = xsc; a.xsh = xsh; a.xrelu = 1;
   a.x = (const float*)A;
   a.w = (const float*)B;
   a.out = (float*)C;
@@ -157,6 +174,8 @@ extern "C" int probe_gemm_glds(int variant, const void* A, const void* B, void* 
     case 1: launch<256, 128, 4, 2, 2>(a, st); break;
     case 2: launch<256, 128, 4, 2, 3>(a, st); break;
     case 3: launch<128, 128, 2, 2, 2>(a, st); break;
+    case 4: launch<256, 128, 4, 2, 2, true>(a, st); break;   // + pending BN + ReLU on A
+    case 5: launch<256, 256, 2, 4, 2, true>(a, st); break;
     default: return -2;
   }
   return hipGetLastError() == hipSuccess ? 0 : -3;

@@ -19,7 +19,7 @@ from mauv import ops  # noqa: E402
 
 lib = ctypes.CDLL(os.path.join(HERE, "libprobe.so"))
 lib.probe_gemm_glds.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 + \
-    [ctypes.c_void_p]
+    [ctypes.c_void_p] * 3
 
 # (name, M per group, N, K): 1x1 convs of the bench trunks (B = 64; sonar 256 px / optical 224)
 SHAPES = [
@@ -34,6 +34,7 @@ SHAPES = [
 ]
 G = 5
 VARIANTS = {0: "glds 256x256", 1: "glds 256x128", 2: "glds 256x128 x3", 3: "glds 128x128"}
+XVARIANTS = {4: "glds 256x128 +BN", 5: "glds 256x256 +BN"}
 
 
 def ev_time(fn, reps):
@@ -50,45 +51,64 @@ def main():
     torch.manual_seed(0)
     dt = torch.bfloat16
     stream = torch.cuda.current_stream().cuda_stream
-    print(f"{'shape':26s} {'GFLOP':>7s} " + " ".join(f"{v:>16s}" for v in
-          ["torch.bmm", "conv_pipe16"] + list(VARIANTS.values())))
-    for name, M, N, K in SHAPES:
-        A = (torch.rand(G, M, K, device="cuda") * 2 - 1).to(dt)
-        B = (torch.rand(G, N, K, device="cuda") * 2 - 1).to(dt)
-        ref = torch.bmm(A.float(), B.float().transpose(1, 2))
-        C = torch.empty(G, M, N, device="cuda", dtype=dt)
-        fns = {"torch.bmm": lambda: torch.bmm(A, B.transpose(1, 2))}
-        Hh = M // 64
-        fns["conv_pipe16"] = lambda: ops.conv2d_fwd(A, B, C, G, 64, Hh, 1, K, N, 1, 1, 0)
-        for v in VARIANTS:
-            fns[VARIANTS[v]] = (lambda v=v: lib.probe_gemm_glds(v, A.data_ptr(), B.data_ptr(),
-                                                                C.data_ptr(), M, N, K, G, stream))
-        errs = {}
-        for k, f in fns.items():
-            C.zero_()
-            out = f()
-            torch.cuda.synchronize()
-            if isinstance(out, int) and out != 0:
-                errs[k] = f"rc {out}"
-                continue
-            got = out if isinstance(out, torch.Tensor) else C
-            errs[k] = ((got.float() - ref).abs().max() / ref.abs().max()).item()
-        times = {k: [] for k in fns}
-        for _ in range(5):
-            for k, f in fns.items():
-                if isinstance(errs[k], str):
-                    continue
-                times[k].append(ev_time(f, 10))
-        fl = 2.0 * G * M * N * K
-        cells = []
-        for k in fns:
-            if isinstance(errs[k], str) or errs[k] > 2e-2:
-                cells.append(f"{'ERR ' + str(errs[k])[:10]:>16s}")
-            else:
-                t = sorted(times[k])[len(times[k]) // 2]
-                cells.append(f"{t * 1e3:7.1f}us {fl / t / 1e9:5.0f}T")
-        print(f"{name:26s} {fl / 1e9:7.1f} " + " ".join(cells), flush=True)
+    for xbn in (False, True):
+        vs = XVARIANTS if xbn else VARIANTS
+        print(("pending BN + ReLU on A (XBN)" if xbn else "plain A") + ":")
+        print(f"{'shape':26s} {'GFLOP':>7s} " + " ".join(f"{v:>16s}" for v in
+              ["torch.bmm", "conv_pipe16", "conv_big16"] + list(vs.values())))
+        for name, M, N, K in SHAPES:
+            run_shape(name, M, N, K, xbn, vs, dt, stream)
 
+
+def run_shape(name, M, N, K, xbn, vs, dt, stream):
+    A = (torch.rand(G, M, K, device="cuda") * 2 - 1).to(dt)
+    B = (torch.rand(G, N, K, device="cuda") * 2 - 1).to(dt)
+    sc = torch.rand(G, K, device="cuda") + 0.5
+    sh = torch.rand(G, K, device="cuda") - 0.5
+    Ar = torch.relu(A.float() * sc[:, None, :] + sh[:, None, :]).to(dt).float() if xbn else A.float()
+    ref = torch.bmm(Ar, B.float().transpose(1, 2))
+    C = torch.empty(G, M, N, device="cuda", dtype=dt)
+    fns = {"torch.bmm": lambda: torch.bmm(A, B.transpose(1, 2))}
+    Hh = M // 64
+    x_bn = (sc, sh, 1) if xbn else None
+    def conv(big):
+        prev = ops.set_big16(big, 64)
+        try:
+            ops.conv2d_fwd(A, B, C, G, 64, Hh, 1, K, N, 1, 1, 0, x_bn=x_bn)
+        finally:
+            ops.set_big16(prev)
+    fns["conv_pipe16"] = lambda: conv(False)
+    fns["conv_big16"] = lambda: conv(True)
+    for v in vs:
+        fns[vs[v]] = (lambda v=v: lib.probe_gemm_glds(v, A.data_ptr(), B.data_ptr(),
+                                                      C.data_ptr(), M, N, K, G, sc.data_ptr(),
+                                                      sh.data_ptr(), stream))
+    errs = {}
+    for k, f in fns.items():
+        C.zero_()
+        out = f()
+        torch.cuda.synchronize()
+        if isinstance(out, int) and out != 0:
+            errs[k] = f"rc {out}"
+            continue
+        got = out if isinstance(out, torch.Tensor) else C
+        r = ref if k != "torch.bmm" else torch.bmm(A.float(), B.float().transpose(1, 2))
+        errs[k] = ((got.float() - r).abs().max() / r.abs().max()).item()
+    times = {k: [] for k in fns}
+    for _ in range(5):
+        for k, f in fns.items():
+            if isinstance(errs[k], str):
+                continue
+            times[k].append(ev_time(f, 10))
+    fl = 2.0 * G * M * N * K
+    cells = []
+    for k in fns:
+        if isinstance(errs[k], str) or errs[k] > 2e-2:
+            cells.append(f"{'ERR ' + str(errs[k])[:10]:>16s}")
+        else:
+            t = sorted(times[k])[len(times[k]) // 2]
+            cells.append(f"{t * 1e3:7.1f}us {fl / t / 1e9:5.0f}T")
+    print(f"{name:26s} {fl / 1e9:7.1f} " + " ".join(cells), flush=True)
 
 if __name__ == "__main__":
     main()
