@@ -65,65 +65,77 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
   float* red = (float*)smem;  // LDS is free: the main loop ended with a barrier
   if (MODE == FWD && a.st_mean) {
     // per-tile BN statistics of y from the fp32 accumulators (tile mean, then M2 around it),
-    // one partial per SR = min(BM, 128) rows (the granularity the host sizes them with): a
-    // 256-row tile (conv_halo16.hip) writes two, from the waves wm / WPS of each half
-    constexpr int SR = BM > 128 ? 128 : BM, SUB = BM / SR, WPS = WGM / SUB;
-    static_assert(WGM % SUB == 0, "whole waves per statistics sub-tile");
-    const int sub = wm / WPS;
-    const int nvalid = min(SR, a.M - (m0 + sub * SR));
+    // one partial per SR = min(BM, 128) rows (the granularity the host sizes them with).  Each
+    // 32-row accumulator group (mi) of each wave is summed on its own and the groups of a
+    // partial are added in row order — the same float operations whatever the tile's wave
+    // layout (a 128 x 128 tile of 32-row waves, a 256-row tile of 128-row waves), so every
+    // kernel that shares this epilogue writes bit-identical statistics for the same rows
+    constexpr int SR = BM > 128 ? 128 : BM, SUB = BM / SR;
+    constexpr int VW = WGM * MI, VPS = VW / SUB;  // 32-row groups: of the tile, of a partial
+    static_assert(VW % SUB == 0, "whole 32-row groups per statistics sub-tile");
     const int tcol = wn * WN + li;
-    float s1[NI], s2[NI], mean[NI];
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) { s1[ni] = 0.f; s2[ni] = 0.f; }
+    float s1[MI][NI], s2[MI][NI], mean[MI][NI];
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
+      for (int ni = 0; ni < NI; ++ni) {
+        s1[mi][ni] = 0.f;
+        s2[mi][ni] = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row < a.M) s1[ni] += acc[mi][ni][r];
+          if (row < a.M) s1[mi][ni] += acc[mi][ni][r];
         }
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) s1[ni] += __shfl_xor(s1[ni], 32, 64);
+        s1[mi][ni] += __shfl_xor(s1[mi][ni], 32, 64);
+      }
     if (lh == 0) {
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) red[wm * BN + tcol + ni * 32] = s1[ni];
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) red[(wm * MI + mi) * BN + tcol + ni * 32] = s1[mi][ni];
     }
     __syncthreads();
 #pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      float t = 0.f;
+    for (int mi = 0; mi < MI; ++mi) {
+      const int vsub = (wm * MI + mi) / VPS;
+      const int nvalid = min(SR, a.M - (m0 + vsub * SR));
 #pragma unroll
-      for (int w = 0; w < WPS; ++w) t += red[(sub * WPS + w) * BN + tcol + ni * 32];
-      mean[ni] = t / (float)(nvalid > 0 ? nvalid : 1);
+      for (int ni = 0; ni < NI; ++ni) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < VPS; ++w) t += red[(vsub * VPS + w) * BN + tcol + ni * 32];
+        mean[mi][ni] = t / (float)(nvalid > 0 ? nvalid : 1);
+      }
     }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
+      for (int ni = 0; ni < NI; ++ni) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           if (row < a.M) {
-            const float d = acc[mi][ni][r] - mean[ni];
-            s2[ni] += d * d;
+            const float d = acc[mi][ni][r] - mean[mi][ni];
+            s2[mi][ni] += d * d;
           }
         }
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) s2[ni] += __shfl_xor(s2[ni], 32, 64);
+        s2[mi][ni] += __shfl_xor(s2[mi][ni], 32, 64);
+      }
     if (lh == 0) {
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) red[WGM * BN + wm * BN + tcol + ni * 32] = s2[ni];
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          red[VW * BN + (wm * MI + mi) * BN + tcol + ni * 32] = s2[mi][ni];
     }
     __syncthreads();
     const int col = tid % BN, sb = tid / BN, nv = min(SR, a.M - (m0 + sb * SR));
     if (tid < SUB * BN && n0 + col < a.N && nv > 0) {
       float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-      for (int w = 0; w < WPS; ++w) {
-        t1 += red[(sb * WPS + w) * BN + col];
-        t2 += red[WGM * BN + (sb * WPS + w) * BN + col];
+      for (int w = 0; w < VPS; ++w) {
+        t1 += red[(sb * VPS + w) * BN + col];
+        t2 += red[VW * BN + (sb * VPS + w) * BN + col];
       }
       const int mt = m0 / SR + sb;
       const int cn = n0 + col;

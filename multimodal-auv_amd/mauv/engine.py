@@ -35,7 +35,9 @@ TRUNK_STREAMS = os.environ.get("MAUV_TRUNK_STREAMS", "1") == "1"
 # bn1 + ReLU is applied inside the max-pool's loads; training block outputs (bn3 + residual +
 # ReLU) write 1-bit ReLU masks that their backward reads instead of the stored output; a block
 # output's residual gradient dres = dout * mask is never written (the conv1 data gradient adds
-# dout under the mask bits, the downsample BN's backward reads dout with them).
+# dout under the mask bits, the downsample BN's backward reads dout with them).  RES_MASK is not
+# a switch: tests set it False to compare with the path that stores dres (bit-identical).
+RES_MASK = True
 _STREAMS = {}
 
 
@@ -623,7 +625,7 @@ class TrunkRunner(_Runner):
         while self.recs:
             r1, s1, r2, s2, r3, s3, rd, sd = self.recs.pop()
             # the residual gradient: dres = da * mask3, kept implicit when bn3 has mask bits
-            rmask = s3.mask if s3.mask is not None and \
+            rmask = s3.mask if RES_MASK and s3.mask is not None and \
                 (rd is not None or self.dt == torch.float32 or self._masked_addend_ok(r1)) \
                 else None
             dy3, dres = self._bn_bwd(s3, da, want_dres=rmask is None)

@@ -3,18 +3,21 @@
 #   PMC traffic of both conv families on this library (copied where bench.py reads it),
 #   the default bench line, serial kernel statistics of one fp32 and one bf16 step, and
 #   kernel statistics of the f16 inference leg.
-# usage (from the repo root, on the box):  bash tools/gpu_evidence.sh TAG [skip-tests]
+# usage (from the repo root, on the box):  bash tools/gpu_evidence.sh TAG [all|tests|rest]
+#   (a gpurun call is capped at 20 minutes: run "tests" and "rest" as two calls)
 #   outputs under gpurun_out/TAG_*; the traffic summaries as profiles/TAG[_bf16]_conv_traffic.json
 set -o pipefail
 TAG=${1:?tag}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-if [ "$2" != "skip-tests" ]; then
+PART=${2:-all}
+if [ "$PART" != "rest" ]; then
   timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { grep -E "FAILED|Error" gpurun_out/${TAG}_tests.log | head; tail -5 gpurun_out/${TAG}_tests.log; exit 1; }
   tail -1 gpurun_out/${TAG}_tests.log
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
   tail -1 gpurun_out/${TAG}_smoke.log
 fi
+[ "$PART" = "tests" ] && exit 0
 B32="bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-infer --no-bf16 --exact-steps 0 --no-roofline --no-sweep"
 B16="bench.py --dtype bf16 --steps 1 --warmup 0 --no-cpu-baseline --no-infer --no-bf16 --exact-steps 0 --no-roofline --no-sweep"
 for pass in "f32 FETCH_SIZE fetch $B32" "f32 WRITE_SIZE write $B32" "b16 FETCH_SIZE fetch $B16" "b16 WRITE_SIZE write $B16"; do
