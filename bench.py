@@ -512,6 +512,29 @@ def main():
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
 
+    uni = None
+    if not args.no_sweep and world == 1:
+        # BASELINE configs[0] (the reference's unimodal CPU config: ResNet50Custom(3, 7) BNN,
+        # B=8, 224 px, num_mc=5, train/unimodal.py) on the HIP path, beside its CPU baseline
+        progress("configs[0] unimodal leg")
+        torch.manual_seed(0)
+        um = define_models(None, 7, DEFAULT_PRIOR)["image_model"].to(dev)
+        uopt = FusedAdam(um.parameters(), lr=5e-5)
+        xu, _, _, yu = synthetic_batch(8, args.optical, args.sonar, dev, 2)
+
+        def ustep():
+            return mc_train_step(um, (xu,), yu, crit, uopt, args.num_mc, 8, kl_w)
+        ustep()
+        tu = timed(ustep, 10)
+        uni = {"value": round(8 * 10 / tu, 2), "unit": "images/s",
+               "ms_per_step": round(tu / 10 * 1e3, 2), "steps": 10, "batch": 8,
+               "num_mc": args.num_mc, "dtype": "fp32",
+               "config": "configs[0] on the HIP path: ResNet50Custom(3, 7) BNN, B=8, "
+                         f"{args.optical} px, num_mc={args.num_mc}"}
+        del um, uopt
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
     infer = None
     if not args.no_infer:
         progress("inference leg")
@@ -622,7 +645,7 @@ def main():
             "f32_math": f32_math if args.dtype == "fp32" else None,
             "fp32_exact_mfma": exact,
             "inference": infer, "infer_sweep": infer_sweep, "bf16_train": bf16,
-            "train_sweep": sweep, "roofline": roof, "comm": comm,
+            "train_sweep": sweep, "configs0_unimodal": uni, "roofline": roof, "comm": comm,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
