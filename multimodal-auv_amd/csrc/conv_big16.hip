@@ -27,7 +27,45 @@ namespace {
 
 constexpr int BK = 64;
 constexpr unsigned kOOBb = 0x7ffffff0u;
-constexpr int kMaxXbnB = 512;  // pending-BN input channels staged in LDS
+constexpr int kMaxXbnB = 512;   // pending-BN input channels staged in LDS
+constexpr int kMaxFold = 2048;  // fold: block-output channels whose BN parameters sit in LDS
+
+__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
+// The block output relu(y*sc + sh + r) of one 8-channel chunk, r = res or res*rsc + rsh (the
+// downsample branch's pending BN): bn_apply_rows' fp32 operations (bn.hip: two fmas, one add,
+// ReLU, one rounding to the 16-bit format), so the value written through and fed to the MFMAs
+// is the one that pass would have stored.  tab = [sc | sh | rsc | rsh] x kMaxFold in LDS.
+template <int DT, bool RBN>
+__device__ __forceinline__ u32x4 fold8(u32x4 y, u32x4 r, const float* tab, int ch, bool ok) {
+  const floatx8 yf = unpack8<DT>(y), rf = unpack8<DT>(r);
+  const floatx8 sc = ldf8(tab + ch), sh = ldf8(tab + kMaxFold + ch);
+  floatx8 rsc, rsh;
+  if constexpr (RBN) {
+    rsc = ldf8(tab + 2 * kMaxFold + ch);
+    rsh = ldf8(tab + 3 * kMaxFold + ch);
+  }
+  u32x4 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float f[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int k = 2 * i + e;
+      float v = __builtin_fmaf(yf[k], sc[k], sh[k]);
+      float rv = rf[k];
+      if constexpr (RBN) rv = __builtin_fmaf(rv, rsc[k], rsh[k]);
+      asm("" : "+v"(v), "+v"(rv));  // no contraction across the add (bn_apply_rows rounds here)
+      v = v + rv;
+      f[e] = v > 0.f ? v : 0.f;
+    }
+    const unsigned p = pk2<DT>(f[0], f[1]);
+    o[i] = ok ? p : 0u;
+  }
+  return o;
+}
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
@@ -53,16 +91,22 @@ struct WavesB {
 
 }  // namespace
 
-template <int DT, int BM, int BN, bool XBN>
+// RES (fold, 1x1 stride-1 only): 0 = off; 1 = A is relu(x*xsc + xsh + rs) (identity residual),
+// 2 = relu(x*xsc + xsh + rs*rs_sc + rs_sh); the column-tile-0 blocks write A through to fout
+template <int DT, int BM, int BN, bool XBN, int RES = 0>
 __global__ __launch_bounds__(512, 2) void conv_big16(const ConvArgs a) {
   constexpr int NT = 512, NW = 8;
   constexpr int WGM = WavesB<BM, BN>::M, WGN = WavesB<BM, BN>::N;
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
   constexpr int A_B = BM * 128, B_B = BN * 128, STG = A_B + B_B;  // bytes
   constexpr int RA = BM / NW, RB = BN / NW, JA = RA / 8, JB = RB / 8, J = JA + JB;
-  constexpr int XOFF = 2 * STG, XB = XBN ? 2 * kMaxXbnB * 4 : 0;
+  constexpr bool XF = XBN || RES != 0;  // a transform of the landed A tile
+  constexpr int XS = RES ? kMaxFold : kMaxXbnB;  // stride of the parameter tables
+  constexpr int XOFF = 2 * STG;
+  constexpr int XB = RES ? (RES == 2 ? 4 : 2) * kMaxFold * 4 : (XBN ? 2 * kMaxXbnB * 4 : 0);
   constexpr int PR = BM / WGM, EPI = PR * (BN + 4) * 4;  // epilogue16's per-pass staging
   constexpr int LDSB = XOFF + XB > EPI ? XOFF + XB : EPI;
+  static_assert(LDSB <= 160 * 1024, "LDS");
   constexpr int TCH = BM * 8 / NT;  // A chunks each thread transforms per stage (XBN)
   // ONE shared array (a second __shared__ object makes hipcc wait vmcnt(0) before ds_reads)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[LDSB];
@@ -100,8 +144,8 @@ __global__ __launch_bounds__(512, 2) void conv_big16(const ConvArgs a) {
     bbase[j] = n0 + r < a.N ? (unsigned)(((n0 + r) * a.K + 8 * c) * 2) : kOOBb;
   }
   // XBN transform: this thread's rows (tid >> 3) + 64 i and their input pixel origins
-  int tp0[XBN ? TCH : 1], tp1[XBN ? TCH : 1];
-  if constexpr (XBN) {
+  int tp0[XF ? TCH : 1], tp1[XF ? TCH : 1];
+  if constexpr (XF) {
 #pragma unroll
     for (int i = 0; i < TCH; ++i) {
       const int m = m0 + (tid >> 3) + (NT / 8) * i, mm = m < a.M ? m : 0;
@@ -111,9 +155,30 @@ __global__ __launch_bounds__(512, 2) void conv_big16(const ConvArgs a) {
     }
     for (int i = tid; i < a.Cin; i += NT) {
       xbn[i] = a.xsc[g * a.Cin + i];
-      xbn[kMaxXbnB + i] = a.xsh[g * a.Cin + i];
+      xbn[XS + i] = a.xsh[g * a.Cin + i];
+      if constexpr (RES == 2) {
+        xbn[2 * XS + i] = a.rs_sc[g * a.Cin + i];
+        xbn[3 * XS + i] = a.rs_sh[g * a.Cin + i];
+      }
     }
   }
+  // fold: this thread's residual chunks (the rows / slots it transforms, 1x1: pixel = row) reach
+  // registers one stage ahead, issued after the transform that frees them
+  u32x4 rres[RES ? TCH : 1];
+  unsigned roff[RES ? TCH : 1];
+  __amdgpu_buffer_rsrc_t rr = ra;
+  if constexpr (RES) {
+    rr = rsrcb((const u16*)a.rs + (long long)g * a.xs_g, (long long)a.B * a.xs_b);
+#pragma unroll
+    for (int i = 0; i < TCH; ++i) {
+      const int row = (tid >> 3) + (NT / 8) * i, c = (tid & 7) ^ ((row >> 1) & 7);
+      roff[i] = m0 + row < a.M ? (unsigned)(((m0 + row) * a.Cin + 8 * c) * 2) : kOOBb;
+    }
+  }
+  auto load_res = [&](int kc) {
+#pragma unroll
+    for (int i = 0; i < TCH; ++i) rres[i] = bload16(rr, roff[i] + (unsigned)(kc * 2));
+  };
 
   const int nt = a.K / BK;
   int t_r = 0, t_s = 0, t_c = 0;  // k position of the next stage to issue
@@ -171,18 +236,22 @@ __global__ __launch_bounds__(512, 2) void conv_big16(const ConvArgs a) {
   const unsigned rfloor = a.xrelu ? 0u : 0x80008000u;
   int x_r = 0, x_s = 0, x_c = 0;  // k position of the stage being transformed
   issue(0);
-  if constexpr (XBN) block_sync();  // xbn staged
+  if constexpr (RES != 0) load_res(0);
+  if constexpr (XF) block_sync();  // xbn staged
   for (int t = 0; t < nt; ++t) {
-    // tile t + 1 goes to the buffer tile t - 1 was read from (free since the barrier ending t - 1)
-    if (t + 1 < nt) {
+    // tile t + 1 goes to the buffer tile t - 1 was read from (free since the barrier ending t - 1).
+    // Fold: issued unconditionally (past the last stage the descriptors return zeros into the
+    // idle buffer), so hipcc's own wait for the residual registers counts these DMAs on every
+    // path instead of draining them (vmcnt(0)) before the transform
+    if (RES != 0 || t + 1 < nt) {
       issue(t + 1);
-      wait_vm<J>();   // this wave's DMAs of tile t have landed
+      wait_vm<J>();   // this wave's DMAs of tile t (and the residual chunks issued before) landed
     } else {
       wait_vm<0>();
     }
     __builtin_amdgcn_s_barrier();  // every wave's DMAs of tile t have landed
     asm volatile("" ::: "memory");
-    if constexpr (XBN) {
+    if constexpr (XF) {
       unsigned char* As = smem + (t & 1) * STG;
 #pragma unroll
       for (int i = 0; i < TCH; ++i) {
@@ -191,14 +260,28 @@ __global__ __launch_bounds__(512, 2) void conv_big16(const ConvArgs a) {
         const bool ok = ((unsigned)(tp0[i] + x_r) < (unsigned)a.H) &
                         ((unsigned)(tp1[i] + x_s) < (unsigned)a.W);
         u32x4* p = (u32x4*)(As + idx * 16);
-        *p = bn_relu8<DT>(*p, ldf8(xbn + ch), ldf8(xbn + kMaxXbnB + ch), rfloor, ok);
+        if constexpr (RES != 0) {
+          const u32x4 v = fold8<DT, RES == 2>(*p, rres[i], xbn, ch, ok);
+          *p = v;
+          if (n0 == 0 && m0 + row < a.M)
+            *(u32x4*)((u16*)a.fout + (long long)g * a.xs_g + (long long)(m0 + row) * a.Cin + ch) = v;
+        } else {
+          *p = bn_relu8<DT>(*p, ldf8(xbn + ch), ldf8(xbn + kMaxXbnB + ch), rfloor, ok);
+        }
       }
+      // 1x1: stage t + 1 covers the next 64 channels (past the last: zeros or unused values)
+      if constexpr (RES != 0) load_res(x_c + BK);
       x_c += BK;
       if (x_c >= a.Cin) { x_c = 0; if (++x_s == a.S) { x_s = 0; ++x_r; } }
       block_sync();
     }
     compute(t);
     block_sync();  // tile t's buffer is free for the DMA issued next
+  }
+  if constexpr (RES != 0) {  // the DMAs past the last stage land before the epilogue reuses LDS
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
   epilogue16<FWD, DT, BM, BN, MI, NI, WGM, WGN, 2 * STG>(a, acc, smem, m0, n0, g);
 }
@@ -224,6 +307,38 @@ bool conv_big16_launch(int dt, const ConvArgs& a, hipStream_t st) {
   else MAUV_BIG_DT(DT_F16);
 #undef MAUV_BIG_DT
 #undef MAUV_BIG_LAUNCH
+  return true;
+}
+
+// true: launched.  a: conv_pipe16_launch-style FWD arguments of a 1x1 / stride-1 conv over a
+// contiguous [G][B][H][W][Cin] input, plus xsc / xsh (the block output's BN) and rs (the
+// residual, same layout as x), rs_sc / rs_sh (nullable), fout (the block output, same layout).
+bool conv_big16_fold_launch(int dt, const ConvArgs& a, hipStream_t st) {
+  if (a.cpg || a.R != 1 || a.S != 1 || a.stride != 1 || a.pad != 0 || a.Cin % 64 ||
+      a.Cin > kMaxFold || a.K != a.Cin || !a.xsc || !a.xsh || !a.rs || !a.fout)
+    return false;
+  if (a.xs_c != 1 || a.xs_w != a.Cin || a.xs_h != (long long)a.W * a.Cin ||
+      a.xs_b != (long long)a.H * a.W * a.Cin || a.xs_g % 8)
+    return false;
+  if ((long long)a.B * a.xs_b * 2 > 0x7fff0000LL || a.ws_g * 2 > 0x7fff0000LL) return false;
+  if (a.M <= 64) return false;  // the statistics partials are 128-row (conv_tile_rows)
+  ConvArgs c = a;
+  c.xrelu = 1;
+  c.xcd_grid = 1;
+  const bool rbn = a.rs_sc != nullptr;
+  const int BN = a.N >= 256 ? 256 : 128;
+  const dim3 grid(ceil_div(a.M, 256) * ceil_div(a.N, BN), a.G);
+#define MAUV_FOLD_LAUNCH(D, N_, R_) \
+  hipLaunchKernelGGL((conv_big16<D, 256, N_, false, R_>), grid, dim3(512), 0, st, c)
+#define MAUV_FOLD_DT(D)                                                                  \
+  do {                                                                                   \
+    if (BN == 256) { if (rbn) MAUV_FOLD_LAUNCH(D, 256, 2); else MAUV_FOLD_LAUNCH(D, 256, 1); } \
+    else { if (rbn) MAUV_FOLD_LAUNCH(D, 128, 2); else MAUV_FOLD_LAUNCH(D, 128, 1); }          \
+  } while (0)
+  if (dt == DT_BF16) MAUV_FOLD_DT(DT_BF16);
+  else MAUV_FOLD_DT(DT_F16);
+#undef MAUV_FOLD_DT
+#undef MAUV_FOLD_LAUNCH
   return true;
 }
 

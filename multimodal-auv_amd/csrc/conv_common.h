@@ -34,6 +34,12 @@ struct ConvArgs {
   const float* xsc;
   const float* xsh;
   int xrelu;
+  // FWD with the previous bottleneck's output formed on load (conv_big16 fold, 1x1 only): the
+  // A operand is relu(x*xsc + xsh + r), r = rs or rs*rs_sc + rs_sh (rs_sc non-null: the
+  // downsample branch's pending BN); the blocks of column tile 0 write it through to fout
+  const void* rs;
+  const float *rs_sc, *rs_sh;
+  void* fout;
   // FWD epilogue BN statistics partials [G][st_nblk][N] (+ counts [G][st_nblk])
   float *st_mean, *st_m2, *st_cnt;
   int st_nblk, st_base;
@@ -154,6 +160,9 @@ bool conv_split_launch(int mode, const ConvArgs& a, int oneacc, hipStream_t st);
 bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
 // 16-bit forwards on 256-row tiles with LDS-DMA operands (conv_big16.hip); false: not covered
 bool conv_big16_launch(int dt, const ConvArgs& a, hipStream_t st);
+// the same kernel forming the previous block's output on load (ConvArgs::rs / fout); false:
+// shape not covered (nothing launched)
+bool conv_big16_fold_launch(int dt, const ConvArgs& a, hipStream_t st);
 // 3x3 / stride-1 forwards and data gradients over 64 -> 64 channels through an LDS image of the
 // input rows (conv_halo16.hip); false: shape not covered (or mauv_set_halo3(0))
 bool conv_halo16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);

@@ -550,6 +550,40 @@ MAUV_API int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_st
   return check_launch("conv2d_fwd_h16");
 }
 
+// A bottleneck's conv1 (1x1, stride 1) whose input is the previous block's output, formed while
+// its tiles are loaded: out = relu(y*scale + shift + r), r = res or res*res_scale + res_shift
+// (conv_big16.hip's fold; bn_apply's arithmetic), written through once and fed to the GEMM.
+// 0: launched; 1: shape outside the kernel (nothing launched: the caller runs mauv_bn_apply,
+// then mauv_conv2d_fwd_h16 on its output); < 0: argument error.
+MAUV_API int mauv_conv2d_fwd_fold_h16(int dtype, const void* y, const float* scale,
+                                      const float* shift, const void* res, const float* res_scale,
+                                      const float* res_shift, void* out, const void* w, void* y1,
+                                      int G, int B, int H, int W, int Cin, int Cout,
+                                      float* st_mean, float* st_m2, float* st_cnt,
+                                      hipStream_t stream) {
+  if (int e = check_shape16("conv2d_fwd_fold_h16", dtype, G, B, Cin, Cout, nullptr)) return e;
+  if (!y || !scale || !shift || !res || !out || !w || !y1 || !res_scale != !res_shift) {
+    set_error("conv2d_fwd_fold_h16: y, scale, shift, res, out, w, y1 required; res_scale and "
+              "res_shift together");
+    return kErrArg;
+  }
+  if (!aligned16(y) || !aligned16(res) || !aligned16(out) || !aligned16(w)) {
+    set_error("conv2d_fwd_fold_h16: y, res, out, w must be 16-B aligned");
+    return kErrArg;
+  }
+  ConvArgs16 h = make_args16(G, B, H, W, Cin, Cout, 1, 1, 1, 0, nullptr);
+  h.x = (const u16*)y; h.w = (const u16*)w; h.out = y1;
+  h.xsc = scale; h.xsh = shift; h.xrelu = 1;
+  h.M = B * H * W; h.N = Cout; h.K = Cin;
+  h.out_sg = (long long)h.M * h.N;
+  h.st_mean = st_mean; h.st_m2 = st_m2; h.st_cnt = st_cnt;
+  h.st_nblk = ceil_div(h.M, conv_tile_rows(h.M));
+  ConvArgs a = pipe_args(h);
+  a.rs = res; a.rs_sc = res_scale; a.rs_sh = res_shift; a.fout = out;
+  if (!conv_big16_fold_launch(dtype, a, stream)) return 1;
+  return check_launch("conv2d_fwd_fold_h16");
+}
+
 // 16-bit counterpart of mauv_stem_fwd_f32 (conv_gemm.hip): the pipelined kernel over the
 // shared im2col rows with the G weight sets stacked along N; Kp % 64 == 0.
 MAUV_API int mauv_stem_fwd_h16(int dtype, const void* cols, const void* w, void* y, int G,

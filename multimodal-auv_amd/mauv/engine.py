@@ -38,6 +38,11 @@ TRUNK_STREAMS = os.environ.get("MAUV_TRUNK_STREAMS", "1") == "1"
 # dout under the mask bits, the downsample BN's backward reads dout with them).  RES_MASK is not
 # a switch: tests set it False to compare with the path that stores dres (bit-identical).
 RES_MASK = True
+# Without a backward (16-bit inference / no-grad evaluation) a block output is not a separate
+# pass: the next block's conv1 forms relu(bn3(y3) + residual) while loading its tiles and writes
+# it through once (ops.conv2d_fwd_fold).  Test hook like RES_MASK: tests set it
+# False to compare with bn_apply + conv1 (bit-identical).
+FOLD = True
 _STREAMS = {}
 
 
@@ -385,24 +390,38 @@ class TrunkRunner(_Runner):
         return Cin if Cin % q == 0 else (Cin + q - 1) // q * q
 
     # ---- conv / bn units ----
-    def _conv(self, conv, x, B, H, W, x_strides=None, x_bn=None, bn_stats=True):
+    def _conv(self, conv, x, B, H, W, x_strides=None, x_bn=None, bn_stats=True, fold=None):
+        """fold = (y3, scale, shift, res, res_bn): x is the previous bottleneck's output, not yet
+        materialised; this 1x1 conv forms it on load (ops.conv2d_fwd_fold) and self.fold_out
+        holds it afterwards."""
         G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
         st, pd = conv.stride[0], conv.padding[0]
         cp = self._cin_pad(Cin)
         alloc = torch.zeros if cp != Cin else torch.empty
-        w = alloc(G, Cout, k, k, cp, device=x.device, dtype=self.dt)
+        dev = x.device if fold is None else fold[0].device
+        w = alloc(G, Cout, k, k, cp, device=dev, dtype=self.dt)
         self._sample(conv, conv.mu_kernel, conv.rho_kernel, "kernel", w, Cout, Cin, k * k,
                      cin_pad=cp)
         Ho, Wo = ops.out_hw(H, k, st, pd), ops.out_hw(W, k, st, pd)
-        y = torch.empty(G, B, Ho, Wo, Cout, device=x.device, dtype=self.dt)
+        y = torch.empty(G, B, Ho, Wo, Cout, device=dev, dtype=self.dt)
         part = None
         if bn_stats:
             nblk = ops.fwd_stat_blocks(G, B, H, W, Cin, Cout, k, st, pd)
-            buf = torch.empty(2 * G * nblk * Cout + G * nblk, device=x.device)
+            buf = torch.empty(2 * G * nblk * Cout + G * nblk, device=dev)
             part = (buf[:G * nblk * Cout], buf[G * nblk * Cout:2 * G * nblk * Cout],
                     buf[2 * G * nblk * Cout:], nblk)
-        ops.conv2d_fwd(x, w, y, G, B, H, W, cp, Cout, k, st, pd, x_strides=x_strides,
-                       x_bn=x_bn, stats=None if part is None else part[:3], alg_cin=Cin)
+        stats = None if part is None else part[:3]
+        if fold is not None:
+            y3, sc, sh, res, res_bn = fold
+            x = torch.empty_like(y3)
+            if not ops.conv2d_fwd_fold(y3, sc, sh, res, res_bn, x, w, y, G, B, H, W, Cin, Cout,
+                                       stats=stats):
+                ops.bn_apply(y3, sc, sh, res, 1, x, G, B * H * W, Cin, res_bn=res_bn)
+                ops.conv2d_fwd(x, w, y, G, B, H, W, cp, Cout, k, st, pd, stats=stats)
+            self.fold_out = x
+        else:
+            ops.conv2d_fwd(x, w, y, G, B, H, W, cp, Cout, k, st, pd, x_strides=x_strides,
+                           x_bn=x_bn, stats=stats, alg_cin=Cin)
         rec = (conv, x, x_strides, x_bn, w, B, H, W) if self.save else None
         return y, rec, part
 
@@ -575,8 +594,17 @@ class TrunkRunner(_Runner):
         self.stem = (rc, rb, idx, (H, W)) if self.save else None
         del idx
         cur, H, W = p, Hp, Wp
-        for blk in t.blocks():
-            y1, r1, p1 = self._conv(blk.conv1, cur, B, H, W)
+        blocks = list(t.blocks())
+        # without a backward to feed (inference, no-grad evaluation) a 16-bit block output is
+        # formed by the next block's conv1 while it loads its tiles (ops.conv2d_fwd_fold)
+        fold_ok = FOLD and not self.save and self.dt != torch.float32
+        pend = None
+        for i, blk in enumerate(blocks):
+            if pend is not None:
+                y1, r1, p1 = self._conv(blk.conv1, None, B, H, W, fold=pend)
+                cur, pend, self.fold_out = self.fold_out, None, None
+            else:
+                y1, r1, p1 = self._conv(blk.conv1, cur, B, H, W)
             _, s1 = self._bn(blk.bn1, y1, p1, relu=True, materialize=False)
             y2, r2, p2 = self._conv(blk.conv2, y1, B, H, W, x_bn=self.last_lazy)
             H2, W2 = y2.shape[2], y2.shape[3]
@@ -589,7 +617,14 @@ class TrunkRunner(_Runner):
                 res_bn = self.last_lazy[:2]
             else:
                 res = cur
-            a3, s3 = self._bn(blk.bn3, y3, p3, relu=True, res=res, res_bn=res_bn)
+            nxt = blocks[i + 1].conv1 if i + 1 < len(blocks) else None
+            if fold_ok and nxt is not None and nxt.kernel_size == (1, 1) and \
+                    nxt.stride == (1, 1) and nxt.padding == (0, 0):
+                _, s3 = self._bn(blk.bn3, y3, p3, relu=True, materialize=False)
+                pend = (y3,) + self.last_lazy[:2] + (res, res_bn)
+                a3 = None
+            else:
+                a3, s3 = self._bn(blk.bn3, y3, p3, relu=True, res=res, res_bn=res_bn)
             del res
             if self.save:
                 recs.append((r1, s1, r2, s2, r3, s3, rd, sd))
