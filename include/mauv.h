@@ -125,16 +125,17 @@ int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_strides,
  * models/base_models.py:74-90, followed by the next block's conv1):
  *   out = relu(y*scale + shift + r),  r = res, or res*res_scale + res_shift (the downsample
  *   branch's BN, res_scale / res_shift both non-NULL), per (group, channel) [G][Cin] parameters;
- * `out` ([G][B][H][W][Cin], written once) gets exactly mauv_bn_apply's values and y1 / the
+ * `out` ([G][B][H][W][Cin], written once) gets exactly mauv_bn_apply's values (out_mask,
+ * nullable: mauv_bn_apply_mask's ReLU bits of it, for a training step) and y1 / the
  * statistics partials exactly mauv_conv2d_fwd_h16's on that `out`.  y, res: contiguous
  * [G][B][H][W][Cin]; Cin % 64 == 0, Cin <= 2048.  Returns 0 when launched, 1 when the shape is
  * outside the kernel (nothing launched: run mauv_bn_apply, then mauv_conv2d_fwd_h16), < 0 on an
  * argument error. */
 int mauv_conv2d_fwd_fold_h16(int dtype, const void* y, const float* scale, const float* shift,
                              const void* res, const float* res_scale, const float* res_shift,
-                             void* out, const void* w, void* y1, int G, int B, int H, int W,
-                             int Cin, int Cout, float* st_mean, float* st_m2, float* st_cnt,
-                             hipStream_t stream);
+                             void* out, unsigned char* out_mask, const void* w, void* y1, int G,
+                             int B, int H, int W, int Cin, int Cout, float* st_mean,
+                             float* st_m2, float* st_cnt, hipStream_t stream);
 int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, void* dx,
                              const void* addend, int accumulate, int G, int B, int H, int W,
                              int Cin, int Cout, int R, int S, int stride, int pad,

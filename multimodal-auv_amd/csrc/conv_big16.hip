@@ -263,8 +263,17 @@ __global__ __launch_bounds__(512, 2) void conv_big16(const ConvArgs a) {
         if constexpr (RES != 0) {
           const u32x4 v = fold8<DT, RES == 2>(*p, rres[i], xbn, ch, ok);
           *p = v;
-          if (n0 == 0 && m0 + row < a.M)
-            *(u32x4*)((u16*)a.fout + (long long)g * a.xs_g + (long long)(m0 + row) * a.Cin + ch) = v;
+          if (n0 == 0 && m0 + row < a.M) {
+            const long long o = (long long)g * a.xs_g + (long long)(m0 + row) * a.Cin + ch;
+            *(u32x4*)((u16*)a.fout + o) = v;
+            if (a.fmask) {  // ReLU output: a stored value is > 0 exactly when its bits are not 0
+              unsigned mb = 0;
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                mb |= ((v[e] & 0xffffu) ? 1u : 0u) << (2 * e) | ((v[e] >> 16) ? 1u : 0u) << (2 * e + 1);
+              a.fmask[o >> 3] = (unsigned char)mb;
+            }
+          }
         } else {
           *p = bn_relu8<DT>(*p, ldf8(xbn + ch), ldf8(xbn + kMaxXbnB + ch), rfloor, ok);
         }

@@ -36,10 +36,12 @@ struct ConvArgs {
   int xrelu;
   // FWD with the previous bottleneck's output formed on load (conv_big16 fold, 1x1 only): the
   // A operand is relu(x*xsc + xsh + r), r = rs or rs*rs_sc + rs_sh (rs_sc non-null: the
-  // downsample branch's pending BN); the blocks of column tile 0 write it through to fout
+  // downsample branch's pending BN); the blocks of column tile 0 write it through to fout and,
+  // with fmask, its ReLU-mask bits (bn_apply_mask's: bit e of byte o / 8 = stored value > 0)
   const void* rs;
   const float *rs_sc, *rs_sh;
   void* fout;
+  unsigned char* fmask;
   // FWD epilogue BN statistics partials [G][st_nblk][N] (+ counts [G][st_nblk])
   float *st_mean, *st_m2, *st_cnt;
   int st_nblk, st_base;

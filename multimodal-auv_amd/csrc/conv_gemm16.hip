@@ -552,13 +552,15 @@ MAUV_API int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_st
 
 // A bottleneck's conv1 (1x1, stride 1) whose input is the previous block's output, formed while
 // its tiles are loaded: out = relu(y*scale + shift + r), r = res or res*res_scale + res_shift
-// (conv_big16.hip's fold; bn_apply's arithmetic), written through once and fed to the GEMM.
+// (conv_big16.hip's fold; bn_apply's arithmetic), written through once (with out_mask non-null
+// also its ReLU-mask bits, mauv_bn_apply_mask's) and fed to the GEMM.
 // 0: launched; 1: shape outside the kernel (nothing launched: the caller runs mauv_bn_apply,
 // then mauv_conv2d_fwd_h16 on its output); < 0: argument error.
 MAUV_API int mauv_conv2d_fwd_fold_h16(int dtype, const void* y, const float* scale,
                                       const float* shift, const void* res, const float* res_scale,
-                                      const float* res_shift, void* out, const void* w, void* y1,
-                                      int G, int B, int H, int W, int Cin, int Cout,
+                                      const float* res_shift, void* out, unsigned char* out_mask,
+                                      const void* w, void* y1, int G, int B, int H, int W,
+                                      int Cin, int Cout,
                                       float* st_mean, float* st_m2, float* st_cnt,
                                       hipStream_t stream) {
   if (int e = check_shape16("conv2d_fwd_fold_h16", dtype, G, B, Cin, Cout, nullptr)) return e;
@@ -579,7 +581,7 @@ MAUV_API int mauv_conv2d_fwd_fold_h16(int dtype, const void* y, const float* sca
   h.st_mean = st_mean; h.st_m2 = st_m2; h.st_cnt = st_cnt;
   h.st_nblk = ceil_div(h.M, conv_tile_rows(h.M));
   ConvArgs a = pipe_args(h);
-  a.rs = res; a.rs_sc = res_scale; a.rs_sh = res_shift; a.fout = out;
+  a.rs = res; a.rs_sc = res_scale; a.rs_sh = res_shift; a.fout = out; a.fmask = out_mask;
   if (!conv_big16_fold_launch(dtype, a, stream)) return 1;
   return check_launch("conv2d_fwd_fold_h16");
 }

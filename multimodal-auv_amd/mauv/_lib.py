@@ -36,7 +36,7 @@ SIGNATURES = {
     "mauv_set_big16": [I, I],
     # conv_gemm16.hip
     "mauv_conv2d_fwd_h16": [I, P, P, P, P, I, P, P] + [I] * 10 + [P, P, P, P],
-    "mauv_conv2d_fwd_fold_h16": [I] + [P] * 9 + [I] * 6 + [P, P, P, P],
+    "mauv_conv2d_fwd_fold_h16": [I] + [P] * 10 + [I] * 6 + [P, P, P, P],
     "mauv_conv2d_bwd_data_h16": [I, P, P, P, P, I] + [I] * 10 + [P],
     "mauv_conv2d_bwd_data_bn_h16": [I, P, P, P, P, I] + [I] * 10 + [P] * 8 + [I, P, P, P],
     "mauv_reparam_sample_ex": [I, P, P, P, ctypes.c_ulonglong, ctypes.c_ulonglong, P, ctypes.c_uint,

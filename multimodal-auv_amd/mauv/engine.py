@@ -38,12 +38,20 @@ TRUNK_STREAMS = os.environ.get("MAUV_TRUNK_STREAMS", "1") == "1"
 # dout under the mask bits, the downsample BN's backward reads dout with them).  RES_MASK is not
 # a switch: tests set it False to compare with the path that stores dres (bit-identical).
 RES_MASK = True
-# Without a backward (16-bit inference / no-grad evaluation) a block output is not a separate
-# pass: the next block's conv1 forms relu(bn3(y3) + residual) while loading its tiles and writes
-# it through once (ops.conv2d_fwd_fold).  Test hook like RES_MASK: tests set it
-# False to compare with bn_apply + conv1 (bit-identical).
+# A 16-bit block output is not a separate pass: the next block's conv1 forms relu(bn3(y3) +
+# residual) while loading its tiles and writes it through once, with its ReLU-mask bits when a
+# backward will read them (ops.conv2d_fwd_fold) — where the launch has at least
+# FOLD_MIN_TILES 256-row tiles (two rounds of the chip's CUs; fewer ran slower than the two
+# passes).  Test hooks like RES_MASK: tests set FOLD False to compare with bn_apply + conv1
+# (bit-identical) and FOLD_MIN_TILES 0 to fold their small shapes.
 FOLD = True
+FOLD_MIN_TILES = 512
 _STREAMS = {}
+
+
+def _first(v):
+    """A conv attribute as one int (bayesian-torch keeps kernel_size an int, torch a tuple)."""
+    return v if isinstance(v, int) else v[0]
 
 
 def _trunk_streams(dev):
@@ -391,9 +399,9 @@ class TrunkRunner(_Runner):
 
     # ---- conv / bn units ----
     def _conv(self, conv, x, B, H, W, x_strides=None, x_bn=None, bn_stats=True, fold=None):
-        """fold = (y3, scale, shift, res, res_bn): x is the previous bottleneck's output, not yet
-        materialised; this 1x1 conv forms it on load (ops.conv2d_fwd_fold) and self.fold_out
-        holds it afterwards."""
+        """fold = (y3, scale, shift, res, res_bn, mask): x is the previous bottleneck's output,
+        not yet materialised; this 1x1 conv forms it on load (ops.conv2d_fwd_fold; mask: its ReLU
+        bits too) and self.fold_out holds it afterwards."""
         G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
         st, pd = conv.stride[0], conv.padding[0]
         cp = self._cin_pad(Cin)
@@ -412,11 +420,14 @@ class TrunkRunner(_Runner):
                     buf[2 * G * nblk * Cout:], nblk)
         stats = None if part is None else part[:3]
         if fold is not None:
-            y3, sc, sh, res, res_bn = fold
+            y3, sc, sh, res, res_bn, mask = fold
             x = torch.empty_like(y3)
             if not ops.conv2d_fwd_fold(y3, sc, sh, res, res_bn, x, w, y, G, B, H, W, Cin, Cout,
-                                       stats=stats):
-                ops.bn_apply(y3, sc, sh, res, 1, x, G, B * H * W, Cin, res_bn=res_bn)
+                                       stats=stats, mask=mask):
+                if mask is not None:
+                    ops.bn_apply_mask(y3, sc, sh, res, x, mask, G, B * H * W, Cin, res_bn=res_bn)
+                else:
+                    ops.bn_apply(y3, sc, sh, res, 1, x, G, B * H * W, Cin, res_bn=res_bn)
                 ops.conv2d_fwd(x, w, y, G, B, H, W, cp, Cout, k, st, pd, stats=stats)
             self.fold_out = x
         else:
@@ -434,6 +445,15 @@ class TrunkRunner(_Runner):
         lim = 0x7fff0000 // 2
         return conv.out_channels % 64 == 0 and \
             B * H * W * max(conv.in_channels, conv.out_channels) <= lim
+
+    def _fold_fits(self, conv, B, H, W):
+        """conv (the next block's conv1) can form the block output on load: a 1x1 / stride-1
+        conv with at least FOLD_MIN_TILES 256-row tiles in its launch."""
+        if _first(conv.kernel_size) != 1 or _first(conv.stride) != 1 or _first(conv.padding) != 0:
+            return False
+        N = conv.out_channels
+        tiles = -(-B * H * W // 256) * self.G * -(-N // (256 if N >= 256 else 128))
+        return tiles >= FOLD_MIN_TILES
 
     def _conv_bwd(self, rec, dy, need_dx=True, addend=None, dx=None, accumulate=False,
                   addend_mask=None):
@@ -595,9 +615,9 @@ class TrunkRunner(_Runner):
         del idx
         cur, H, W = p, Hp, Wp
         blocks = list(t.blocks())
-        # without a backward to feed (inference, no-grad evaluation) a 16-bit block output is
-        # formed by the next block's conv1 while it loads its tiles (ops.conv2d_fwd_fold)
-        fold_ok = FOLD and not self.save and self.dt != torch.float32
+        # a 16-bit block output is formed by the next block's conv1 while it loads its tiles
+        # (ops.conv2d_fwd_fold)
+        fold_ok = FOLD and self.dt != torch.float32
         pend = None
         for i, blk in enumerate(blocks):
             if pend is not None:
@@ -618,10 +638,13 @@ class TrunkRunner(_Runner):
             else:
                 res = cur
             nxt = blocks[i + 1].conv1 if i + 1 < len(blocks) else None
-            if fold_ok and nxt is not None and nxt.kernel_size == (1, 1) and \
-                    nxt.stride == (1, 1) and nxt.padding == (0, 0):
+            if fold_ok and nxt is not None and self._fold_fits(nxt, B, H2, W2):
                 _, s3 = self._bn(blk.bn3, y3, p3, relu=True, materialize=False)
-                pend = (y3,) + self.last_lazy[:2] + (res, res_bn)
+                mask = None
+                if self.save:   # the backward reads the block output's ReLU bits (_bn's rule)
+                    mask = torch.empty(y3.numel() // 8, dtype=torch.uint8, device=y3.device)
+                    s3.mask = mask
+                pend = (y3,) + self.last_lazy[:2] + (res, res_bn, mask)
                 a3 = None
             else:
                 a3, s3 = self._bn(blk.bn3, y3, p3, relu=True, res=res, res_bn=res_bn)

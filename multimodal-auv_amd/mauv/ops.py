@@ -168,25 +168,30 @@ def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_stri
 
 
 def conv2d_fwd_fold(y, scale, shift, res, res_bn, out, w, y1, G, B, H, W, Cin, Cout,
-                    stats=None):
+                    stats=None, mask=None):
     """A bottleneck's 1x1 conv1 over the previous block's output formed on load
     (mauv_conv2d_fwd_fold_h16): out = relu(y*scale + shift + res'), res' = res or
-    res*res_scale + res_shift (res_bn), is written through exactly as bn_apply would write it and
-    y1 = conv1x1(out) exactly as conv2d_fwd would compute it.  True: done; False: the shape is
-    outside the kernel and nothing ran (the caller runs bn_apply, then conv2d_fwd)."""
+    res*res_scale + res_shift (res_bn), is written through exactly as bn_apply would write it
+    (mask: also its ReLU bits as bn_apply_mask writes them) and y1 = conv1x1(out) exactly as
+    conv2d_fwd would compute it.  True: done; False: the shape is outside the kernel and nothing
+    ran (the caller runs bn_apply[_mask], then conv2d_fwd)."""
     rs, rh = res_bn if res_bn is not None else (None, None)
     if w.dtype not in H16:
         raise ValueError("conv2d_fwd_fold: 16-bit trunks only")
     _h16(w.dtype, y, res, out, w, y1)
     _f32(scale, shift, rs, rh)
+    if mask is not None:
+        _dev(torch.uint8, mask)
+        if mask.numel() * 8 != out.numel():
+            raise ValueError("conv2d_fwd_fold: mask needs out.numel() / 8 bytes")
     sm, s2, sn = stats if stats is not None else (None, None, None)
     M = B * H * W
     fl = 2.0 * G * M * Cout * Cin
     nb = w.element_size() * (3 * G * M * Cin + G * Cout * Cin + G * M * Cout)
     with _Prof("fwd_" + str(w.dtype)[6:], fl, nb):
         rc = lib.mauv_conv2d_fwd_fold_h16(H16[w.dtype], _p(y), _p(scale), _p(shift), _p(res),
-                                          _p(rs), _p(rh), _p(out), _p(w), _p(y1), G, B, H, W, Cin,
-                                          Cout, _p(sm), _p(s2), _p(sn), stream())
+                                          _p(rs), _p(rh), _p(out), _p(mask), _p(w), _p(y1), G, B,
+                                          H, W, Cin, Cout, _p(sm), _p(s2), _p(sn), stream())
     if rc == 1:
         if PROFILE is not None:
             PROFILE.pop()

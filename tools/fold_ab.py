@@ -1,9 +1,11 @@
 """A/B of the block-output fold (engine.FOLD; ops.conv2d_fwd_fold) on the
 bench's f16 MC-inference workload (B=256, N=100, 224 / 256 px, mc_statistics under autocast
-like the drop-in predictor): interleaved rounds in one process, HIP-event-free wall clock of
-whole batches after a warm-up chunk.
+like the drop-in predictor) or, with --train, its bf16 training step (B=64, num_mc=5,
+mc_train_step + FusedAdam): interleaved rounds in one process, wall clock of whole batches /
+steps after warm-up.
 
-    python tools/fold_ab.py [--rounds 3] [--batch 256] [--mc 100] [--sonar 256]
+    python tools/fold_ab.py [--rounds 3] [--batch 256] [--mc 100] [--sonar 256] [--only 0|1]
+    python tools/fold_ab.py --train [--rounds 3] [--steps 10]
 """
 import argparse
 import os
@@ -26,7 +28,13 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--mc", type=int, default=100)
     ap.add_argument("--sonar", type=int, default=256)
+    ap.add_argument("--only", type=int, choices=[0, 1], default=None,
+                    help="run one setting (for a rocprofv3 kernel trace of it)")
+    ap.add_argument("--train", action="store_true")
+    ap.add_argument("--steps", type=int, default=10)
     a = ap.parse_args()
+    if a.train:
+        return train_ab(a)
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model = define_models(None, 7, DEFAULT_PRIOR)["multimodal_model"].to(dev)
@@ -36,7 +44,8 @@ def main():
     res = {False: [], True: []}
     outs = {}
     for r in range(a.rounds):
-        for fold in ((False, True) if r % 2 == 0 else (True, False)):
+        order = (False, True) if r % 2 == 0 else (True, False)
+        for fold in (order if a.only is None else (bool(a.only),)):
             engine.FOLD = fold
             with torch.no_grad(), torch.autocast("cuda"):
                 mc_statistics(model, x, b, s, chunk, chunk=chunk)   # warm-up chunk
@@ -50,10 +59,53 @@ def main():
                   f"MC-samples/s ({res[fold][-1] * 1e3:.0f} ms)", flush=True)
     engine.FOLD = True
     for f in (False, True):
+        if not res[f]:
+            continue
         t = min(res[f])
         print(f"fold={int(f)} best {a.mc * a.batch / t:.0f} MC-samples/s ({t * 1e3:.0f} ms), "
               f"mc_chunk {chunk}")
-    print(f"speedup {min(res[False]) / min(res[True]):.3f}x")
+    if res[False] and res[True]:
+        print(f"speedup {min(res[False]) / min(res[True]):.3f}x")
+
+
+def train_ab(a):
+    from mauv.engine import set_precision
+    from mauv.optim import FusedAdam
+    from mauv.train import mc_train_step
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = define_models(None, 7, DEFAULT_PRIOR)["multimodal_model"].to(dev)
+    opt = FusedAdam(model.parameters(), lr=5e-5)
+    crit = torch.nn.CrossEntropyLoss()
+    B = 64
+    x, b, s, y = bench.synthetic_batch(B, 224, a.sonar, dev, 1234)
+    set_precision(model, torch.bfloat16)
+    kl_w = 2.0 ** 1 / 2.0 ** 30
+
+    def step():
+        return mc_train_step(model, (x, b, s), y, crit, opt, 5, B, kl_w)
+    res = {False: [], True: []}
+    for r in range(a.rounds):
+        order = (False, True) if r % 2 == 0 else (True, False)
+        for fold in (order if a.only is None else (bool(a.only),)):
+            engine.FOLD = fold
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                step()
+            torch.cuda.synchronize()
+            res[fold].append((time.perf_counter() - t0) / a.steps)
+            print(f"round {r} fold={int(fold)}: {B / res[fold][-1]:.1f} triplets/s "
+                  f"({res[fold][-1] * 1e3:.2f} ms/step)", flush=True)
+    engine.FOLD = True
+    for f in (False, True):
+        if res[f]:
+            t = min(res[f])
+            print(f"fold={int(f)} best {B / t:.1f} triplets/s ({t * 1e3:.2f} ms/step)")
+    if res[False] and res[True]:
+        print(f"speedup {min(res[False]) / min(res[True]):.3f}x")
 
 
 if __name__ == "__main__":
