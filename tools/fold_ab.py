@@ -32,6 +32,8 @@ def main():
                     help="run one setting (for a rocprofv3 kernel trace of it)")
     ap.add_argument("--train", action="store_true")
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--tiles", type=int, nargs=2, default=None, metavar=("A", "B"),
+                    help="--train: compare engine.FOLD_MIN_TILES A against B (fold on in both)")
     a = ap.parse_args()
     if a.train:
         return train_ab(a)
@@ -88,7 +90,10 @@ def train_ab(a):
     for r in range(a.rounds):
         order = (False, True) if r % 2 == 0 else (True, False)
         for fold in (order if a.only is None else (bool(a.only),)):
-            engine.FOLD = fold
+            if a.tiles:   # arm False = FOLD_MIN_TILES A, arm True = B
+                engine.FOLD, engine.FOLD_MIN_TILES = True, a.tiles[int(fold)]
+            else:
+                engine.FOLD = fold
             for _ in range(2):
                 step()
             torch.cuda.synchronize()
