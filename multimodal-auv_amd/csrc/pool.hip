@@ -56,6 +56,30 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const typename S::T* _
       sc = ldf8(scale + gc);
       sh = ldf8(shift + gc);
     }
+    if (scale && !idx) {
+      // no argmax wanted (inference): f(y) = round(relu(y*sc + sh)) is monotone in y for one
+      // channel (non-decreasing for sc >= 0, non-increasing for sc < 0), so the window maximum
+      // of f is f of the window's largest (sc >= 0) or smallest (sc < 0) raw value — one
+      // transform per output instead of nine.  NaN taps: f(NaN) = 0 <= every f, and
+      // fmaxf / fminf skip them.  The centre tap (2oh, 2ow) is always inside the image.
+      floatx8 hi = v[4], lo = v[4], out;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t == 4 || !((ok >> t) & 1u)) continue;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          hi[e] = fmaxf(hi[e], v[t][e]);
+          lo[e] = fminf(lo[e], v[t][e]);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float u = __builtin_fmaf(sc[e] >= 0.f ? hi[e] : lo[e], sc[e], sh[e]);
+        out[e] = u > 0.f ? u : 0.f;
+      }
+      S::st8(y + 8 * (long long)i, out);
+      continue;
+    }
     floatx8 best;
     int bi[8];
 #pragma unroll

@@ -679,6 +679,7 @@ def test_maxpool_bn_fused_matches_materialised(dt):
     y = (torch.randn(G, B, H, W, C, device=dev) * 2).to(dt)
     s, h = torch.randn(G, C, device=dev), torch.randn(G, C, device=dev)
     s[:, :8] = 0.0            # ties: whole windows of zeros after the ReLU
+    y[0, 1, 4, 5, 8:20] = float("nan")   # NaN taps: relu(NaN * s + h) stores 0 in every path
     a = torch.empty_like(y)
     ops.bn_apply(y, s, h, None, True, a, G, B * H * W, C)
     Ho, Wo = ops.out_hw(H, 3, 2, 1), ops.out_hw(W, 3, 2, 1)
