@@ -188,7 +188,9 @@ def conv2d_fwd_fold(y, scale, shift, res, res_bn, out, w, y1, G, B, H, W, Cin, C
     M = B * H * W
     fl = 2.0 * G * M * Cout * Cin
     nb = w.element_size() * (3 * G * M * Cin + G * Cout * Cin + G * M * Cout)
-    with _Prof("fwd_" + str(w.dtype)[6:], fl, nb):
+    # its own profile kind: the launch also carries the block output's BN pass (bench.py's
+    # breakdown lists it beside fwd / wgrad / dgrad)
+    with _Prof("fold_" + str(w.dtype)[6:], fl, nb):
         rc = lib.mauv_conv2d_fwd_fold_h16(H16[w.dtype], _p(y), _p(scale), _p(shift), _p(res),
                                           _p(rs), _p(rh), _p(out), _p(mask), _p(w), _p(y1), G, B,
                                           H, W, Cin, Cout, _p(sm), _p(s2), _p(sn), stream())
