@@ -32,6 +32,8 @@ def main():
                     help="run one setting (for a rocprofv3 kernel trace of it)")
     ap.add_argument("--train", action="store_true")
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--flag", default="FOLD",
+                    help="the engine switch the two arms set False / True (FOLD, BWD_PARTIALS)")
     ap.add_argument("--tiles", type=int, nargs=2, default=None, metavar=("A", "B"),
                     help="--train: compare engine.FOLD_MIN_TILES A against B (fold on in both)")
     a = ap.parse_args()
@@ -48,7 +50,7 @@ def main():
     for r in range(a.rounds):
         order = (False, True) if r % 2 == 0 else (True, False)
         for fold in (order if a.only is None else (bool(a.only),)):
-            engine.FOLD = fold
+            setattr(engine, a.flag, fold)
             with torch.no_grad(), torch.autocast("cuda"):
                 mc_statistics(model, x, b, s, chunk, chunk=chunk)   # warm-up chunk
                 torch.cuda.synchronize()
@@ -59,7 +61,7 @@ def main():
             outs[fold] = o
             print(f"round {r} fold={int(fold)}: {a.mc * a.batch / res[fold][-1]:.0f} "
                   f"MC-samples/s ({res[fold][-1] * 1e3:.0f} ms)", flush=True)
-    engine.FOLD = True
+    setattr(engine, a.flag, True)
     for f in (False, True):
         if not res[f]:
             continue
@@ -93,7 +95,7 @@ def train_ab(a):
             if a.tiles:   # arm False = FOLD_MIN_TILES A, arm True = B
                 engine.FOLD, engine.FOLD_MIN_TILES = True, a.tiles[int(fold)]
             else:
-                engine.FOLD = fold
+                setattr(engine, a.flag, fold)
             for _ in range(2):
                 step()
             torch.cuda.synchronize()
@@ -104,7 +106,7 @@ def train_ab(a):
             res[fold].append((time.perf_counter() - t0) / a.steps)
             print(f"round {r} fold={int(fold)}: {B / res[fold][-1]:.1f} triplets/s "
                   f"({res[fold][-1] * 1e3:.2f} ms/step)", flush=True)
-    engine.FOLD = True
+    setattr(engine, a.flag, True)
     for f in (False, True):
         if res[f]:
             t = min(res[f])
