@@ -228,10 +228,19 @@ def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic="fp32", suffix="",
     by = {}
     nbytes = 0.0
     roof_ms, n_hbm = 0.0, 0
+    fold = [0, 0.0, 0.0, 0.0]   # launches, flops, bytes, ms of the block-output folds
     for kind, fl, nb, nl, e0, e1 in rows:
         if (suffix and not kind.endswith(suffix)) or (not suffix and "_" in kind):
             continue
         ms = e0.elapsed_time(e1)
+        if kind.startswith("fold_"):
+            # conv1 launches that also form the previous block's output: an
+            # HBM-bound pass fused into a GEMM, reported beside the MFMA roofline, not in it
+            fold[0] += nl
+            fold[1] += fl
+            fold[2] += nb
+            fold[3] += ms
+            continue
         # this launch's own roofline time: its FLOPs at the MFMA peak or its algorithmic bytes
         # at the HBM peak, whichever is longer
         t_fl, t_hbm = fl / (peak * 1e12) * 1e3, nb / (HBM_PEAK_GBS * 1e9) * 1e3
@@ -267,6 +276,12 @@ def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic="fp32", suffix="",
         "breakdown": {k: {"launches": v[0], "gflop": round(v[1] / 1e9, 1),
                           "ms": round(v[2], 2), "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 1)}
                       for k, v in by.items()},
+        "fold": None if not fold[0] else {
+            "launches": fold[0], "gflop": round(fold[1] / 1e9, 1), "ms": round(fold[3], 2),
+            "algorithmic_gbytes": round(fold[2] / 1e9, 2),
+            "tbytes_per_s": round(fold[2] / (fold[3] * 1e-3) / 1e12, 2),
+            "note": "conv1 launches that also form the previous block output (bn3 + residual "
+                    "+ ReLU, DESIGN.md 2.20); not in achieved / frac / launches above"},
     }
 
 
@@ -461,8 +476,8 @@ def main():
             bf16["roofline"] = roofline_step(
                 step, peak=BF16_MFMA_PEAK_TF, traffic="bf16", suffix="_bfloat16",
                 kernel="16-bit convs of one step (conv_pipe16 / conv_halo16 / conv_big16: "
-                       "implicit-GEMM fwd+dgrad+wgrad, stems as one GEMM over shared im2col rows; "
-                       "'fold' = conv1 launches that also form the previous block output)")
+                       "implicit-GEMM fwd+dgrad+wgrad, stems as one GEMM over shared im2col rows); "
+                       "the conv1 launches that also form the previous block output: 'fold'")
         set_precision(model.module if world > 1 else model,
                       torch.bfloat16 if args.dtype == "bf16" else None)
 

@@ -15,6 +15,8 @@ from collections import defaultdict
 
 
 def family(name):
+    if "conv_big16<" in name and name.split("(")[0].rstrip().endswith((", 1>", ", 2>")):
+        return "conv_fold16"     # conv1 forming the previous block output (its own family)
     if "conv_gemm_f32" in name or "conv_split_f32" in name:
         return "conv_f32"        # the fp32 conv family: split kernels + stems on conv_gemm_f32
     if any(k in name for k in ("conv_gemm_h16", "conv_pipe16", "conv_halo16", "conv_big16")):
