@@ -335,14 +335,17 @@ bool conv_big16_fold_launch(int dt, const ConvArgs& a, hipStream_t st) {
   c.xrelu = 1;
   c.xcd_grid = 1;
   const bool rbn = a.rs_sc != nullptr;
-  const int BN = a.N >= 256 ? 256 : 128;
+  // 64 output channels (layer 1's conv1): 256 x 64 tiles of 4 x 2 waves (64 x 32), no half-empty
+  // B tile or MFMAs on padding columns
+  const int BN = a.N >= 256 ? 256 : (a.N > 64 ? 128 : 64);
   const dim3 grid(ceil_div(a.M, 256) * ceil_div(a.N, BN), a.G);
 #define MAUV_FOLD_LAUNCH(D, N_, R_) \
   hipLaunchKernelGGL((conv_big16<D, 256, N_, false, R_>), grid, dim3(512), 0, st, c)
 #define MAUV_FOLD_DT(D)                                                                  \
   do {                                                                                   \
     if (BN == 256) { if (rbn) MAUV_FOLD_LAUNCH(D, 256, 2); else MAUV_FOLD_LAUNCH(D, 256, 1); } \
-    else { if (rbn) MAUV_FOLD_LAUNCH(D, 128, 2); else MAUV_FOLD_LAUNCH(D, 128, 1); }          \
+    else if (BN == 128) { if (rbn) MAUV_FOLD_LAUNCH(D, 128, 2); else MAUV_FOLD_LAUNCH(D, 128, 1); } \
+    else { if (rbn) MAUV_FOLD_LAUNCH(D, 64, 2); else MAUV_FOLD_LAUNCH(D, 64, 1); }            \
   } while (0)
   if (dt == DT_BF16) MAUV_FOLD_DT(DT_BF16);
   else MAUV_FOLD_DT(DT_F16);
