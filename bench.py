@@ -285,9 +285,48 @@ def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic="fp32", suffix="",
     }
 
 
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without torchrun: N child processes of this script, rank r on
+    GPU r (torch.distributed env rendezvous on 127.0.0.1), started before this parent
+    initialises the GPU (it never does).  Rank 0 prints the JSON line; the exit status is the
+    first failing rank's (the others are then stopped)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   GROUP_RANK="0")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:     # a rank died: the others would wait on it forever
+                    q.terminate()
+        if live:
+            time.sleep(0.5)
+    for p in procs:
+        p.wait()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node, one rank each (default: WORLD_SIZE, else 1).  "
+                         "Without torchrun, N > 1 starts N rank processes itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=64, help="triplets per GPU")
@@ -328,6 +367,17 @@ def main():
                     help="torch.distributed backend for world > 1 (nccl = RCCL over xGMI; gloo "
                          "rehearses the multi-rank harness, e.g. two ranks on one GPU)")
     args = ap.parse_args()
+
+    # --gpus N is honoured or refused, never silently measured on one GPU: without a launcher
+    # (WORLD_SIZE unset) N > 1 ranks are started here, before this process touches the GPU;
+    # under torchrun the world size must equal N
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if env_world is not None and args.gpus is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (one rank per GPU)",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

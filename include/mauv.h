@@ -105,6 +105,12 @@ int mauv_set_halo3(int on);
  * forward it covers with K = R*S*Cin >= min_k, 0 none; -1 keeps; min_k <= 0 keeps the
  * threshold (512).  Returns the previous mode. */
 int mauv_set_big16(int mode, int min_k);
+/* 16-bit forwards on 128 x 128 tiles of four waves with LDS-DMA operands (conv_big16.hip,
+   conv_dma128_launch; same operands and k order as the implicit GEMM: bit-identical outputs and
+   statistics): mode 1 (default) = where measured faster, 2 = every covered forward with
+   K >= min_k, 0 = none; -1 queries.  Returns the previous mode.  Replaces nothing in the
+   reference (F.conv2d under Conv2dReparameterization, models/base_models.py:74-90). */
+int mauv_set_dma16(int mode, int min_k);
 
 /* ---- 16-bit implicit-GEMM convs (conv_gemm16.hip) -----------------------------------------
  * Same three GEMM views on v_mfma_f32_32x32x16_{bf16,f16}: dtype 0 = bf16 (BASELINE configs[2]

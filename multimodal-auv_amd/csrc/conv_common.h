@@ -162,6 +162,8 @@ bool conv_split_launch(int mode, const ConvArgs& a, int oneacc, hipStream_t st);
 bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
 // 16-bit forwards on 256-row tiles with LDS-DMA operands (conv_big16.hip); false: not covered
 bool conv_big16_launch(int dt, const ConvArgs& a, hipStream_t st);
+// the same kernel on 128 x 128 tiles of four waves; false: not covered
+bool conv_dma128_launch(int dt, const ConvArgs& a, hipStream_t st);
 // the same kernel forming the previous block's output on load (ConvArgs::rs / fout); false:
 // shape not covered (nothing launched)
 bool conv_big16_fold_launch(int dt, const ConvArgs& a, hipStream_t st);

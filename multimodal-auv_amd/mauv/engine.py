@@ -258,6 +258,11 @@ class _Runner:
         if eps is not None and fixed >= 0 and not s0 <= fixed < s0 + self.G:
             # explicit epsilons whose last draw belongs to a later forward: its rows
             ls0, leps = self.st.eps_last[(id(m), name)]
+            if not ls0 <= fixed < ls0 + leps.shape[0]:
+                raise RuntimeError(
+                    f"mauv: the reference-mode rho gradient of {name} needs the epsilon of MC "
+                    f"sample {fixed}, but this layer's last explicit draw covers samples "
+                    f"{ls0}..{ls0 + leps.shape[0] - 1} (a forward skipped this layer)")
             eps, s0 = leps[fixed - ls0:fixed - ls0 + 1], fixed
         ops.reparam_bwd(dw, splits, mu, rho, mu.grad, rho.grad, self.G, self.st.seed, s0,
                         self.st.layer_id(m, bias), Cout, Cin, RS, eps=eps,

@@ -64,14 +64,16 @@ def out_hw(H, R, stride, pad):
 # stream the kernel runs on (torch's current stream); entries: (kind, flops, bytes, launches,
 # ev0, ev1) — a strided dgrad call is stride^2 kernel launches (one per output-parity class)
 # with the ALGORITHMIC bytes of the launch (every operand read once, every output written once).
+PROFILE_INFO = None   # when a list (with PROFILE): one shape tuple per PROFILE row
 PROFILE = None
 
 
 class _Prof:
-    __slots__ = ("kind", "flops", "nbytes", "launches", "e0")
+    __slots__ = ("kind", "flops", "nbytes", "launches", "e0", "info")
 
-    def __init__(self, kind, flops, nbytes=0.0, launches=1):
+    def __init__(self, kind, flops, nbytes=0.0, launches=1, info=None):
         self.kind, self.flops, self.nbytes, self.launches = kind, flops, nbytes, launches
+        self.info = info
 
     def __enter__(self):
         if PROFILE is not None:
@@ -83,6 +85,8 @@ class _Prof:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
             PROFILE.append((self.kind, self.flops, self.nbytes, self.launches, self.e0, e1))
+            if PROFILE_INFO is not None:   # the launch's shape, parallel to PROFILE (tools/)
+                PROFILE_INFO.append(self.info)
 
 
 # ----------------------------------------------------------------------- convolutions
@@ -122,6 +126,16 @@ def set_big16(mode=None, min_k=0):
     return rc
 
 
+def set_dma16(mode=None, min_k=0):
+    """Route 16-bit forwards through the 128 x 128 LDS-DMA tiles: 1 (default) where they measured
+    faster, 2 (or True) every forward they cover with K >= min_k, 0 (or False) none; None /
+    min_k=0 keep.  Returns the previous mode (0 / 1 / 2)."""
+    m = -1 if mode is None else (2 if mode is True else (0 if mode is False else int(mode)))
+    rc = lib.mauv_set_dma16(m, int(min_k))
+    check(0 if rc >= 0 else rc, "set_dma16")
+    return rc
+
+
 def set_reparam_kernels(sample_blk=None, bwd4=None):
     """Kernel forms of reparam_sample (block form, bit-identical) and reparam_bwd (16-byte slab
     loads); None keeps a setting.  Returns the previous (sample_blk, bwd4)."""
@@ -154,14 +168,15 @@ def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_stri
         assert bias is None, "16-bit convs carry no bias (the trunks' convs are bias=False)"
         _h16(w.dtype, w, y)
         assert x.is_cuda and x.dtype == w.dtype and x.device.index == torch.cuda.current_device()
-        with _Prof("fwd_" + str(w.dtype)[6:], fl, nb):
+        with _Prof("fwd_" + str(w.dtype)[6:], fl, nb,
+                   info=(G, B, H, W, Cin, Cout, R, stride, pad, x_bn is not None)):
             check(lib.mauv_conv2d_fwd_h16(H16[w.dtype], _p(x), xs, _p(sc), _p(sh), int(rl), _p(w),
                                           _p(y), G, B, H, W, Cin, Cout, R, R, stride, pad,
                                           _p(sm), _p(s2), _p(sn), stream()), "conv2d_fwd_h16")
         return
     _f32(w, y, bias)
     assert x.is_cuda and x.dtype == torch.float32 and x.device.index == torch.cuda.current_device()
-    with _Prof("fwd", fl, nb):
+    with _Prof("fwd", fl, nb, info=(G, B, H, W, Cin, Cout, R, stride, pad, x_bn is not None)):
         check(lib.mauv_conv2d_fwd_f32(_p(x), xs, _p(sc), _p(sh), int(rl), _p(w), _p(bias), _p(y),
                                       G, B, H, W, Cin, Cout, R, R, stride, pad, _p(sm), _p(s2),
                                       _p(sn), stream()), "conv2d_fwd")
@@ -190,7 +205,7 @@ def conv2d_fwd_fold(y, scale, shift, res, res_bn, out, w, y1, G, B, H, W, Cin, C
     nb = w.element_size() * (3 * G * M * Cin + G * Cout * Cin + G * M * Cout)
     # its own profile kind: the launch also carries the block output's BN pass (bench.py's
     # breakdown lists it beside fwd / wgrad / dgrad)
-    with _Prof("fold_" + str(w.dtype)[6:], fl, nb):
+    with _Prof("fold_" + str(w.dtype)[6:], fl, nb, info=(G, B, H, W, Cin, Cout, 1, 1, 0, True)):
         rc = lib.mauv_conv2d_fwd_fold_h16(H16[w.dtype], _p(y), _p(scale), _p(shift), _p(res),
                                           _p(rs), _p(rh), _p(out), _p(mask), _p(w), _p(y1), G, B,
                                           H, W, Cin, Cout, _p(sm), _p(s2), _p(sn), stream())
@@ -236,7 +251,9 @@ def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=Non
             _dev(torch.uint8, mk)
         if bn is not None:      # + reads y (and out / mask bits) beside each dx chunk
             nb += w.element_size() * G * B * H * W * Cin * (1 + (b.get("out") is not None))
-        with _Prof("dgrad_" + str(w.dtype)[6:], fl, nb, nl):
+        with _Prof("dgrad_" + str(w.dtype)[6:], fl, nb, nl,
+                   info=(G, B, H, W, Cin, Cout, R, stride, pad,
+                         (addend is not None, bool(accumulate), addend_mask is not None))):
             check(lib.mauv_conv2d_bwd_data_bn_h16(
                 H16[w.dtype], _p(dy), _p(w), _p(dx), _p(addend), int(accumulate), G, B, H, W,
                 Cin, Cout, R, R, stride, pad, _p(addend_mask), _p(b.get("y")), _p(b.get("out")),
@@ -251,7 +268,9 @@ def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=Non
         _dev(torch.uint8, b["mask"])
     if bn is not None:
         nb += 4 * G * B * H * W * Cin * (1 + (b.get("out") is not None))
-    with _Prof("dgrad", fl, nb, nl):
+    with _Prof("dgrad", fl, nb, nl, info=(G, B, H, W, Cin, Cout, R, stride, pad,
+                                           (addend is not None, bool(accumulate),
+                                            addend_mask is not None))):
         check(lib.mauv_conv2d_bwd_data_f32(
             _p(dy), _p(w), _p(dx), _p(addend), _p(addend_mask), int(accumulate), G, B, H, W,
             Cin, Cout, R, R,
@@ -277,14 +296,15 @@ def conv2d_bwd_weight(x, dy, ws, splits, G, B, H, W, Cin, Cout, R, stride, pad,
         _h16(dy.dtype, dy)
         _f32(ws)
         assert x.is_cuda and x.dtype == dy.dtype and x.device.index == torch.cuda.current_device()
-        with _Prof("wgrad_" + str(dy.dtype)[6:], fl, nb):
+        with _Prof("wgrad_" + str(dy.dtype)[6:], fl, nb,
+                   info=(G, B, H, W, Cin, Cout, R, stride, pad, x_bn is not None)):
             check(lib.mauv_conv2d_bwd_weight_h16(H16[dy.dtype], _p(x), xs, _p(sc), _p(sh), int(rl),
                                                  _p(dy), _p(ws), splits, G, B, H, W, Cin, Cout,
                                                  R, R, stride, pad, stream()),
                   "conv2d_bwd_weight_h16")
         return
     _f32(dy, ws)
-    with _Prof("wgrad", fl, nb):
+    with _Prof("wgrad", fl, nb, info=(G, B, H, W, Cin, Cout, R, stride, pad, x_bn is not None)):
         check(lib.mauv_conv2d_bwd_weight_f32(_p(x), xs, _p(sc), _p(sh), int(rl), _p(dy), _p(ws),
                                              splits, G, B, H, W, Cin, Cout, R, R, stride, pad,
                                              stream()), "conv2d_bwd_weight")
@@ -569,12 +589,12 @@ def stem_fwd(cols, w, y, G, M, Kp, Cout, stats, alg_k):
     nb = esz * (M * Kp + G * Cout * Kp + G * M * Cout)
     if w.dtype in H16:
         _h16(w.dtype, cols, w, y)
-        with _Prof("fwd_" + str(w.dtype)[6:], fl, nb):
+        with _Prof("fwd_" + str(w.dtype)[6:], fl, nb, info=("stem", G, M, Kp, Cout)):
             check(lib.mauv_stem_fwd_h16(H16[w.dtype], _p(cols), _p(w), _p(y), G, M, Kp, Cout,
                                         _p(sm), _p(s2), _p(sn), stream()), "stem_fwd_h16")
         return
     _f32(cols, w, y)
-    with _Prof("fwd", fl, nb):
+    with _Prof("fwd", fl, nb, info=("stem", G, M, Kp, Cout)):
         check(lib.mauv_stem_fwd_f32(_p(cols), _p(w), _p(y), G, M, Kp, Cout, _p(sm), _p(s2),
                                     _p(sn), stream()), "stem_fwd_f32")
 

@@ -163,8 +163,22 @@ class FusedAdam(torch.optim.Optimizer):
                       for p in gp}
             if len(counts) != 1:
                 return None
+            # the gate takes a skipped batch's gradients back out by zeroing a clean arena, so it
+            # starts from what the arena holds: non-finite values (an ungated step skipped on
+            # them: "poisoned", kept as the reference keeps them) or nothing.  Finite leftovers
+            # (a backward outside the loop) would be lost by that zeroing: such a step takes the
+            # host-decided path, whose skip runs no backward (multimodal.py:133-135)
+            grads = [p.grad for p in gp if p.grad is not None]
+            poisoned = 0
+            if grads:
+                top = torch.stack(torch._foreach_norm(grads, float("inf")))
+                if not bool(torch.isfinite(top).all()):
+                    poisoned = 1
+                elif bool((top != 0).any()):
+                    return None
             g = torch.zeros(GATE_WORDS, dtype=torch.int32)
             g[G_STEP] = counts.pop()
+            g[G_POISONED] = poisoned
             self._gate = g.to(device)
             self._gate_dirty = False
         self._gate_params = params
@@ -189,10 +203,20 @@ class FusedAdam(torch.optim.Optimizer):
             self._remember(0, live, t, tab)
             fast = self._fast[0]
         tab = fast[5]
+        from torch.optim import optimizer as _topt
+        for hook in list(_topt._global_optimizer_pre_hooks.values()) + \
+                list(self._optimizer_step_pre_hooks.values()):
+            hook(self, (self,), {})
         check(lib.mauv_adam_step_gated(tab.data_ptr(), len(live), group["lr"], b1, b2,
                                        group["eps"], group["weight_decay"], gate.data_ptr(),
                                        ops.stream()), "adam_step_gated")
         self._gate_dirty = True
+        # what torch.optim.Optimizer.step's wrapper records: an LR scheduler stepped after this
+        # does not warn "lr_scheduler.step() before optimizer.step()"; step hooks still run
+        self._opt_called = True
+        for hook in list(self._optimizer_step_post_hooks.values()) + \
+                list(_topt._global_optimizer_post_hooks.values()):
+            hook(self, (self,), {})
 
     def _gate_step_host(self):
         """Step count held by the gate (one device read; only on a cache rebuild)."""

@@ -244,7 +244,7 @@ class _TrainEpoch:
         if "ok_loss" in r and not bool(r["ok_loss"]):
             logging.warning(f"Skipping batch {i} due to NaN/Inf loss: {r['loss']}")
             return
-        if not bool(r["stepped"]):
+        if "ok_loss" in r and not bool(r["stepped"]):   # (the host-decided path warned already)
             logging.warning("Skipping optimizer step due to NaN/Inf gradients")
         lv = r["loss"].item()
         self.total_loss += lv

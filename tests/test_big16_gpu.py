@@ -18,7 +18,9 @@ ULP = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11}
 
 
 def _run(ops, x, w, G, B, H, W, Cin, Cout, R, st, pd, x_bn, big):
-    prev = ops.set_big16(2 if big else 0, 512)
+    """big: "big16" (256-row tiles), "dma128" (128 x 128 four-wave tiles) or False (conv_pipe16)."""
+    prev = ops.set_big16(2 if big in (True, "big16") else 0, 512)
+    prevd = ops.set_dma16(2 if big == "dma128" else 0, 512)
     try:
         Ho, Wo = ops.out_hw(H, R, st, pd), ops.out_hw(W, R, st, pd)
         y = torch.full((G, B, Ho, Wo, Cout), float("nan"), device=dev, dtype=x.dtype)
@@ -31,8 +33,10 @@ def _run(ops, x, w, G, B, H, W, Cin, Cout, R, st, pd, x_bn, big):
         return y, pm, pm2, pc
     finally:
         ops.set_big16(prev)
+        ops.set_dma16(prevd)
 
 
+@pytest.mark.parametrize("kern", ["big16", "dma128"])
 @pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
 @pytest.mark.parametrize("G,B,H,W,Cin,Cout,R,st,bn", [
     (2, 3, 8, 8, 512, 256, 3, 1, "relu"),     # layer-4-like 3x3, 256-wide tiles, ragged M
@@ -41,7 +45,7 @@ def _run(ops, x, w, G, B, H, W, Cin, Cout, R, st, pd, x_bn, big):
     (1, 4, 8, 8, 512, 384, 1, 1, "norelu"),   # ragged N (384 = 256 + 128), BN without ReLU
     (3, 2, 6, 6, 512, 512, 1, 2, None),       # stride-2 1x1 (a downsample shape), G = 3
 ])
-def test_big16_bit_identical_to_implicit_gemm(G, B, H, W, Cin, Cout, R, st, bn, dt):
+def test_big16_bit_identical_to_implicit_gemm(G, B, H, W, Cin, Cout, R, st, bn, dt, kern):
     from mauv import ops
     torch.manual_seed(13)
     pd = R // 2
@@ -52,7 +56,7 @@ def test_big16_bit_identical_to_implicit_gemm(G, B, H, W, Cin, Cout, R, st, bn, 
         sc = (torch.rand(G, Cin) + 0.5).to(dev)
         sh = (torch.randn(G, Cin) * 0.2).to(dev)
         x_bn = (sc, sh, 1 if bn == "relu" else 0)
-    yb, pmb, pm2b, pcb = _run(ops, x, w, G, B, H, W, Cin, Cout, R, st, pd, x_bn, True)
+    yb, pmb, pm2b, pcb = _run(ops, x, w, G, B, H, W, Cin, Cout, R, st, pd, x_bn, kern)
     yg, pmg, pm2g, pcg = _run(ops, x, w, G, B, H, W, Cin, Cout, R, st, pd, x_bn, False)
     assert not torch.isnan(yb).any()
     assert torch.equal(yb, yg)
@@ -71,6 +75,25 @@ def test_big16_bit_identical_to_implicit_gemm(G, B, H, W, Cin, Cout, R, st, bn, 
     assert err <= 2 * ULP[dt] * ref.abs().max().item(), err
 
 
+def test_probe_fault_shape_through_every_forward_kernel():
+    """The shape at which gpurun_out/probe1.log faulted (G = 5, M = 16,384 per group as B = 64,
+    H = 256, W = 1; 1x1 1024 -> 512): the fault was torch.bmm's (hipblasLtMatmul returned
+    HIPBLAS_STATUS_INTERNAL_ERROR on this bf16 shape and its fallback raised the illegal address,
+    profiles/round5/probe_fault_trace.log).  Every 16-bit forward kernel of this
+    library at exactly that shape against fp32 torch on the CPU; no vendor GEMM is called."""
+    from mauv import ops
+    G, B, H, W, Cin, Cout = 5, 64, 256, 1, 1024, 512
+    g = torch.Generator().manual_seed(3)
+    A = (torch.rand(G, B * H * W, Cin, generator=g) * 2 - 1).to(torch.bfloat16)
+    Wt = (torch.rand(G, Cout, Cin, generator=g) * 2 - 1).to(torch.bfloat16)
+    ref = torch.stack([A[i].float() @ Wt[i].float().t() for i in range(G)])
+    x, w = A.to(dev), Wt.reshape(G, Cout, 1, 1, Cin).to(dev)
+    for kern in (False, "big16", "dma128"):
+        y, _, _, _ = _run(ops, x, w, G, B, H, W, Cin, Cout, 1, 1, 0, None, kern)
+        err = ((y.float().cpu().reshape(G, -1, Cout) - ref).abs().max() / ref.abs().max()).item()
+        assert err <= 2 * ULP[torch.bfloat16], (kern, err)
+
+
 def test_big16_switch_round_trip():
     from mauv import ops
     prev = ops.set_big16(False)
@@ -78,3 +101,6 @@ def test_big16_switch_round_trip():
     assert ops.set_big16(True) == 0
     assert ops.set_big16(prev) == 2
     assert ops.set_big16(None) == 1
+    prev = ops.set_dma16(False)
+    assert prev == 1
+    assert ops.set_dma16(True) == 0 and ops.set_dma16(prev) == 2 and ops.set_dma16(None) == 1

@@ -31,3 +31,16 @@ def test_mauv_model_multi_device_single_process_raises(monkeypatch):
     devs = [torch.device("cuda", 0), torch.device("cuda", 1)]
     with pytest.raises(RuntimeError, match="torchrun --nproc-per-node 2"):
         move_models_to_device(models, devs, use_multigpu_for_multimodal=True)
+
+
+def test_bench_refuses_gpus_unequal_world_size():
+    """Under a launcher, --gpus must equal WORLD_SIZE: bench.py exits non-zero before it
+    imports the model or touches a GPU."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr, (r.returncode, r.stderr[-500:])

@@ -250,6 +250,14 @@ def test_g6_predict_under_autocast(tmp_path):
     # the reference's scheme on the same weights / epsilon stream: oracle under f16 autocast
     from oracle import bayes_ref
     oc = copy.deepcopy(o).cuda()
+    # what autocast stores between blocks: the dtypes of a bottleneck's bn3
+    # output, the residual add and the block output, recorded by hooks on the oracle
+    from oracle.resnet_ref import Bottleneck
+    blk = next(mm for mm in oc.modules() if isinstance(mm, Bottleneck))
+    dts = {}
+    hooks = [blk.bn3.register_forward_hook(lambda mod, i, out: dts.setdefault("bn3", out.dtype)),
+             blk.register_forward_hook(lambda mod, i, out: dts.setdefault("block", out.dtype)),
+             blk.conv3.register_forward_hook(lambda mod, i, out: dts.setdefault("conv3", out.dtype))]
     bayes_ref.set_eps_source(eps_generator_source(SEED_EPS + 3))
     try:
         with torch.autocast("cuda", dtype=torch.float16):
@@ -259,6 +267,10 @@ def test_g6_predict_under_autocast(tmp_path):
                                 for b in batches]).double()
     finally:
         bayes_ref.set_eps_source(None)
+    for h in hooks:
+        h.remove()
+    print(f"\ntorch-autocast(f16) dtypes in a bottleneck: conv3 out {dts.get('conv3')}, bn3 out "
+          f"{dts.get('bn3')}, block output relu(bn3 + identity) {dts.get('block')}")
     var_gold = torch.tensor([float(r[2]) for r in G["g6_predict_csv"][1:]], dtype=torch.float64)
     var_hip = torch.tensor([float(r[2]) for r in rows[1:]], dtype=torch.float64)
     dh = (var_hip - var_gold).abs().max().item()

@@ -36,11 +36,9 @@ from tests.helpers import build_pair, EpsBridge, oracle_replay, cosines, fit_mod
 pytestmark = pytest.mark.gpu
 
 COS_MARGIN = 0.02    # whole-trunk / head gradient cosine: HIP >= autocast - COS_MARGIN
-# A whole-trunk cosine is judged where at least one 16-bit scheme resolves the float64
-# direction (cos >= RESOLVED).  Below that both are rounding noise: round 4 measured bf16 at
-# 64 px HIP 0.011-0.060 vs autocast -0.004-0.040 (MIOpen's autocast backward is itself not
-# deterministic run to run), where a 0.02 margin decides nothing and fails at random.
-RESOLVED = 0.2
+RESOLVED = 0.5       # ... judged at RESOLVED_SHAPE, where autocast's own cosine is >= this
+RESOLVED_SHAPE = (64, 64, 32, 2)   # (S_opt, S_son, B, N): placeholder until measured
+WEAK_MARGIN = 0.1    # every other shape: HIP >= autocast - WEAK_MARGIN (never skipped)
 
 
 def _cat_cos(params, truth_params, pick):
@@ -62,10 +60,12 @@ def _cuda(*ts):
     return [t.cuda() for t in ts]
 
 
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
-@pytest.mark.parametrize("S_opt,S_son,B,N", [(224, 256, 4, 2), (64, 64, 2, 3)],
-                         ids=["224-256", "64"])
-def test_train_step16_grads_vs_torch_autocast(dt, S_opt, S_son, B, N):
+def train_step16_cosines(dt, S_opt, S_son, B, N, truth_device="cpu", fp32_cpu=True):
+    """One MC training step (N samples, B triplets) of the HIP 16-bit path, of the oracle under
+    torch.autocast on the GPU and (fp32_cpu) of the fp32 CPU oracle, with the same weights and
+    epsilons; gradients against a float64 run of the oracle (on truth_device).  Returns the
+    per-tensor cosines, the whole-gradient cosines of each trunk / the head, and the logit
+    errors against float64."""
     from mauv.engine import root_state, set_precision
     from mauv.kl import get_kl_loss
     from mauv import mchead
@@ -86,25 +86,58 @@ def test_train_step16_grads_vs_torch_autocast(dt, S_opt, S_son, B, N):
         loss.backward()
         return lg, loss
 
+    # the epsilons depend on the layers only: record them on a 1-triplet 64 px forward
+    tiny = make_batches(SEED_DATA, 1, B=1, S_opt=64, S_son=64)[0]
     bridge = EpsBridge(o, m, 99)
-    with bridge, torch.no_grad():          # records the epsilons (fp32 CPU forward)
+    with bridge, torch.no_grad():
         for _ in range(N):
-            o(x, b, s)
+            o(tiny["main_image"], tiny["bathy_image"], tiny["sss_image"])
     bridge.collect()
-    o64, (lg64, _) = oracle_replay(o, bridge.store, lambda mm: loss_of(mm, "cpu", torch.float64),
-                                   dtype=torch.float64)
+    o64, (lg64, _) = oracle_replay(o, bridge.store,
+                                   lambda mm: loss_of(mm, truth_device, torch.float64),
+                                   dtype=torch.float64, device=truth_device)
     oac, (lgac, _) = oracle_replay(o, bridge.store, lambda mm: loss_of(mm, "cuda", amp=dt),
                                    device="cuda")
     root_state(m).eps_provider = bridge.provider
     logits = m.mc_forward(*_cuda(x, b, s), N)
     ce, _, _ = mchead.mc_mean_ce(logits, y.cuda())
     (ce + get_kl_loss(m) / B * 0.5).backward()
-
-    o32, _ = oracle_replay(o, bridge.store, lambda mm: loss_of(mm, "cpu"))   # fp32 CPU path
+    o32 = None
+    if fp32_cpu:
+        o32, _ = oracle_replay(o, bridge.store, lambda mm: loss_of(mm, "cpu"))
     truth = list(o64.parameters())
-    c_hip = cosines(list(m.named_parameters()), truth)
-    c_ac = cosines(list(oac.named_parameters()), truth)
-    c_32 = cosines(list(o32.named_parameters()), truth)
+    out = {"tensor": {}, "whole": {}}
+    out["tensor"]["hip"] = cosines(list(m.named_parameters()), truth)
+    out["tensor"]["autocast"] = cosines(list(oac.named_parameters()), truth)
+    if o32 is not None:
+        out["tensor"]["fp32_cpu"] = cosines(list(o32.named_parameters()), truth)
+    for gname in ("image_model_feat", "bathy_model_feat", "sss_model_feat", "head"):
+        pick = (lambda n, g=gname: n.startswith(g + ".")) if gname != "head" else \
+            (lambda n: not n.split(".")[0].endswith("_feat"))
+        out["whole"][gname] = {
+            "hip": _cat_cos(list(m.named_parameters()), truth, pick),
+            "autocast": _cat_cos(list(oac.named_parameters()), truth, pick),
+            "fp32_cpu": None if o32 is None else _cat_cos(list(o32.named_parameters()), truth,
+                                                          pick)}
+    l64 = lg64.detach().double().cpu()
+    out["dlogit_hip"] = (logits.detach().double().cpu() - l64).abs().max().item()
+    out["dlogit_autocast"] = (lgac.detach().double().cpu() - l64).abs().max().item()
+    return out
+
+
+def _print_whole(tag, r):
+    for gname, c in r["whole"].items():
+        f = "" if c["fp32_cpu"] is None else f" (fp32 CPU {c['fp32_cpu']:.5f})"
+        print(f"  {tag} {gname:17s} whole-gradient cos vs fp64: HIP {c['hip']:.5f} "
+              f"autocast {c['autocast']:.5f}{f}")
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("S_opt,S_son,B,N", [(224, 256, 4, 2), (64, 64, 2, 3)],
+                         ids=["224-256", "64"])
+def test_train_step16_grads_vs_torch_autocast(dt, S_opt, S_son, B, N):
+    r = train_step16_cosines(dt, S_opt, S_son, B, N)
+    c_hip, c_ac, c_32 = r["tensor"]["hip"], r["tensor"]["autocast"], r["tensor"]["fp32_cpu"]
     assert set(c_hip) == set(c_ac) and len(c_hip) > 600, len(c_hip)
     names = sorted(c_hip)
     h = np.array([c_hip[n] for n in names])
@@ -120,24 +153,33 @@ def test_train_step16_grads_vs_torch_autocast(dt, S_opt, S_son, B, N):
     for sel in (np.ones_like(trunk), trunk):
         (mh, ph), (ma, pa) = _q(h[sel]), _q(a[sel])
         assert mh >= ma - 0.01 and ph >= pa - 0.02, (mh, ma, ph, pa)
-    groups = {"image_model_feat": None, "bathy_model_feat": None, "sss_model_feat": None,
-              "head": None}
-    for gname in groups:
-        pick = (lambda n, g=gname: n.startswith(g + ".")) if gname != "head" else \
-            (lambda n: not n.split(".")[0].endswith("_feat"))
-        ch = _cat_cos(list(m.named_parameters()), truth, pick)
-        ca = _cat_cos(list(oac.named_parameters()), truth, pick)
-        c3 = _cat_cos(list(o32.named_parameters()), truth, pick)
-        judged = max(ch, ca) >= RESOLVED
-        print(f"  {gname:17s} whole-gradient cos vs fp64: HIP {ch:.5f} autocast {ca:.5f} "
-              f"(fp32 CPU {c3:.5f})" + ("" if judged else "  [both unresolved: not judged]"))
-        if judged:
-            assert ch >= ca - COS_MARGIN, (gname, ch, ca)
-    # logits: both schemes against the float64 truth
-    dh = (logits.detach().double().cpu() - lg64.detach()).abs().max().item()
-    da = (lgac.detach().double().cpu() - lg64.detach()).abs().max().item()
-    print(f"  max |dlogit| vs fp64: HIP {dh:.3e}  torch-autocast {da:.3e}")
-    assert dh <= max(2 * da, 1e-3)
+    _print_whole(tag, r)
+    for gname, c in r["whole"].items():
+        # at these batches both 16-bit schemes sit near rounding noise for bf16 (cos ~0.1, the
+        # BN backward over B = 2-4 per sample amplifies it): a loose bar that still catches a
+        # broken trunk; the tight bar is test_train_step16_whole_trunk_resolved's
+        assert c["hip"] >= c["autocast"] - WEAK_MARGIN, (gname, c)
+    print(f"  max |dlogit| vs fp64: HIP {r['dlogit_hip']:.3e}  torch-autocast "
+          f"{r['dlogit_autocast']:.3e}")
+    assert r["dlogit_hip"] <= max(2 * r["dlogit_autocast"], 1e-3)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+def test_train_step16_whole_trunk_resolved(dt):
+    """Whole-trunk gradient cosines at a batch where torch-autocast itself resolves the float64
+    direction (its cosine >= RESOLVED on every trunk, asserted: the bar is not vacuous); HIP
+    >= autocast - COS_MARGIN there.  float64 truth on the GPU."""
+    S_opt, S_son, B, N = RESOLVED_SHAPE
+    r = train_step16_cosines(dt, S_opt, S_son, B, N, truth_device="cuda", fp32_cpu=False)
+    tag = f"{str(dt)[6:]} {S_opt}/{S_son} B={B} N={N}"
+    print()
+    _print_whole(tag, r)
+    print(f"  max |dlogit| vs fp64: HIP {r['dlogit_hip']:.3e}  torch-autocast "
+          f"{r['dlogit_autocast']:.3e}")
+    for gname, c in r["whole"].items():
+        assert c["autocast"] >= RESOLVED, (gname, c)
+        assert c["hip"] >= c["autocast"] - COS_MARGIN, (gname, c)
+    assert r["dlogit_hip"] <= max(2 * r["dlogit_autocast"], 1e-3)
 
 
 @pytest.mark.parametrize("S_opt,S_son,B,N", [(64, 64, 64, 8), (128, 128, 64, 8),

@@ -182,6 +182,72 @@ def test_nan_loss_batch_leaves_clean_arena_and_counts():
     assert int(opt._gate[4].item()) == 2                   # two steps taken
 
 
+def test_gate_starts_from_the_arena_state():
+    """the gate takes a skipped batch's gradients back out by zeroing a CLEAN arena.
+    (a) finite gradients left by a backward outside the loop: the steps take the host-decided
+    path (a NaN-loss batch runs no backward and the leftovers stay, multimodal.py:133-135; the
+    next good batch steps on their sum) until a zero_grad leaves the arena clean, then the gated
+    path resumes; (b) an arena poisoned by an ungated skip: the gate starts poisoned, so a NaN-loss
+    batch keeps the non-finite gradients instead of zeroing them."""
+    import mauv.train as T
+    from mauv.optim import FusedAdam, G_POISONED
+    from mauv.engine import root_state
+    crit = torch.nn.CrossEntropyLoss()
+    m = _model(2)
+    opt = FusedAdam(m.parameters(), lr=1e-4)
+    x, b, s, y = _batch(60, "ok")
+    T.mc_loss(m, (x, b, s), y, crit, 2, 2, 1e-3)[0].backward()   # outside the loop
+    flat = root_state(m).arena.flat
+    left = flat.clone()
+    assert (left != 0).any()
+    r = T.mc_train_step(m, _batch(61, "nan_loss")[:3], y, crit, opt, 2, 2, 1e-3)
+    assert r is None and torch.equal(flat, left)            # skipped, leftovers kept
+    r = T.mc_train_step(m, _batch(62, "ok")[:3], y, crit, opt, 2, 2, 1e-3)
+    assert "ok_loss" not in r and r["stepped"]               # host path, stepped, zero_grad
+    assert all(p.grad is None or not p.grad.any() for p in m.parameters())
+    r = T.mc_train_step(m, _batch(63, "ok")[:3], y, crit, opt, 2, 2, 1e-3)
+    assert "ok_loss" in r                                    # clean arena: gated again
+    # (b) poisoned by an ungated skip
+    m2 = _model(3)
+    opt2 = FusedAdam(m2.parameters(), lr=1e-4)
+    inject = _InjectNaNGrad()
+    real_gate = T._step_gate
+    try:
+        T._step_gate = lambda *a: None
+        inject.on = True
+        r = T.mc_train_step(m2, _batch(64, "ok")[:3], y, crit, opt2, 2, 2, 1e-3)
+        inject.on = False
+        assert r is not None and not r["stepped"]
+    finally:
+        T._step_gate = real_gate
+        inject.close()
+    assert not torch.isfinite(root_state(m2).arena.flat).all()
+    r = T.mc_train_step(m2, _batch(65, "nan_loss")[:3], y, crit, opt2, 2, 2, 1e-3)
+    assert "ok_loss" in r and not bool(r["ok_loss"])
+    assert int(opt2._gate[G_POISONED].item()) == 1
+    assert not torch.isfinite(root_state(m2).arena.flat).all()   # kept, not zeroed
+
+
+def test_gated_step_runs_optimizer_hooks_and_marks_the_step():
+    """the gated step records torch's step flag (no scheduler warning) and runs the
+    optimizer's step hooks like Optimizer.step."""
+    import warnings
+    from mauv.optim import FusedAdam
+    from mauv.train import mc_train_step
+    m = _model(4)
+    opt = FusedAdam(m.parameters(), lr=1e-4)
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5)
+    calls = []
+    opt.register_step_pre_hook(lambda o, a, k: calls.append("pre"))
+    opt.register_step_post_hook(lambda o, a, k: calls.append("post"))
+    x, b, s, y = _batch(70, "ok")
+    r = mc_train_step(m, (x, b, s), y, torch.nn.CrossEntropyLoss(), opt, 2, 2, 1e-3)
+    assert "ok_loss" in r and calls == ["pre", "post"]
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        sched.step()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

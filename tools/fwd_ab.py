@@ -1,7 +1,8 @@
-"""A/B of the 16-bit forward kernels over every conv of the three trunks (the bench's training
-slice G=5, B=64 by default; --G 50 --B 256 ~ an f16 inference chunk): conv_big16 (256-row
-LDS-DMA tiles) against the implicit GEMM (conv_pipe16), interleaved rounds in one process, with
-the pending BN on load where the engine has it (conv2, conv3) and the statistics epilogue.
+"""A/B/C of the 16-bit forward kernels over every conv of the three trunks (the bench's training
+slice G=5, B=64 by default; --G 50 --B 256 ~ an f16 inference chunk): conv_big16's 256-row
+LDS-DMA tiles ("big16") and its 128 x 128 four-wave tiles ("dma128") against the implicit GEMM
+(conv_pipe16), interleaved rounds in one process, with the pending BN on load where the engine
+has it (conv2, conv3) and the statistics epilogue.
 
     python tools/fwd_ab.py [--dtype bf16|f16] [--G 5] [--B 64] [--min-k 512] [--rounds 3]
 """
@@ -36,7 +37,8 @@ def main():
             key = (Cin, Cout, R, st, pd, H, name.endswith(("c2", "c3")))
             shapes.setdefault(key, []).append(f"{trunk}:{name}")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    res = {k: {True: [], False: []} for k in shapes}
+    ARMS = ("pipe16", "big16", "dma128")
+    res = {k: {arm: [] for arm in ARMS} for k in shapes}
     for rnd in range(a.rounds):
         for key in shapes:
             Cin, Cout, R, st, pd, H, xb = key
@@ -49,8 +51,10 @@ def main():
                                                                (G, nblk)))
             x_bn = (torch.rand(G, Cin, device=dev) + 0.5, torch.randn(G, Cin, device=dev) * 0.1,
                     1) if xb else None
-            for big in ((True, False) if rnd % 2 == 0 else (False, True)):
-                prev = ops.set_big16(2 if big else 0, a.min_k)
+            order = ARMS[rnd % 3:] + ARMS[:rnd % 3]
+            for arm in order:
+                prev = ops.set_big16(2 if arm == "big16" else 0, a.min_k)
+                prevd = ops.set_dma16(2 if arm == "dma128" else 0, a.min_k)
                 try:
                     fn = lambda: ops.conv2d_fwd(x, w, y, G, B, H, H, Cin, Cout, R, st, pd,
                                                 x_bn=x_bn, stats=stats)
@@ -60,25 +64,25 @@ def main():
                         fn()
                     e1.record()
                     torch.cuda.synchronize()
-                    res[key][big].append(e0.elapsed_time(e1) / a.reps)
+                    res[key][arm].append(e0.elapsed_time(e1) / a.reps)
                 finally:
                     ops.set_big16(prev)
+                    ops.set_dma16(prevd)
             del x, w, y
-    tot = {True: 0.0, False: 0.0}
-    print(f"{'Cin,Cout,R,s,H,xbn':28s} {'n':>3s} {'pipe16 ms':>10s} {'big16 ms':>10s} {'ratio':>6s} "
-          f"{'TF/s pipe':>9s} {'TF/s big':>9s}  layers")
-    for key, v in sorted(shapes.items(), key=lambda kv: -min(res[kv[0]][False])):
+    tot = {arm: 0.0 for arm in ARMS}
+    print(f"{'Cin,Cout,R,s,H,xbn':28s} {'n':>3s} " + " ".join(f"{x + ' ms':>11s}" for x in ARMS) +
+          " " + " ".join(f"{'TF/s ' + x:>12s}" for x in ARMS) + "  layers")
+    for key, v in sorted(shapes.items(), key=lambda kv: -min(res[kv[0]]["pipe16"])):
         Cin, Cout, R, st, pd, H, xb = key
         Ho = ops.out_hw(H, R, st, pd)
         fl = 2.0 * G * B * Ho * Ho * Cout * R * R * Cin
-        tb, tp = min(res[key][True]), min(res[key][False])
-        tot[True] += tb * len(v)
-        tot[False] += tp * len(v)
-        print(f"{str((Cin, Cout, R, st, H, int(xb))):28s} {len(v):3d} {tp:10.3f} {tb:10.3f} "
-              f"{tb / tp:6.3f} {fl / tp / 1e9:9.0f} {fl / tb / 1e9:9.0f}  {' '.join(v[:4])}")
-    print(f"TOTAL (x occurrences): pipe16 {tot[False]:.2f} ms, big16 {tot[True]:.2f} ms, "
-          f"ratio {tot[True] / tot[False]:.3f}")
-
+        t = {arm: min(res[key][arm]) for arm in ARMS}
+        for arm in ARMS:
+            tot[arm] += t[arm] * len(v)
+        print(f"{str((Cin, Cout, R, st, H, int(xb))):28s} {len(v):3d} " +
+              " ".join(f"{t[x]:11.3f}" for x in ARMS) + " " +
+              " ".join(f"{fl / t[x] / 1e9:12.0f}" for x in ARMS) + f"  {' '.join(v[:4])}")
+    print("TOTAL (x occurrences): " + ", ".join(f"{x} {tot[x]:.2f} ms" for x in ARMS))
 
 if __name__ == "__main__":
     main()

@@ -33,6 +33,7 @@ SHAPES = [
     ("square 16k x 1k x 1k", 16384, 1024, 1024),
 ]
 G = 5
+TRACE = os.environ.get("PROBE_TRACE") == "1"
 VARIANTS = {0: "glds 256x256", 1: "glds 256x128", 2: "glds 256x128 x3", 3: "glds 128x128"}
 XVARIANTS = {4: "glds 256x128 +BN", 5: "glds 256x256 +BN"}
 
@@ -86,8 +87,13 @@ def run_shape(name, M, N, K, xbn, vs, dt, stream):
     errs = {}
     for k, f in fns.items():
         C.zero_()
+        torch.cuda.synchronize()
+        if TRACE:   # which launch faults (gpurun_out/probe1.log's shape 3): one line per launch
+            print(f"  [trace] {name} {'XBN ' if xbn else ''}{k}: launch", flush=True)
         out = f()
         torch.cuda.synchronize()
+        if TRACE:
+            print(f"  [trace] {name} {k}: ok", flush=True)
         if isinstance(out, int) and out != 0:
             errs[k] = f"rc {out}"
             continue
