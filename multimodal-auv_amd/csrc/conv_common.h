@@ -181,6 +181,92 @@ __device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int
 }
 
 
+// fp32 data-gradient epilogue with a residual addend (optionally counted under ReLU-mask bits)
+// and / or accumulation into dx: the accumulators are parked in LDS ([rows][BN + 4] floats, the
+// whole tile when it fits SCRATCH bytes, else one wave row band per pass) and every thread then
+// moves 16-byte row chunks: the addend, its 4 mask bits and the previous dx are fetched into
+// registers BEFORE the accumulators are parked (their HBM latency hides behind the LDS round
+// trip), added in fp32 and stored as float4.  The direct per-element form (conv_epilogue: one
+// 4-byte addend load behind each 1-byte mask load, per element) ran the bench's masked-addend
+// data gradients at 1.6-2.3 TB/s.  Requires N % 4 == 0 (host-checked Cin % 4).
+template <int BM, int BN, int MI, int NI, int WGM, int WGN, int SCRATCH>
+__device__ __forceinline__ void dgrad_epilogue_f32(const ConvArgs& a, floatx16 (&acc)[MI][NI],
+                                                   float* stile, int m0, int n0, int g) {
+  constexpr int NT = 64 * WGM * WGN, WM = BM / WGM, WN = BN / WGN;
+  constexpr int SLD = BN + 4, CPR = BN / 4;
+  constexpr int PASSES = BM * SLD * 4 <= SCRATCH ? 1
+                         : ((WGM % 2 == 0 && (BM / 2) * SLD * 4 <= SCRATCH) ? 2 : WGM);
+  static_assert((BM / PASSES) * SLD * 4 <= SCRATCH && WGM % PASSES == 0, "dgrad epilogue scratch");
+  constexpr int PR = BM / PASSES, NCH = PR * CPR, CPT = (NCH + NT - 1) / NT;
+  constexpr int WPP = WGM / PASSES;  // wave rows per pass
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
+  float* outp = a.out;
+  auto chunk = [&](int pass, int c, long long& o) -> bool {
+    const int rl = c / CPR, cc = c - rl * CPR;
+    const int row = m0 + pass * PR + rl, col = n0 + 4 * cc;
+    if (c >= NCH || row >= a.M || col >= a.N) return false;
+    long long orow = row;
+    if (a.stride != 1) {  // class-local row -> input pixel
+      const int HW = a.Hc * a.Wc, b = row / HW, rem = row - b * HW;
+      const int i = rem / a.Wc, jj = rem - i * a.Wc;
+      orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
+    }
+    o = (long long)g * a.out_sg + orow * a.N + col;
+    return true;
+  };
+  // two chunks in flight (a deeper prefetch spills the 128-VGPR budget of the eight-wave tiles)
+  constexpr int PFD = 2;
+  floatx4 pa[PFD], pd[PFD];
+  unsigned pm[PFD];
+  auto prefetch = [&](int pass, int k) {
+    const int q = k % PFD;
+    long long o = 0;
+    pa[q] = pd[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+    pm[q] = 0xfu;
+    if (k < CPT && chunk(pass, tid + k * NT, o)) {
+      if (a.addend) {
+        pa[q] = *(const floatx4*)(a.addend + o);
+        if (a.add_mask) pm[q] = (unsigned)(a.add_mask[o >> 3] >> (o & 7));
+      }
+      if (a.accumulate) pd[q] = *(const floatx4*)(outp + o);
+    }
+  };
+#pragma unroll
+  for (int pass = 0; pass < PASSES; ++pass) {
+#pragma unroll
+    for (int k = 0; k < PFD; ++k) prefetch(pass, k);
+    if (wm / WPP == pass) {
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            stile[(wm * WM - pass * PR + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SLD +
+                  wn * WN + ni * 32 + li] = acc[mi][ni][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int c = tid + k * NT, q = k % PFD;
+      long long o;
+      if (chunk(pass, c, o)) {
+        const int rl = c / CPR, cc = c - rl * CPR;
+        floatx4 v = *(const floatx4*)(stile + rl * SLD + 4 * cc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if ((pm[q] >> e) & 1u) v[e] += pa[q][e];
+          v[e] += pd[q][e];
+        }
+        *(floatx4*)(outp + o) = v;
+      }
+      prefetch(pass, k + PFD);   // (slot q is this chunk's: free)
+    }
+    if (pass + 1 < PASSES) __syncthreads();
+  }
+}
+
 // Epilogue of one BM x BN block tile: acc[mi][ni] holds the fp32 32x32 accumulator tiles of
 // this wave (the C/D layout of both v_mfma_f32_32x32x2_f32 and v_mfma_f32_32x32x16_bf16:
 // lane l = column l&31, register r = row (r&3) + 8(r>>2) + 4(l>>5)).

@@ -398,6 +398,12 @@ void conv_split_f32(const ConvArgs a) {
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) acc[mi][ni] += acl[mi][ni];
   }
+  if constexpr (MODE == DGRAD && !BP) {
+    if (a.addend || a.accumulate) {
+      dgrad_epilogue_f32<BM, BN, MI, NI, WGM, WGN, NBUF * STG * 2>(a, acc, (float*)smem, m0, n0, g);
+      return;
+    }
+  }
   conv_epilogue<MODE, BM, BN, MI, NI, WGM, WGN, BP>(a, acc, (float*)smem, tid, m0, n0, g, sp);
 }
 

@@ -46,12 +46,6 @@ RES_MASK = True
 # (bit-identical) and FOLD_MIN_TILES 0 to fold their small shapes.
 FOLD = True
 FOLD_MIN_TILES = 512
-# 16-bit training option: the data gradients of conv3 /
-# conv2 write the backward partial sums of bn2 / bn1 in their epilogue, so those BNs' partial
-# passes over (y, dout) disappear.  Measured wall-neutral on the bf16 step (the removed passes
-# overlapped the other trunks' convs; the data gradients grow and lose their short-K form), so
-# it is off; tests compare both.
-BWD_PARTIALS = False
 _STREAMS = {}
 
 
@@ -466,27 +460,8 @@ class TrunkRunner(_Runner):
         tiles = -(-B * H * W // 256) * self.G * -(-N // (256 if N >= 256 else 128))
         return tiles >= FOLD_MIN_TILES
 
-    def _dgrad_partials(self, rec, s):
-        """16-bit: the data gradient of rec's conv writes the backward partial sums of BN s
-        (whose output gradient it is; a lazily applied bn1 / bn2: ReLU from y*scale + shift) in its
-        epilogue — not for the 3x3 / stride-1 64 -> 64 convs, whose data gradient runs on the
-        halo kernel without that epilogue."""
-        if not BWD_PARTIALS or self.dt == torch.float32 or s.mask is not None or \
-                s.out is not None:
-            return None
-        conv, x, xs, x_bn, w, B, H, W = rec
-        G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, _first(conv.kernel_size)
-        st, pd = _first(conv.stride), _first(conv.padding)
-        if Cout % 64 or (k == 3 and st == 1 and Cin == 64 and Cout == 64):
-            return None
-        nblk = ops.dgrad_stat_blocks(G, B, H, W, Cin, Cout, k, st, pd)
-        buf = torch.empty(2, G, nblk, Cin, device=s.y.device)
-        st_ = s.stats
-        return dict(y=s.y, out=None, mask=None, scale=st_[2], shift=st_[3], mean=st_[0],
-                    invstd=st_[1], relu=int(s.relu), p1=buf[0], p2=buf[1], nblk=nblk)
-
     def _conv_bwd(self, rec, dy, need_dx=True, addend=None, dx=None, accumulate=False,
-                  addend_mask=None, bn=None):
+                  addend_mask=None):
         """Weight gradient (+ reparameterisation backward) and data gradient (+ addend, counted
         only under addend_mask's ReLU bits when given)."""
         conv, x, xs, x_bn, w, B, H, W = rec
@@ -506,7 +481,7 @@ class TrunkRunner(_Runner):
         if dx is None:
             dx = torch.empty(G, B, H, W, Cin, device=dy.device, dtype=self.dt)
         ops.conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, k, st, pd, addend=addend,
-                            accumulate=accumulate, addend_mask=addend_mask, bn=bn)
+                            accumulate=accumulate, addend_mask=addend_mask)
         return dx
 
     def _stem(self, conv, x, B, H, W):
@@ -587,10 +562,9 @@ class TrunkRunner(_Runner):
         self.last_lazy = (scale, shift, int(relu))  # for a consumer applying it on load
         return out, rec
 
-    def _bn_bwd(self, rec, dout, want_dres=False, mask=None, pre=None):
+    def _bn_bwd(self, rec, dout, want_dres=False, mask=None):
         """mask: ReLU-mask bits applied to dout (a downsample BN fed the block output's
-        dres = dout * mask without that tensor); pre: the partial sums dout's data gradient
-        wrote (_dgrad_partials), so the partial pass is skipped."""
+        dres = dout * mask without that tensor)."""
         if not rec.batch_stats:
             raise NotImplementedError("mauv: backward through eval-mode BN is not on the path "
                                       "(the reference trains and predicts in .train())")
@@ -601,10 +575,7 @@ class TrunkRunner(_Runner):
         dg = bn.weight.grad if bn.weight.requires_grad else None
         db = bn.bias.grad if bn.bias.requires_grad else None
         s = rec.stats
-        if pre is not None:
-            ops.bn_bwd_ex(rec.y, None, None, dout, rec.relu, s[0], s[1], s[2], s[3], G, M, C, ws,
-                          dy, dres, dg, db, pre=(pre["p1"], pre["p2"], pre["nblk"]))
-        elif mask is not None:
+        if mask is not None:
             ops.bn_bwd_ex(rec.y, None, mask, dout, 1, s[0], s[1], s[2], s[3], G, M, C, ws, dy,
                           dres, dg, db)
         elif rec.mask is not None:
@@ -724,16 +695,13 @@ class TrunkRunner(_Runner):
             if rmask is not None:
                 dres = da
             del da, s3
-            pre2 = self._dgrad_partials(r3, s2)
-            da2 = self._conv_bwd(r3, dy3, bn=pre2)
+            da2 = self._conv_bwd(r3, dy3)
             del dy3, r3
-            dy2, _ = self._bn_bwd(s2, da2, pre=pre2)
-            del da2, s2, pre2
-            pre1 = self._dgrad_partials(r2, s1)
-            da1 = self._conv_bwd(r2, dy2, bn=pre1)
+            dy2, _ = self._bn_bwd(s2, da2)
+            del da2, s2
+            da1 = self._conv_bwd(r2, dy2)
             del dy2, r2
-            dy1, _ = self._bn_bwd(s1, da1, pre=pre1)
-            del pre1
+            dy1, _ = self._bn_bwd(s1, da1)
             del da1, s1
             if rd is not None:
                 dyd, _ = self._bn_bwd(sd, dres, mask=rmask)

@@ -788,3 +788,51 @@ def test_reparam_sample_block_form_bit_identical(dt, G, Cout, Cin, R, cin_pad, e
         assert (outs[1][0][..., Cin:].float() == 7.0).all()
     if not explicit:   # the device counter shifts the sample index by 3
         assert not torch.equal(outs[1][0], outs[1][1])
+
+
+@pytest.mark.parametrize("Cin,Cout,R,st,H,form", [
+    (256, 64, 1, 1, 16, "masked"),      # K = 64: the short-K (SEQ) kernel, half-tile LDS passes
+    (256, 512, 1, 1, 15, "masked"),     # pipelined 128 x 128 tiles, ragged M
+    (128, 128, 3, 1, 9, "addend"),      # 3x3, addend without mask bits
+    (256, 512, 1, 2, 16, "accumulate"), # stride-2 downsample class accumulating into dx
+    (192, 256, 3, 2, 11, "both"),       # strided 3x3, ragged classes, addend + accumulate
+    (96, 64, 1, 1, 7, "masked"),        # 64-wide tiles (64 x 64 kernel)
+])
+def test_dgrad_f32_staged_epilogue(Cin, Cout, R, st, H, form):
+    """fp32 data gradients with a residual addend (under ReLU-mask bits or not) and / or
+    accumulation into dx: the LDS-staged 16-byte epilogue (conv_common.h dgrad_epilogue_f32)
+    against float64 — the addend counted exactly where the mask bit is set, classes without taps
+    leaving dx (+ addend) as it was."""
+    from mauv import ops
+    G, B = 2, 2
+    pd = R // 2
+    torch.manual_seed(8)
+    Ho = ops.out_hw(H, R, st, pd)
+    dy = torch.randn(G, B, Ho, Ho, Cout)
+    w = torch.randn(G, Cout, R, R, Cin) / (Cout * R * R) ** 0.5
+    ad = torch.randn(G, B, H, H, Cin) if form in ("masked", "addend", "both") else None
+    mask = None
+    keep = torch.ones(G, B, H, H, Cin, dtype=torch.bool)
+    if form == "masked":
+        keep = torch.rand(G, B, H, H, Cin) > 0.4
+        bits = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)
+        mask = bits.sum(1).to(torch.uint8).to(dev)
+    dx0 = torch.randn(G, B, H, H, Cin)
+    acc = form in ("accumulate", "both")
+    dx = dx0.clone().to(dev) if acc else torch.full((G, B, H, H, Cin), float("nan"), device=dev)
+    ops.conv2d_bwd_data(dy.to(dev), w.to(dev), dx, G, B, H, H, Cin, Cout, R, st, pd,
+                        addend=None if ad is None else ad.to(dev), accumulate=acc,
+                        addend_mask=mask)
+    ref = []
+    for g in range(G):
+        xg = torch.zeros(B, Cin, H, H, dtype=torch.float64, requires_grad=True)
+        F.conv2d(xg, w[g].permute(0, 3, 1, 2).double(), stride=st, padding=pd).backward(
+            dy[g].permute(0, 3, 1, 2).double())
+        ref.append(xg.grad.permute(0, 2, 3, 1))
+    ref = torch.stack(ref)
+    if ad is not None:
+        ref = ref + torch.where(keep, ad.double(), torch.zeros((), dtype=torch.float64))
+    if acc:
+        ref = ref + dx0.double()
+    assert not torch.isnan(dx).any()
+    close(dx, ref, rtol=1e-5, atol=1e-5)

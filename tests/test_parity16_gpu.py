@@ -60,7 +60,7 @@ def _cuda(*ts):
     return [t.cuda() for t in ts]
 
 
-def train_step16_cosines(dt, S_opt, S_son, B, N, truth_device="cpu", fp32_cpu=True):
+def train_step16_cosines(dt, S_opt, S_son, B, N, truth_device="cpu", fp32_cpu=True, fit_steps=0):
     """One MC training step (N samples, B triplets) of the HIP 16-bit path, of the oracle under
     torch.autocast on the GPU and (fp32_cpu) of the fp32 CPU oracle, with the same weights and
     epsilons; gradients against a float64 run of the oracle (on truth_device).  Returns the
@@ -70,9 +70,12 @@ def train_step16_cosines(dt, S_opt, S_son, B, N, truth_device="cpu", fp32_cpu=Tr
     from mauv.kl import get_kl_loss
     from mauv import mchead
     o, m = build_pair()
-    set_precision(m, dt)
     batch = make_batches(SEED_DATA, 1, B=B, S_opt=S_opt, S_son=S_son)[0]
     x, b, s, y = batch["main_image"], batch["bathy_image"], batch["sss_image"], batch["label"]
+    if fit_steps:   # a model trained a few (fp32) steps on this batch, in both implementations
+        fit_model(m, *_cuda(x, b, s), y.cuda(), steps=fit_steps)
+        o.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    set_precision(m, dt)
 
     def loss_of(model, dev, dtp=torch.float32, amp=None):
         xs = [t.to(dev, dtp) for t in (x, b, s)]

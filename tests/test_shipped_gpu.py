@@ -91,7 +91,7 @@ def _fp32_checks(m, o32, res, tag):
     assert d <= 2e-4 * max(1.0, lo.abs().max().item())
     assert abs(ch.item() - co.item()) <= 1e-4 * abs(co.item())
     if o32 is not None:
-        mp, op = list(m.named_parameters()), list(o32.named_parameters())
+        mp, op = list(m.named_parameters()), list(o32.parameters())
         for tr in TRUNKS + ("head",):
             pick = (lambda n, g=tr: n.startswith(g + ".")) if tr != "head" else \
                 (lambda n: not n.split(".")[0].endswith("_feat"))

@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--train", action="store_true")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--flag", default="FOLD",
-                    help="the engine switch the two arms set False / True (FOLD, BWD_PARTIALS)")
+                    help="the engine switch the two arms set False / True (e.g. FOLD)")
     ap.add_argument("--tiles", type=int, nargs=2, default=None, metavar=("A", "B"),
                     help="--train: compare engine.FOLD_MIN_TILES A against B (fold on in both)")
     a = ap.parse_args()

@@ -19,6 +19,7 @@ from tests.test_parity16_gpu import train_step16_cosines  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
+    ap.add_argument("--fit", type=int, default=0, help="train the model this many fp32 steps first")
     ap.add_argument("shapes", nargs="+")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
@@ -27,10 +28,11 @@ def main():
     for sh in a.shapes:
         S_opt, S_son, B, N = (int(v) for v in sh.split(","))
         t0 = time.time()
-        r = train_step16_cosines(dt, S_opt, S_son, B, N, truth_device="cuda", fp32_cpu=False)
+        r = train_step16_cosines(dt, S_opt, S_son, B, N, truth_device="cuda", fp32_cpu=False,
+                                 fit_steps=a.fit)
         cells = "  ".join(f"{g[:5]} HIP {c['hip']:.3f} ac {c['autocast']:.3f}"
                           for g, c in r["whole"].items())
-        print(f"{a.dtype} {S_opt}/{S_son} B={B} N={N} ({time.time() - t0:.0f} s): {cells}  "
+        print(f"{a.dtype} fit={a.fit} {S_opt}/{S_son} B={B} N={N} ({time.time() - t0:.0f} s): {cells}  "
               f"dlogit HIP {r['dlogit_hip']:.2e} ac {r['dlogit_autocast']:.2e}", flush=True)
         torch.cuda.empty_cache()
 
