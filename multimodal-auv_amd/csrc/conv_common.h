@@ -181,6 +181,91 @@ __device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int
 }
 
 
+// FWD BatchNorm statistics partials of the block tile from the fp32 accumulators (+ bias): the
+// statistics half of conv_epilogue (same operations, same partial layout), for the staged
+// store of staged_epilogue_f32.  Ends with a barrier (the LDS is free again).
+template <int BM, int BN, int MI, int NI, int WGM, int WGN>
+__device__ __forceinline__ void fwd_stats_f32(const ConvArgs& a, floatx16 (&acc)[MI][NI],
+                                              float* red, int tid, int m0, int n0, int g) {
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int SR = BM > 128 ? 128 : BM, SUB = BM / SR, WPS = WGM / SUB;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
+  const int sub = wm / WPS;
+  float s1[NI], s2[NI];
+  const int nvalid = min(SR, a.M - (m0 + sub * SR));
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    s1[ni] = 0.f;
+    s2[ni] = 0.f;
+    const int col = n0 + wn * WN + ni * 32 + li;
+    if (col >= a.N) continue;
+    const float bias = a.bias ? a.bias[(long long)g * a.bias_sg + col] : 0.f;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < a.M) s1[ni] += acc[mi][ni][r] + bias;
+      }
+  }
+  const int tcol = wn * WN + li;
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) s1[ni] += __shfl_xor(s1[ni], 32, 64);
+  if (lh == 0) {
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) red[wm * BN + tcol + ni * 32] = s1[ni];
+  }
+  __syncthreads();
+  float mean[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < WPS; ++w) t += red[(sub * WPS + w) * BN + tcol + ni * 32];
+    mean[ni] = t / (float)nvalid;
+  }
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int col = n0 + wn * WN + ni * 32 + li;
+      const float bias = (a.bias && col < a.N) ? a.bias[(long long)g * a.bias_sg + col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < a.M) {
+          const float d = acc[mi][ni][r] + bias - mean[ni];
+          s2[ni] += d * d;
+        }
+      }
+    }
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) s2[ni] += __shfl_xor(s2[ni], 32, 64);
+  if (lh == 0) {
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) red[WGM * BN + wm * BN + tcol + ni * 32] = s2[ni];
+  }
+  __syncthreads();
+  const int col = tid % BN, sb = tid / BN, nv = min(SR, a.M - (m0 + sb * SR));
+  if (tid < SUB * BN && n0 + col < a.N && nv > 0) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < WPS; ++w) {
+      t1 += red[(sb * WPS + w) * BN + col];
+      t2 += red[WGM * BN + (sb * WPS + w) * BN + col];
+    }
+    const int mt = m0 / SR + sb;
+    const int gc = a.cpg ? (n0 + col) / a.cpg : g, cc = a.cpg ? (n0 + col) % a.cpg : n0 + col;
+    const int nc = a.cpg ? a.cpg : a.N;
+    const long long so = ((long long)gc * a.st_nblk + a.st_base + mt) * nc + cc;
+    a.st_mean[so] = t1 / (float)nv;
+    a.st_m2[so] = t2;
+    if (cc == 0) a.st_cnt[(long long)gc * a.st_nblk + a.st_base + mt] = (float)nv;
+  }
+  __syncthreads();
+}
+
 // fp32 data-gradient epilogue with a residual addend (optionally counted under ReLU-mask bits)
 // and / or accumulation into dx: the accumulators are parked in LDS ([rows][BN + 4] floats, the
 // whole tile when it fits SCRATCH bytes, else one wave row band per pass) and every thread then
@@ -189,14 +274,17 @@ __device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int
 // trip), added in fp32 and stored as float4.  The direct per-element form (conv_epilogue: one
 // 4-byte addend load behind each 1-byte mask load, per element) ran the bench's masked-addend
 // data gradients at 1.6-2.3 TB/s.  Requires N % 4 == 0 (host-checked Cin % 4).
-template <int BM, int BN, int MI, int NI, int WGM, int WGN, int SCRATCH>
-__device__ __forceinline__ void dgrad_epilogue_f32(const ConvArgs& a, floatx16 (&acc)[MI][NI],
-                                                   float* stile, int m0, int n0, int g) {
+// FWD (after fwd_stats_f32): the same 16-byte stores of the output rows (+ bias), for the
+// output-heavy short-K forwards (fp32 training step 267.6-267.9 -> 269.8-270.3 triplets/s
+// over the data-gradient change alone, same box).
+template <int MODE, int BM, int BN, int MI, int NI, int WGM, int WGN, int SCRATCH>
+__device__ __forceinline__ void staged_epilogue_f32(const ConvArgs& a, floatx16 (&acc)[MI][NI],
+                                                    float* stile, int m0, int n0, int g) {
   constexpr int NT = 64 * WGM * WGN, WM = BM / WGM, WN = BN / WGN;
   constexpr int SLD = BN + 4, CPR = BN / 4;
   constexpr int PASSES = BM * SLD * 4 <= SCRATCH ? 1
                          : ((WGM % 2 == 0 && (BM / 2) * SLD * 4 <= SCRATCH) ? 2 : WGM);
-  static_assert((BM / PASSES) * SLD * 4 <= SCRATCH && WGM % PASSES == 0, "dgrad epilogue scratch");
+  static_assert((BM / PASSES) * SLD * 4 <= SCRATCH && WGM % PASSES == 0, "staged epilogue scratch");
   constexpr int PR = BM / PASSES, NCH = PR * CPR, CPT = (NCH + NT - 1) / NT;
   constexpr int WPP = WGM / PASSES;  // wave rows per pass
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -207,12 +295,16 @@ __device__ __forceinline__ void dgrad_epilogue_f32(const ConvArgs& a, floatx16 (
     const int row = m0 + pass * PR + rl, col = n0 + 4 * cc;
     if (c >= NCH || row >= a.M || col >= a.N) return false;
     long long orow = row;
-    if (a.stride != 1) {  // class-local row -> input pixel
-      const int HW = a.Hc * a.Wc, b = row / HW, rem = row - b * HW;
-      const int i = rem / a.Wc, jj = rem - i * a.Wc;
-      orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
+    if constexpr (MODE == DGRAD) {
+      if (a.stride != 1) {  // class-local row -> input pixel
+        const int HW = a.Hc * a.Wc, b = row / HW, rem = row - b * HW;
+        const int i = rem / a.Wc, jj = rem - i * a.Wc;
+        orow = ((long long)b * a.H + a.stride * i + a.ph) * a.W + a.stride * jj + a.pw;
+      }
+      o = (long long)g * a.out_sg + orow * a.N + col;
+    } else {
+      o = (long long)g * a.out_sg + conv_out_index(a, orow, col);
     }
-    o = (long long)g * a.out_sg + orow * a.N + col;
     return true;
   };
   // two chunks in flight (a deeper prefetch spills the 128-VGPR budget of the eight-wave tiles)
@@ -224,7 +316,7 @@ __device__ __forceinline__ void dgrad_epilogue_f32(const ConvArgs& a, floatx16 (
     long long o = 0;
     pa[q] = pd[q] = floatx4{0.f, 0.f, 0.f, 0.f};
     pm[q] = 0xfu;
-    if (k < CPT && chunk(pass, tid + k * NT, o)) {
+    if (MODE == DGRAD && k < CPT && chunk(pass, tid + k * NT, o)) {
       if (a.addend) {
         pa[q] = *(const floatx4*)(a.addend + o);
         if (a.add_mask) pm[q] = (unsigned)(a.add_mask[o >> 3] >> (o & 7));
@@ -254,10 +346,14 @@ __device__ __forceinline__ void dgrad_epilogue_f32(const ConvArgs& a, floatx16 (
       if (chunk(pass, c, o)) {
         const int rl = c / CPR, cc = c - rl * CPR;
         floatx4 v = *(const floatx4*)(stile + rl * SLD + 4 * cc);
+        if constexpr (MODE == DGRAD) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if ((pm[q] >> e) & 1u) v[e] += pa[q][e];
-          v[e] += pd[q][e];
+          for (int e = 0; e < 4; ++e) {
+            if ((pm[q] >> e) & 1u) v[e] += pa[q][e];
+            v[e] += pd[q][e];
+          }
+        } else if (a.bias) {
+          v += *(const floatx4*)(a.bias + (long long)g * a.bias_sg + n0 + 4 * cc);
         }
         *(floatx4*)(outp + o) = v;
       }

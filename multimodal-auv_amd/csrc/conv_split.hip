@@ -398,9 +398,21 @@ void conv_split_f32(const ConvArgs a) {
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) acc[mi][ni] += acl[mi][ni];
   }
+  // fp32 outputs through LDS as 16-byte rows (staged_epilogue_f32): data gradients with a
+  // residual addend / accumulation, and forwards (statistics from the registers first); the
+  // per-element stores of conv_epilogue stay for the rest (plain data gradients, N % 4 != 0)
   if constexpr (MODE == DGRAD && !BP) {
     if (a.addend || a.accumulate) {
-      dgrad_epilogue_f32<BM, BN, MI, NI, WGM, WGN, NBUF * STG * 2>(a, acc, (float*)smem, m0, n0, g);
+      staged_epilogue_f32<DGRAD, BM, BN, MI, NI, WGM, WGN, NBUF * STG * 2>(a, acc, (float*)smem,
+                                                                          m0, n0, g);
+      return;
+    }
+  }
+  if constexpr (MODE == FWD) {
+    if (a.N % 4 == 0 && a.out_sg % 4 == 0 && a.cpg % 4 == 0 && a.bias_sg % 4 == 0) {
+      if (a.st_mean) fwd_stats_f32<BM, BN, MI, NI, WGM, WGN>(a, acc, (float*)smem, tid, m0, n0, g);
+      staged_epilogue_f32<FWD, BM, BN, MI, NI, WGM, WGN, NBUF * STG * 2>(a, acc, (float*)smem,
+                                                                        m0, n0, g);
       return;
     }
   }

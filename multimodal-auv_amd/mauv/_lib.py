@@ -122,8 +122,20 @@ def _load():
             "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
             "There is no CPU/PyTorch fallback.")
     lib = ctypes.CDLL(LIB_PATH)
+    # an explicitly chosen older library (MAUV_LIB, same-box A/B against a previous build) may
+    # lack entry points added since: those raise when called, every other binding is checked
+    older_ok = "MAUV_LIB" in os.environ
     for name, argt in SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if not older_ok:
+                raise
+
+            def missing(*a, _n=name):
+                raise MauvError(f"{_n} is not in {LIB_PATH} (an older library, MAUV_LIB)")
+            setattr(lib, name, missing)
+            continue
         fn.argtypes = argt
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
     return lib

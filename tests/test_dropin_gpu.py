@@ -255,9 +255,13 @@ def test_g6_predict_under_autocast(tmp_path):
     from oracle.resnet_ref import Bottleneck
     blk = next(mm for mm in oc.modules() if isinstance(mm, Bottleneck))
     dts = {}
-    hooks = [blk.bn3.register_forward_hook(lambda mod, i, out: dts.setdefault("bn3", out.dtype)),
-             blk.register_forward_hook(lambda mod, i, out: dts.setdefault("block", out.dtype)),
-             blk.conv3.register_forward_hook(lambda mod, i, out: dts.setdefault("conv3", out.dtype))]
+
+    def rec(key):
+        def hook(mod, inp, out):
+            dts.setdefault(key, out.dtype)   # returns None: the output is left as it is
+        return hook
+    hooks = [blk.bn3.register_forward_hook(rec("bn3")), blk.register_forward_hook(rec("block")),
+             blk.conv3.register_forward_hook(rec("conv3"))]
     bayes_ref.set_eps_source(eps_generator_source(SEED_EPS + 3))
     try:
         with torch.autocast("cuda", dtype=torch.float16):

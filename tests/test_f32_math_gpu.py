@@ -166,3 +166,4 @@ def test_mode_switch_roundtrip(f32_math):
     assert ops.f32_math() == "exact"
     assert f32_math("split") == "exact"
     assert ops.f32_math() == "split"
+

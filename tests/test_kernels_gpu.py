@@ -800,7 +800,7 @@ def test_reparam_sample_block_form_bit_identical(dt, G, Cout, Cin, R, cin_pad, e
 ])
 def test_dgrad_f32_staged_epilogue(Cin, Cout, R, st, H, form):
     """fp32 data gradients with a residual addend (under ReLU-mask bits or not) and / or
-    accumulation into dx: the LDS-staged 16-byte epilogue (conv_common.h dgrad_epilogue_f32)
+    accumulation into dx: the LDS-staged 16-byte epilogue (conv_common.h staged_epilogue_f32)
     against float64 — the addend counted exactly where the mask bit is set, classes without taps
     leaving dx (+ addend) as it was."""
     from mauv import ops

@@ -36,8 +36,14 @@ from tests.helpers import build_pair, EpsBridge, oracle_replay, cosines, fit_mod
 pytestmark = pytest.mark.gpu
 
 COS_MARGIN = 0.02    # whole-trunk / head gradient cosine: HIP >= autocast - COS_MARGIN
-RESOLVED = 0.5       # ... judged at RESOLVED_SHAPE, where autocast's own cosine is >= this
-RESOLVED_SHAPE = (64, 64, 32, 2)   # (S_opt, S_son, B, N): placeholder until measured
+# ... judged where torch-autocast's own whole-trunk cosine is >= RESOLVED.  At random init it
+# never is for bf16 (0.08-0.17 over B = 8-32 at 64-224 px, both schemes; f16 autocast 0.004-0.02,
+# its backward underflows without a GradScaler; profiles/round5/autocast_resolution_sweep.txt):
+# the resolved shapes are a model trained FIT_STEPS fp32 steps on the batch first (bf16: autocast
+# 1.000 at B = 8, 0.73-0.76 at B = 32)
+RESOLVED = 0.5
+FIT_STEPS = 20
+RESOLVED_SHAPES = [(64, 64, 8, 2), (64, 64, 32, 2)]   # (S_opt, S_son, B, N)
 WEAK_MARGIN = 0.1    # every other shape: HIP >= autocast - WEAK_MARGIN (never skipped)
 
 
@@ -167,20 +173,28 @@ def test_train_step16_grads_vs_torch_autocast(dt, S_opt, S_son, B, N):
     assert r["dlogit_hip"] <= max(2 * r["dlogit_autocast"], 1e-3)
 
 
+@pytest.mark.parametrize("shape", RESOLVED_SHAPES, ids=lambda s: f"B{s[2]}")
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
-def test_train_step16_whole_trunk_resolved(dt):
-    """Whole-trunk gradient cosines at a batch where torch-autocast itself resolves the float64
-    direction (its cosine >= RESOLVED on every trunk, asserted: the bar is not vacuous); HIP
-    >= autocast - COS_MARGIN there.  float64 truth on the GPU."""
-    S_opt, S_son, B, N = RESOLVED_SHAPE
-    r = train_step16_cosines(dt, S_opt, S_son, B, N, truth_device="cuda", fp32_cpu=False)
-    tag = f"{str(dt)[6:]} {S_opt}/{S_son} B={B} N={N}"
+def test_train_step16_whole_trunk_resolved(dt, shape):
+    """Whole-trunk gradient cosines where the reference's scheme resolves the float64 direction
+    (VERDICT r4 next 1), on a model trained FIT_STEPS steps on the batch: bf16 — torch-autocast's
+    cosine >= RESOLVED on every trunk (asserted, so the bar is not vacuous) and HIP >= autocast -
+    COS_MARGIN; f16 — autocast's training backward does not resolve it (f16 underflow without a
+    GradScaler; the reference runs f16 only in its predictor), so HIP's own cosine must be >=
+    RESOLVED and >= autocast's - COS_MARGIN.  float64 truth on the GPU."""
+    S_opt, S_son, B, N = shape
+    r = train_step16_cosines(dt, S_opt, S_son, B, N, truth_device="cuda", fp32_cpu=False,
+                             fit_steps=FIT_STEPS)
+    tag = f"{str(dt)[6:]} fit={FIT_STEPS} {S_opt}/{S_son} B={B} N={N}"
     print()
     _print_whole(tag, r)
     print(f"  max |dlogit| vs fp64: HIP {r['dlogit_hip']:.3e}  torch-autocast "
           f"{r['dlogit_autocast']:.3e}")
     for gname, c in r["whole"].items():
-        assert c["autocast"] >= RESOLVED, (gname, c)
+        if dt == torch.bfloat16:
+            assert c["autocast"] >= RESOLVED, (gname, c)
+        else:
+            assert c["hip"] >= RESOLVED, (gname, c)
         assert c["hip"] >= c["autocast"] - COS_MARGIN, (gname, c)
     assert r["dlogit_hip"] <= max(2 * r["dlogit_autocast"], 1e-3)
 
