@@ -277,7 +277,11 @@ __device__ __forceinline__ void fwd_stats_f32(const ConvArgs& a, floatx16 (&acc)
 // FWD (after fwd_stats_f32): the same 16-byte stores of the output rows (+ bias), for the
 // output-heavy short-K forwards (fp32 training step 267.6-267.9 -> 269.8-270.3 triplets/s
 // over the data-gradient change alone, same box).
-template <int MODE, int BM, int BN, int MI, int NI, int WGM, int WGN, int SCRATCH>
+// DGRAD + BP (bp_p1): dx is the output gradient of a BatchNorm (+ReLU); the store loop also
+// sums dz = dx * relu-mask and dz * xhat per column (bn_bwd_partial's two sums), with y (and the
+// mask bits / the BN's output) fetched beside the addend — one partial per block tile (the
+// conv_tile_rows m-tile) instead of a pass over (y, dout).
+template <int MODE, int BM, int BN, int MI, int NI, int WGM, int WGN, int SCRATCH, bool BP = false>
 __device__ __forceinline__ void staged_epilogue_f32(const ConvArgs& a, floatx16 (&acc)[MI][NI],
                                                     float* stile, int m0, int n0, int g) {
   constexpr int NT = 64 * WGM * WGN, WM = BM / WGM, WN = BN / WGN;
@@ -309,19 +313,46 @@ __device__ __forceinline__ void staged_epilogue_f32(const ConvArgs& a, floatx16 
   };
   // two chunks in flight (a deeper prefetch spills the 128-VGPR budget of the eight-wave tiles)
   constexpr int PFD = 2;
-  floatx4 pa[PFD], pd[PFD];
-  unsigned pm[PFD];
+  floatx4 pa[PFD], pd[PFD], py[PFD];
+  unsigned pm[PFD], pr[PFD];
+  static_assert(!BP || NT % CPR == 0, "BP: each thread keeps one column chunk");
+  const bool bst = MODE == DGRAD && BP && a.bp_p1;
+  // BP: this thread's column chunk (fixed: NT % CPR == 0) and its BN parameters
+  const int bcol = n0 + 4 * (tid % CPR);
+  floatx4 b1 = {0.f, 0.f, 0.f, 0.f}, b2 = b1, bmu = b1, bis = b1, bsc = b1, bsh = b1;
+  if (bst && bcol < a.N) {
+    bmu = *(const floatx4*)(a.bp_mean + (long long)g * a.N + bcol);
+    bis = *(const floatx4*)(a.bp_invstd + (long long)g * a.N + bcol);
+    if (a.bp_relu && !a.bp_out && !a.bp_mask) {
+      bsc = *(const floatx4*)(a.bp_sc + (long long)g * a.N + bcol);
+      bsh = *(const floatx4*)(a.bp_sh + (long long)g * a.N + bcol);
+    }
+  }
   auto prefetch = [&](int pass, int k) {
     const int q = k % PFD;
     long long o = 0;
-    pa[q] = pd[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+    pa[q] = pd[q] = py[q] = floatx4{0.f, 0.f, 0.f, 0.f};
     pm[q] = 0xfu;
+    pr[q] = 0xfu;
     if (MODE == DGRAD && k < CPT && chunk(pass, tid + k * NT, o)) {
       if (a.addend) {
         pa[q] = *(const floatx4*)(a.addend + o);
         if (a.add_mask) pm[q] = (unsigned)(a.add_mask[o >> 3] >> (o & 7));
       }
       if (a.accumulate) pd[q] = *(const floatx4*)(outp + o);
+      if (bst) {
+        py[q] = *(const floatx4*)(a.bp_y + o);
+        if (a.bp_relu) {
+          if (a.bp_mask) {
+            pr[q] = (unsigned)(a.bp_mask[o >> 3] >> (o & 7));
+          } else {
+            const floatx4 pre = a.bp_out ? *(const floatx4*)(a.bp_out + o) : py[q] * bsc + bsh;
+            pr[q] = 0u;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pr[q] |= (pre[e] > 0.f ? 1u : 0u) << e;
+          }
+        }
+      }
     }
   };
 #pragma unroll
@@ -352,6 +383,14 @@ __device__ __forceinline__ void staged_epilogue_f32(const ConvArgs& a, floatx16 
             if ((pm[q] >> e) & 1u) v[e] += pa[q][e];
             v[e] += pd[q][e];
           }
+          if (bst) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float dz = (pr[q] >> e) & 1u ? v[e] : 0.f;
+              b1[e] += dz;
+              b2[e] += dz * (py[q][e] - bmu[e]) * bis[e];
+            }
+          }
         } else if (a.bias) {
           v += *(const floatx4*)(a.bias + (long long)g * a.bias_sg + n0 + 4 * cc);
         }
@@ -360,6 +399,25 @@ __device__ __forceinline__ void staged_epilogue_f32(const ConvArgs& a, floatx16 
       prefetch(pass, k + PFD);   // (slot q is this chunk's: free)
     }
     if (pass + 1 < PASSES) __syncthreads();
+  }
+  if (bst) {
+    // the NT / CPR threads of a column chunk, through LDS (after the last pass's stile reads)
+    constexpr int TPC = NT / CPR;
+    float* red = stile;
+    __syncthreads();
+    *(floatx4*)(red + (tid / CPR) * BN + 4 * (tid % CPR)) = b1;
+    *(floatx4*)(red + (TPC + tid / CPR) * BN + 4 * (tid % CPR)) = b2;
+    __syncthreads();
+    if (tid < 2 * BN) {
+      const int col = tid % BN, which = tid / BN;
+      if (n0 + col < a.N) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < TPC; ++w) t += red[(which * TPC + w) * BN + col];
+        const long long so = ((long long)g * a.bp_nblk + a.bp_base + m0 / BM) * a.N + n0 + col;
+        (which ? a.bp_p2 : a.bp_p1)[so] = t;
+      }
+    }
   }
 }
 

@@ -83,7 +83,7 @@ __device__ __forceinline__ int row_of(int idx) {
 template <int MODE, int BM, int BN, bool XBN, bool ONEACC, int WV, bool STEM = false,
           bool SEQ = false, bool BP = false>
 __global__ __launch_bounds__((SplitWaves<BM, BN, WV>::T))
-__attribute__((amdgpu_waves_per_eu(SEQ ? 6 : SplitWaves<BM, BN, WV>::EU)))
+__attribute__((amdgpu_waves_per_eu(SEQ && !BP ? 6 : SplitWaves<BM, BN, WV>::EU)))
 void conv_split_f32(const ConvArgs a) {
   constexpr int BK = 16;
   constexpr int WGM = SplitWaves<BM, BN, WV>::M, WGN = SplitWaves<BM, BN, WV>::N;
@@ -401,10 +401,10 @@ void conv_split_f32(const ConvArgs a) {
   // fp32 outputs through LDS as 16-byte rows (staged_epilogue_f32): data gradients with a
   // residual addend / accumulation, and forwards (statistics from the registers first); the
   // per-element stores of conv_epilogue stay for the rest (plain data gradients, N % 4 != 0)
-  if constexpr (MODE == DGRAD && !BP) {
-    if (a.addend || a.accumulate) {
-      staged_epilogue_f32<DGRAD, BM, BN, MI, NI, WGM, WGN, NBUF * STG * 2>(a, acc, (float*)smem,
-                                                                          m0, n0, g);
+  if constexpr (MODE == DGRAD) {
+    if (BP || a.addend || a.accumulate) {
+      staged_epilogue_f32<DGRAD, BM, BN, MI, NI, WGM, WGN, NBUF * STG * 2, BP>(
+          a, acc, (float*)smem, m0, n0, g);
       return;
     }
   }
@@ -445,7 +445,9 @@ static void split_tiles(const ConvArgs& a, int oneacc, hipStream_t st) {
   const int bm = conv_tile_rows(a.M), bn = conv_tile_rows(a.N);
   if constexpr (MODE == DGRAD) {
     if (a.bp_p1) {  // BN-backward partials from the epilogue (the bn_p1 arguments of the C-ABI)
-      if (bm == 128 && bn == 128) launch_split<MODE, 128, 128, XBN, 8, false, false, true>(a, oneacc, st);
+      if (bm == 128 && bn == 128 && a.K > 0 && a.K <= kSplitShortK)
+        launch_split<MODE, 128, 128, XBN, 8, false, true, true>(a, oneacc, st);
+      else if (bm == 128 && bn == 128) launch_split<MODE, 128, 128, XBN, 8, false, false, true>(a, oneacc, st);
       else if (bm == 128 && bn == 64) launch_split<MODE, 128, 64, XBN, 8, false, false, true>(a, oneacc, st);
       else if (bm == 64 && bn == 128) launch_split<MODE, 64, 128, XBN, 8, false, false, true>(a, oneacc, st);
       else launch_split<MODE, 64, 64, XBN, 4, false, false, true>(a, oneacc, st);

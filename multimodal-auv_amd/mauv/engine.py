@@ -46,6 +46,13 @@ RES_MASK = True
 # (bit-identical) and FOLD_MIN_TILES 0 to fold their small shapes.
 FOLD = True
 FOLD_MIN_TILES = 512
+# fp32 training: the BatchNorm-backward partial sums (sum dz, sum dz * xhat per channel) of a BN
+# whose output gradient a data gradient produces are summed in that data gradient's LDS-staged
+# epilogue (conv_common.h staged_epilogue_f32 + BP), so the partial pass over (y, dout) is not
+# run: bn2 / bn1 from the conv3 / conv2 data gradients, the previous block's bn3 from conv1's
+# (whose epilogue already adds the residual gradient; not where a downsample branch accumulates
+# into that dx afterwards).  Test hook like FOLD: the same sums in another fp32 order.
+BWD_PARTIALS_F32 = True
 _STREAMS = {}
 
 
@@ -460,8 +467,23 @@ class TrunkRunner(_Runner):
         tiles = -(-B * H * W // 256) * self.G * -(-N // (256 if N >= 256 else 128))
         return tiles >= FOLD_MIN_TILES
 
+    def _dgrad_partials(self, rec, s):
+        """fp32: a {p1, p2, nblk, y, ...} dict for conv2d_bwd_data(bn=...) — rec's data gradient
+        is the output gradient of BN s — or None (16-bit, or the switch off)."""
+        if not BWD_PARTIALS_F32 or self.dt != torch.float32 or s is None or \
+                (s.out is not None and s.mask is None):
+            return None
+        conv, x, xs, x_bn, w, B, H, W = rec
+        G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, _first(conv.kernel_size)
+        st, pd = _first(conv.stride), _first(conv.padding)
+        nblk = ops.dgrad_stat_blocks(G, B, H, W, Cin, Cout, k, st, pd)
+        buf = torch.empty(2, G, nblk, Cin, device=s.y.device)
+        st_ = s.stats
+        return dict(y=s.y, out=None, mask=s.mask, scale=st_[2], shift=st_[3], mean=st_[0],
+                    invstd=st_[1], relu=int(s.relu), p1=buf[0], p2=buf[1], nblk=nblk)
+
     def _conv_bwd(self, rec, dy, need_dx=True, addend=None, dx=None, accumulate=False,
-                  addend_mask=None):
+                  addend_mask=None, bn=None):
         """Weight gradient (+ reparameterisation backward) and data gradient (+ addend, counted
         only under addend_mask's ReLU bits when given)."""
         conv, x, xs, x_bn, w, B, H, W = rec
@@ -481,7 +503,7 @@ class TrunkRunner(_Runner):
         if dx is None:
             dx = torch.empty(G, B, H, W, Cin, device=dy.device, dtype=self.dt)
         ops.conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, k, st, pd, addend=addend,
-                            accumulate=accumulate, addend_mask=addend_mask)
+                            accumulate=accumulate, addend_mask=addend_mask, bn=bn)
         return dx
 
     def _stem(self, conv, x, B, H, W):
@@ -562,9 +584,10 @@ class TrunkRunner(_Runner):
         self.last_lazy = (scale, shift, int(relu))  # for a consumer applying it on load
         return out, rec
 
-    def _bn_bwd(self, rec, dout, want_dres=False, mask=None):
+    def _bn_bwd(self, rec, dout, want_dres=False, mask=None, pre=None):
         """mask: ReLU-mask bits applied to dout (a downsample BN fed the block output's
-        dres = dout * mask without that tensor)."""
+        dres = dout * mask without that tensor); pre: the partial sums dout's data gradient
+        wrote (_dgrad_partials), so the partial pass is skipped."""
         if not rec.batch_stats:
             raise NotImplementedError("mauv: backward through eval-mode BN is not on the path "
                                       "(the reference trains and predicts in .train())")
@@ -575,7 +598,10 @@ class TrunkRunner(_Runner):
         dg = bn.weight.grad if bn.weight.requires_grad else None
         db = bn.bias.grad if bn.bias.requires_grad else None
         s = rec.stats
-        if mask is not None:
+        if pre is not None:
+            ops.bn_bwd_ex(rec.y, None, rec.mask, dout, rec.relu, s[0], s[1], s[2], s[3], G, M, C,
+                          ws, dy, dres, dg, db, pre=(pre["p1"], pre["p2"], pre["nblk"]))
+        elif mask is not None:
             ops.bn_bwd_ex(rec.y, None, mask, dout, 1, s[0], s[1], s[2], s[3], G, M, C, ws, dy,
                           dres, dg, db)
         elif rec.mask is not None:
@@ -685,24 +711,28 @@ class TrunkRunner(_Runner):
         da = torch.empty(G, B, H, W, 2048, device=dout.device, dtype=self.dt)
         ops.avgpool_bwd(dfeat, G * B, H * W, 2048, da)
         del dfeat
+        pre3 = None   # the partials of this block's bn3, from the next block's conv1 data gradient
         while self.recs:
             r1, s1, r2, s2, r3, s3, rd, sd = self.recs.pop()
             # the residual gradient: dres = da * mask3, kept implicit when bn3 has mask bits
             rmask = s3.mask if RES_MASK and s3.mask is not None and \
                 (rd is not None or self.dt == torch.float32 or self._masked_addend_ok(r1)) \
                 else None
-            dy3, dres = self._bn_bwd(s3, da, want_dres=rmask is None)
+            dy3, dres = self._bn_bwd(s3, da, want_dres=rmask is None, pre=pre3)
             if rmask is not None:
                 dres = da
-            del da, s3
-            da2 = self._conv_bwd(r3, dy3)
+            del da, s3, pre3
+            pre2 = self._dgrad_partials(r3, s2)
+            da2 = self._conv_bwd(r3, dy3, bn=pre2)
             del dy3, r3
-            dy2, _ = self._bn_bwd(s2, da2)
-            del da2, s2
-            da1 = self._conv_bwd(r2, dy2)
+            dy2, _ = self._bn_bwd(s2, da2, pre=pre2)
+            del da2, s2, pre2
+            pre1 = self._dgrad_partials(r2, s1)
+            da1 = self._conv_bwd(r2, dy2, bn=pre1)
             del dy2, r2
-            dy1, _ = self._bn_bwd(s1, da1)
-            del da1, s1
+            dy1, _ = self._bn_bwd(s1, da1, pre=pre1)
+            del da1, s1, pre1
+            pre3 = None
             if rd is not None:
                 dyd, _ = self._bn_bwd(sd, dres, mask=rmask)
                 del dres, sd
@@ -710,7 +740,12 @@ class TrunkRunner(_Runner):
                 self._conv_bwd(rd, dyd, dx=dx, accumulate=True)
                 del dyd, rd
             else:
-                dx = self._conv_bwd(r1, dy1, addend=dres, addend_mask=rmask)
+                # dx is the previous block's block-output gradient: its bn3 partials come from
+                # this epilogue (with its ReLU-mask bits), after the residual addend is added
+                prev3 = self.recs[-1][5] if self.recs else None
+                pre3 = self._dgrad_partials(r1, prev3) if prev3 is not None and \
+                    prev3.mask is not None else None
+                dx = self._conv_bwd(r1, dy1, addend=dres, addend_mask=rmask, bn=pre3)
                 del dres
             del dy1, r1
             da = dx

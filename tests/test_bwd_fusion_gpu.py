@@ -48,3 +48,33 @@ def test_residual_gradient_from_mask_bits_is_exact(dt, monkeypatch):
     assert torch.equal(lg0, lg1)
     bad = [n for n in g0 if not torch.equal(g0[n], g1[n])]
     assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("S,B", [(64, 2), (96, 3)])
+def test_fp32_bn_partials_from_data_gradient_epilogue(S, B, monkeypatch):
+    """engine.BWD_PARTIALS_F32: in the fp32 step the BN-backward partial sums
+    of bn2 / bn1 and of the previous block's bn3 come from the LDS-staged epilogue of the data
+    gradient that produces their output gradient instead of a pass over (y, dout).  The same
+    fp32 terms summed in another order: logits identical, every gradient tensor at cosine >=
+    0.9999 with the pass form and the whole arena at >= 0.99999."""
+    from mauv import engine
+    _, m = build_pair()
+    x, b, s, y = _batch(B, S)
+    monkeypatch.setattr(engine, "BWD_PARTIALS_F32", False)
+    lg0, g0 = _step(m, x, b, s, y, 2)
+    monkeypatch.setattr(engine, "BWD_PARTIALS_F32", True)
+    lg1, g1 = _step(m, x, b, s, y, 2)
+    assert torch.equal(lg0, lg1)
+    worst = (1.0, None)
+    for n in g0:
+        a, c = g0[n].double().flatten(), g1[n].double().flatten()
+        if a.norm().item() == 0.0:
+            assert c.norm().item() == 0.0, n
+            continue
+        cos = (a @ c).item() / (a.norm() * c.norm()).item()
+        worst = min(worst, (cos, n))
+    A = torch.cat([g0[n].double().flatten() for n in g0])
+    C = torch.cat([g1[n].double().flatten() for n in g0])
+    gcos = (A @ C).item() / (A.norm() * C.norm()).item()
+    print(f"fp32 {S} px B={B}: whole arena cosine {gcos:.9f}, worst tensor {worst}")
+    assert gcos >= 0.99999 and worst[0] >= 0.9999, (gcos, worst)

@@ -307,7 +307,7 @@ def test_reparam16_padded_sample_and_bwd(dt):
 def test_conv16_dgrad_bn_partials_epilogue(case, src, res, dt):
     """The data gradient's epilogue writes the BN-backward partials of the BN whose output
     gradient dx is (conv2d_bwd_data(..., bn=...); 16-bit: conv_epi16.h, fp32: the split
-    kernel's direct-store epilogue): dx bit-identical to the plain data gradient;
+    kernel's LDS-staged epilogue, conv_common.h staged_epilogue_f32): dx bit-identical to the plain data gradient;
     the BN backward finished from those partials (bn_bwd_ex(pre=...)) matches the standalone
     partial pass within fp32 summation order, and both match float64 on the same 16-bit dx."""
     from mauv import ops

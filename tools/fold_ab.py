@@ -5,7 +5,7 @@ mc_train_step + FusedAdam): interleaved rounds in one process, wall clock of who
 steps after warm-up.
 
     python tools/fold_ab.py [--rounds 3] [--batch 256] [--mc 100] [--sonar 256] [--only 0|1]
-    python tools/fold_ab.py --train [--rounds 3] [--steps 10]
+    python tools/fold_ab.py --train [--rounds 3] [--steps 10] [--dtype fp32] [--flag BWD_PARTIALS_F32]
 """
 import argparse
 import os
@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--flag", default="FOLD",
                     help="the engine switch the two arms set False / True (e.g. FOLD)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="--train: trunk precision of the step")
     ap.add_argument("--tiles", type=int, nargs=2, default=None, metavar=("A", "B"),
                     help="--train: compare engine.FOLD_MIN_TILES A against B (fold on in both)")
     a = ap.parse_args()
@@ -83,7 +85,7 @@ def train_ab(a):
     crit = torch.nn.CrossEntropyLoss()
     B = 64
     x, b, s, y = bench.synthetic_batch(B, 224, a.sonar, dev, 1234)
-    set_precision(model, torch.bfloat16)
+    set_precision(model, torch.bfloat16 if a.dtype == "bf16" else None)
     kl_w = 2.0 ** 1 / 2.0 ** 30
 
     def step():
