@@ -268,7 +268,11 @@ def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=Non
         _dev(torch.uint8, b["mask"])
     if bn is not None:
         nb += 4 * G * B * H * W * Cin * (1 + (b.get("out") is not None))
-    with _Prof("dgrad", fl, nb, nl, info=(G, B, H, W, Cin, Cout, R, stride, pad,
+    # a data gradient that also sums a BN's backward partials in its epilogue (engine
+    # BWD_PARTIALS_F32) is its own kind in the bench's breakdown ("dgrad+bn"; inside the fp32
+    # MFMA roofline, with the y bytes it reads counted)
+    with _Prof("dgrad" if bn is None else "dgrad+bn", fl, nb, nl,
+               info=(G, B, H, W, Cin, Cout, R, stride, pad,
                                            (addend is not None, bool(accumulate),
                                             addend_mask is not None))):
         check(lib.mauv_conv2d_bwd_data_f32(
