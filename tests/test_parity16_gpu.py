@@ -8,21 +8,19 @@ predictor's statistics) as that scheme, within a stated margin.
 
 * Training step at the BASELINE tile sizes (224 optical / 256 sonar, B=4, N=2) and at 64 px:
   gradients of EVERY parameter tensor (trunks included, 696 tensors) against the float64
-  truth.  At random init the 16-bit trunk gradients of BOTH schemes are dominated by amplified
-  rounding (measured per-tensor cosines with the truth: median ~0.2 bf16 for both; the fp32
-  CPU oracle's own is printed beside them), so two noisy estimates of one tensor are not
-  comparable one by one; the bars are on the distribution and on whole trunks:
-    - median and 10th percentile of the per-tensor cosines, over all tensors and over the
-      trunk tensors: HIP >= autocast - 0.01 (median) / - 0.02 (p10);
-    - cosine of each trunk's whole gradient (its tensors concatenated) and of the fusion
-      head's: HIP >= autocast - COS_MARGIN wherever either scheme resolves the float64
-      direction (cos >= RESOLVED; printed and kept in profiles/round4/ either way);
-    - logits: max |HIP - fp64| <= 2x max |autocast - fp64|.
+  truth, by the per-tensor cosine distribution (median / p10: HIP >= autocast - 0.01 / - 0.02)
+  and each trunk's whole gradient (HIP >= autocast - WEAK_MARGIN, always judged: at random init
+  both bf16 schemes sit at cosines 0.08-0.17 and f16 autocast at 0.004-0.03, so this bar only
+  catches a broken trunk); logits: max |HIP - fp64| <= 2x max |autocast - fp64|.
+* The same step on a model trained FIT_STEPS steps on the batch (64 px, B = 8 and 32), where
+  the reference's scheme resolves the float64 direction: whole-trunk cosines HIP >= autocast -
+  COS_MARGIN, with autocast >= RESOLVED asserted (bf16) / HIP >= RESOLVED (f16, whose autocast
+  backward underflows) so the bar cannot pass vacuously.
 * f16 predictor (the drop-in default path, ``multimodal_predict_and_save``'s maths) at B=64,
-  N=8 (64 / 128 px) and B=16, N=8 at 224 / 256 px after a few training steps on the batch (``fit_model``: the class then depends on the
-  input; at random init every golden item is class 4): predictive variance and aleatoric uncertainty deviate from
-  the fp32 oracle by at most 2x what torch-autocast deviates (max over items), and the class
-  agrees with the fp32 oracle on >= 99 % of the items.
+  N=8 (64 / 128 px) and B=16, N=8 at 224 / 256 px on a model fitted to the batch (``fit_model``:
+  the class then depends on the input): logits within SURVEY §8c's 16-bit row, variance and
+  aleatoric deviations vs the fp32 oracle <= 2x torch-autocast's on average and 3x at the worst
+  item, argmax agreement >= 99 %.
 """
 import numpy as np
 import pytest
@@ -204,7 +202,17 @@ def test_train_step16_whole_trunk_resolved(dt, shape):
                          ids=["64px", "128px", "224-256px"])
 def test_predictor_f16_vs_torch_autocast(S_opt, S_son, B, N):
     """The drop-in predictor's default path (f16 trunks under autocast, predictors.py:55),
-    also at the configs[3] tile sizes (224 optical / 256 sonar)."""
+    also at the configs[3] tile sizes (224 optical / 256 sonar), on a model fitted to the batch.
+
+    Bars: the logits within SURVEY §8c's 16-bit row of the fp32 oracle, normwise (max |d| <= 5e-2
+    max(1, max |ref|): the fitted logits span +-50 and both schemes' errors scale with that range,
+    not with each element), and on average no more than 1.25x torch-autocast's; the per-item predictive-variance and aleatoric deviations from the fp32 oracle at most
+    2x torch-autocast's on average over the items and 3x at the worst item; argmax agreement
+    >= 99 %.  Why the mean and not only the worst item (round 5): on two fitted weight sets that
+    differ only in the last bits of the fp32 training sums, the worst-item ratio HIP / autocast
+    was 0.67x and 2.45x while the mean logit errors of the two schemes were equal (4.3e-2 vs
+    4.2e-2, logits up to 50) — the worst of 16 items is an extreme value of two noisy estimates
+    (autocast's own worst item moved 2.0e-3 .. 5.4e-3 between runs on the same weights)."""
     from mauv.engine import root_state
     from mauv.predict import mc_statistics
     o, m = build_pair()
@@ -219,6 +227,13 @@ def test_predictor_f16_vs_torch_autocast(S_opt, S_son, B, N):
     with bridge:
         pred32, var32, alea32, _ = loops_ref.predict_batch(o, x, b, s, N)   # fp32 oracle
     bridge.collect()
+    _, lg32 = oracle_replay(o, bridge.store, lambda mm: torch.stack(
+        [mm(x, b, s) for _ in range(N)]).detach())
+
+    def ac_logits(mm):
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+            return torch.stack([mm(*_cuda(x, b, s)) for _ in range(N)]).double().cpu()
+    _, lg_ac = oracle_replay(o, bridge.store, ac_logits, device="cuda")
 
     def ac(mm):
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
@@ -227,17 +242,28 @@ def test_predictor_f16_vs_torch_autocast(S_opt, S_son, B, N):
     root_state(m).eps_provider = bridge.provider
     with torch.no_grad(), torch.autocast("cuda"):
         st = mc_statistics(m, *_cuda(x, b, s), N, chunk=N)
+    root_state(m).eps_provider = bridge.provider
+    with torch.no_grad(), torch.autocast("cuda"):
+        lg16 = m.mc_forward(*_cuda(x, b, s), N).double().cpu()
     classes = len(set(pred32.tolist()))
-    dv_h = (st["var"].double().cpu() - var32.double()).abs().max().item()
-    dv_a = (var_ac.double().cpu() - var32.double()).abs().max().item()
-    da_h = (st["aleatoric"].double().cpu() - alea32.double()).abs().max().item()
-    da_a = (alea_ac.double().cpu() - alea32.double()).abs().max().item()
+    ref = lg32.double()
+    dl = (lg16 - ref).abs()
+    dl_ac = (lg_ac - ref).abs()
+    dv_h = (st["var"].double().cpu() - var32.double()).abs()
+    dv_a = (var_ac.double().cpu() - var32.double()).abs()
+    da_h = (st["aleatoric"].double().cpu() - alea32.double()).abs()
+    da_a = (alea_ac.double().cpu() - alea32.double()).abs()
     agree = (st["pred"].cpu() == pred32).float().mean().item()
     agree_ac = (pred_ac.cpu() == pred32).float().mean().item()
-    print(f"\nS={S} B={B} N={N}: {classes} classes predicted; |dvar| HIP {dv_h:.3e} autocast "
-          f"{dv_a:.3e}; |dalea| HIP {da_h:.3e} autocast {da_a:.3e}; argmax agreement HIP "
-          f"{agree:.3f} autocast {agree_ac:.3f}")
+    print(f"\nS={S} B={B} N={N}: {classes} classes predicted; logits |d| max/mean HIP "
+          f"{dl.max():.3e}/{dl.mean():.3e} autocast {dl_ac.max():.3e}/{dl_ac.mean():.3e} "
+          f"(|ref| <= {ref.abs().max():.1f}); |dvar| max/mean HIP {dv_h.max():.3e}/"
+          f"{dv_h.mean():.3e} autocast {dv_a.max():.3e}/{dv_a.mean():.3e}; |dalea| max/mean HIP "
+          f"{da_h.max():.3e}/{da_h.mean():.3e} autocast {da_a.max():.3e}/{da_a.mean():.3e}; "
+          f"argmax agreement HIP {agree:.3f} autocast {agree_ac:.3f}")
     assert classes >= 3            # the class check is not degenerate
-    assert dv_h <= 2 * dv_a + 1e-7
-    assert da_h <= 2 * da_a + 1e-6
+    assert dl.max() <= 5e-2 * max(1.0, ref.abs().max().item())
+    assert dl.mean() <= 1.25 * dl_ac.mean()
+    assert dv_h.mean() <= 2 * dv_a.mean() + 1e-7 and dv_h.max() <= 3 * dv_a.max() + 1e-7
+    assert da_h.mean() <= 2 * da_a.mean() + 1e-6 and da_h.max() <= 3 * da_a.max() + 1e-6
     assert agree >= 0.99
