@@ -215,9 +215,9 @@ def test_g6_predict_under_autocast(tmp_path):
     scheme (the oracle under torch.autocast(f16) on the GPU, same weights and epsilons) is
     printed beside it but is not the bar: its deviation moves 2x from box to box (max 0.98 -
     2.11e-8, mean 0.49 - 1.51e-8: the vendor conv kernels it picks), while this path's is deterministic (max 3.34e-8,
-    mean 1.48e-8).  The larger part of the difference is the residual stream: autocast keeps a
-    block output fp32 (relu(bn3 + identity) outside its f16 op list) and rounds it only as the
-    next conv's input, here the block output is stored once in f16."""
+    mean 1.48e-8).  Both schemes keep conv outputs, BN outputs and block outputs in float16 —
+    printed below from hooks on the oracle under autocast — so the difference
+    is where each rounds inside the block, not a wider residual stream on autocast's side."""
     import Multimodal_AUV.inference.predictors as pr
     from Multimodal_AUV.models.model_utils import define_models
     o = _oracle_trained_g5()
