@@ -303,6 +303,8 @@ def test_reparam16_padded_sample_and_bwd(dt):
     ((1, 2, 4, 512, 2048, 1, 1, 0), "none", True),     # no ReLU (the downsample's BN), BM = 64
     ((1, 8, 136, 64, 64, 1, 1, 0), "mask", True),      # 1,156 partials per channel: the
                                                        # segmented finalize (bn_bwd_seg)
+    ((2, 2, 12, 512, 128, 1, 1, 0), "mask", True),     # 16-bit: the short-K form (K = 128)
+    ((1, 2, 12, 1024, 256, 1, 1, 0), "lazy", False),   # 16-bit: the short-K form (K = 256)
 ])
 def test_conv16_dgrad_bn_partials_epilogue(case, src, res, dt):
     """The data gradient's epilogue writes the BN-backward partials of the BN whose output
