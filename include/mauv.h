@@ -111,6 +111,12 @@ int mauv_set_big16(int mode, int min_k);
    K >= min_k, 0 = none; -1 queries.  Returns the previous mode.  Replaces nothing in the
    reference (F.conv2d under Conv2dReparameterization, models/base_models.py:74-90). */
 int mauv_set_dma16(int mode, int min_k);
+// Route 16-bit 1x1 / stride-1 expansion forwards (K = 64 / 128 / 256 input channels, N a multiple
+// of 256 / 512 outputs: the bottleneck conv3s, the layer-1 downsample) through the
+// weight-stationary kernel (conv_expand16.hip): 1 (default) where it measured faster, 2 every
+// covered shape, 0 none, -1 query.  Returns the previous mode.  (Replaces nothing in the
+// reference: a routing switch for A/Bs.)
+int mauv_set_expand16(int mode);
 
 /* ---- 16-bit implicit-GEMM convs (conv_gemm16.hip) -----------------------------------------
  * Same three GEMM views on v_mfma_f32_32x32x16_{bf16,f16}: dtype 0 = bf16 (BASELINE configs[2]

@@ -126,6 +126,17 @@ def set_big16(mode=None, min_k=0):
     return rc
 
 
+def set_expand16(mode=None):
+    """Route 16-bit 1x1 / stride-1 expansion forwards (K = 64 / 128 / 256) through the
+    weight-stationary kernel (conv_expand16.hip): 1 (default) where it measured faster, 2 (or
+    True) every shape it covers, 0 (or False) none (the implicit GEMM), None keep.  Returns the
+    previous mode (0 / 1 / 2)."""
+    m = -1 if mode is None else (2 if mode is True else (0 if mode is False else int(mode)))
+    rc = lib.mauv_set_expand16(m)
+    check(0 if rc >= 0 else rc, "set_expand16")
+    return rc
+
+
 def set_dma16(mode=None, min_k=0):
     """Route 16-bit forwards through the 128 x 128 LDS-DMA tiles: 1 (default) where they measured
     faster, 2 (or True) every forward they cover with K >= min_k, 0 (or False) none; None /

@@ -1,0 +1,83 @@
+"""A/B of the weight-stationary 16-bit expansion forwards (conv_expand16.hip)
+against the implicit GEMM (conv_pipe16) over every 1x1 / stride-1 forward of the three trunks it
+covers (K = 64 / 128 / 256 into N = 4K; conv3 with the pending BN on load, the layer-1
+downsample without), interleaved rounds in one process, outputs compared bit for bit.
+
+    python tools/expand_ab.py [--dtype bf16|f16] [--G 5] [--B 64] [--rounds 3]
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-auv_amd"), os.path.join(REPO, "tools")]
+import torch  # noqa: E402
+from mauv import ops  # noqa: E402
+from conv_bench import trunk_convs  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
+    ap.add_argument("--G", type=int, default=5)
+    ap.add_argument("--B", type=int, default=64)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    dt = {"bf16": torch.bfloat16, "f16": torch.float16}[a.dtype]
+    G, B = a.G, a.B
+    torch.manual_seed(0)
+    shapes = {}
+    for trunk, cin, S in (("opt", 3, 224), ("bathy", 3, 256), ("sss", 1, 256)):
+        for name, Cin, Cout, R, st, pd, H in trunk_convs(cin, S):
+            if R == 1 and st == 1 and Cin in (64, 128, 256) and Cout == 4 * Cin:
+                shapes.setdefault((Cin, Cout, H, name.endswith("c3")), []).append(f"{trunk}:{name}")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    res = {k: {0: [], 1: []} for k in shapes}
+    for rnd in range(a.rounds):
+        for key in shapes:
+            Cin, Cout, H, xb = key
+            x = torch.randn(G, B, H, H, Cin, device="cuda").to(dt)
+            w = (torch.randn(G, Cout, 1, 1, Cin, device="cuda") / Cin ** 0.5).to(dt)
+            nblk = ops.fwd_stat_blocks(G, B, H, H, Cin, Cout, 1, 1, 0)
+            stats = tuple(torch.empty(*s, device="cuda") for s in ((G, nblk, Cout), (G, nblk, Cout),
+                                                                  (G, nblk)))
+            x_bn = (torch.rand(G, Cin, device="cuda") + 0.5,
+                    torch.randn(G, Cin, device="cuda") * 0.1, 1) if xb else None
+            outs = {}
+            for arm in ((0, 1) if rnd % 2 == 0 else (1, 0)):
+                y = torch.empty(G, B, H, H, Cout, device="cuda", dtype=dt)
+                prev = ops.set_expand16(2 * arm)   # 0: conv_pipe16, 2: every covered shape
+                try:
+                    fn = lambda: ops.conv2d_fwd(x, w, y, G, B, H, H, Cin, Cout, 1, 1, 0,
+                                                x_bn=x_bn, stats=stats)
+                    fn()
+                    e0.record()
+                    for _ in range(a.reps):
+                        fn()
+                    e1.record()
+                    torch.cuda.synchronize()
+                finally:
+                    ops.set_expand16(prev)
+                res[key][arm].append(e0.elapsed_time(e1) / a.reps)
+                outs[arm] = y
+            if not torch.equal(outs[0], outs[1]):
+                print(f"OUTPUT DIFFERS {key}", flush=True)
+            del x, w, outs
+    tot = {0: 0.0, 1: 0.0}
+    print(f"{'Cin,Cout,H,xbn':22s} {'n':>3s} {'pipe16 ms':>10s} {'expand ms':>10s} {'GB/s':>7s} "
+          f"{'GB/s e':>7s} {'speedup':>8s}  layers")
+    for key, v in sorted(shapes.items(), key=lambda kv: -min(res[kv[0]][0])):
+        Cin, Cout, H, xb = key
+        nb = 2 * G * B * H * H * (Cin + Cout)
+        t0, t1 = min(res[key][0]), min(res[key][1])
+        tot[0] += t0 * len(v)
+        tot[1] += t1 * len(v)
+        print(f"{str(key):22s} {len(v):3d} {t0:10.3f} {t1:10.3f} {nb / t0 / 1e6:7.0f} "
+              f"{nb / t1 / 1e6:7.0f} {t0 / t1:8.3f}  {' '.join(v[:4])}")
+    print(f"TOTAL (x occurrences): pipe16 {tot[0]:.2f} ms, expand {tot[1]:.2f} ms "
+          f"({tot[0] / tot[1]:.3f}x)")
+
+
+if __name__ == "__main__":
+    main()

@@ -22,6 +22,16 @@ from mauv.predict import mc_statistics, mc_chunk  # noqa: E402
 from mauv.models import define_models, DEFAULT_PRIOR  # noqa: E402
 
 
+def _set(flag, on):
+    """An engine switch (engine.FOLD, ...) or a library routing switch named ops.set_<flag>
+    (e.g. --flag expand16)."""
+    from mauv import ops
+    if hasattr(engine, flag):
+        setattr(engine, flag, on)
+    else:
+        getattr(ops, "set_" + flag)(1 if on else 0)   # 1: the library's default routing
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
@@ -33,7 +43,8 @@ def main():
     ap.add_argument("--train", action="store_true")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--flag", default="FOLD",
-                    help="the engine switch the two arms set False / True (e.g. FOLD)")
+                    help="the engine switch the two arms set False / True (e.g. FOLD), or a "
+                         "library routing switch ops.set_<flag> (e.g. expand16)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="--train: trunk precision of the step")
     ap.add_argument("--tiles", type=int, nargs=2, default=None, metavar=("A", "B"),
@@ -52,7 +63,7 @@ def main():
     for r in range(a.rounds):
         order = (False, True) if r % 2 == 0 else (True, False)
         for fold in (order if a.only is None else (bool(a.only),)):
-            setattr(engine, a.flag, fold)
+            _set(a.flag, fold)
             with torch.no_grad(), torch.autocast("cuda"):
                 mc_statistics(model, x, b, s, chunk, chunk=chunk)   # warm-up chunk
                 torch.cuda.synchronize()
@@ -63,7 +74,7 @@ def main():
             outs[fold] = o
             print(f"round {r} fold={int(fold)}: {a.mc * a.batch / res[fold][-1]:.0f} "
                   f"MC-samples/s ({res[fold][-1] * 1e3:.0f} ms)", flush=True)
-    setattr(engine, a.flag, True)
+    _set(a.flag, True)
     for f in (False, True):
         if not res[f]:
             continue
@@ -97,7 +108,7 @@ def train_ab(a):
             if a.tiles:   # arm False = FOLD_MIN_TILES A, arm True = B
                 engine.FOLD, engine.FOLD_MIN_TILES = True, a.tiles[int(fold)]
             else:
-                setattr(engine, a.flag, fold)
+                _set(a.flag, fold)
             for _ in range(2):
                 step()
             torch.cuda.synchronize()
@@ -108,7 +119,7 @@ def train_ab(a):
             res[fold].append((time.perf_counter() - t0) / a.steps)
             print(f"round {r} fold={int(fold)}: {B / res[fold][-1]:.1f} triplets/s "
                   f"({res[fold][-1] * 1e3:.2f} ms/step)", flush=True)
-    setattr(engine, a.flag, True)
+    _set(a.flag, True)
     for f in (False, True):
         if res[f]:
             t = min(res[f])
