@@ -34,7 +34,7 @@ __device__ __forceinline__ u32x4 xload16(__amdgpu_buffer_rsrc_t r, unsigned off)
 // per block).  grid (slots, G * N / NB); block (slot, g * ncg + cg) walks row pairs slot,
 // slot + slots, ... < npairs.
 template <int DT, int K, int WN, bool XBN>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(K == 64 ? 4 : 2)))
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WN == 32 && K <= 128 ? 4 : 2)))
 void conv_expand16(const ConvArgs a, int npairs, int ncg) {
   constexpr int BM = 64, NW = 8, NT = 64 * NW, NI = WN / 32, MI = BM / 32;
   constexpr int KS = K / 16, KQ = K / 8, NVA = BM * KQ / NT;
@@ -141,31 +141,70 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
     const int nval = min(BM, a.M - t * BM);  // may be <= 0: the second half past M
     if (a.st_mean) {
       // row (r & 3) + 8 (r >> 2) + 4 lh + 32 mi of the tile is valid iff (r & 3) + 8 (r >> 2)
-      // < lim - 32 mi: immediates against one per-lane limit (the full tiles skip the test)
-      const bool full = nval >= BM;
-      const int lim = nval - 4 * lh;
+      // < lim - 32 mi: immediates against one per-lane limit
       float s1[NI], m2[NI];
+      if constexpr (K <= 128) {
+        // rows past M hold exact zeros (their A rows were loaded and transformed as 0): the sums
+        // need no mask; on a partial tile those rows are set to the mean before the M2 pass
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) {
-        float sum = 0.f;
+        for (int ni = 0; ni < NI; ++ni) {
+          float sum = 0.f;
 #pragma unroll
-        for (int mi = 0; mi < MI; ++mi) {
-          float p = 0.f;
+          for (int mi = 0; mi < MI; ++mi) {
+            float p = 0.f;
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            p += (full || (r & 3) + 8 * (r >> 2) < lim - 32 * mi) ? acc[mi][ni][r] : 0.f;
-          sum += p + __shfl_xor(p, 32, 64);
-        }
-        s1[ni] = sum / (float)(nval > 0 ? nval : 1);
-        float q = 0.f;
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float d = acc[mi][ni][r] - s1[ni];
-            q += (full || (r & 3) + 8 * (r >> 2) < lim - 32 * mi) ? d * d : 0.f;
+            for (int r = 0; r < 16; ++r) p += acc[mi][ni][r];
+            sum += p + __shfl_xor(p, 32, 64);
           }
-        m2[ni] = q + __shfl_xor(q, 32, 64);
+          s1[ni] = sum / (float)(nval > 0 ? nval : 1);
+        }
+        if (nval < BM) {  // block-uniform
+          const int lim = nval - 4 * lh;
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+              for (int r = 0; r < 16; ++r)
+                if ((r & 3) + 8 * (r >> 2) >= lim - 32 * mi) acc[mi][ni][r] = s1[ni];
+        }
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          float q = 0.f;
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float d = acc[mi][ni][r] - s1[ni];
+              q += d * d;
+            }
+          m2[ni] = q + __shfl_xor(q, 32, 64);
+        }
+      } else {  // measured: the form below runs the K = 256 kernel (255 VGPRs) 1.5x faster
+        const bool full = nval >= BM;
+        const int lim = nval - 4 * lh;
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          float sum = 0.f;
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi) {
+            float p = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              p += (full || (r & 3) + 8 * (r >> 2) < lim - 32 * mi) ? acc[mi][ni][r] : 0.f;
+            sum += p + __shfl_xor(p, 32, 64);
+          }
+          s1[ni] = sum / (float)(nval > 0 ? nval : 1);
+          float q = 0.f;
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float d = acc[mi][ni][r] - s1[ni];
+              q += (full || (r & 3) + 8 * (r >> 2) < lim - 32 * mi) ? d * d : 0.f;
+            }
+          m2[ni] = q + __shfl_xor(q, 32, 64);
+        }
       }
       const float n1 = (float)(nval > 0 ? nval : 0);
       if ((i & 1) == 0) {
@@ -234,7 +273,10 @@ template <int DT>
 static bool expand_dt(const ConvArgs& a, hipStream_t st) {
   switch (a.K) {
     case 64: launch_expand<DT, 64, 32>(a, st); return true;
-    case 128: launch_expand<DT, 128, 64>(a, st); return true;
+    case 128:
+      if (g_expand16 == 3) launch_expand<DT, 128, 32>(a, st);
+      else launch_expand<DT, 128, 64>(a, st);
+      return true;
     case 256: launch_expand<DT, 256, 64>(a, st); return true;
   }
   return false;
@@ -277,7 +319,7 @@ bool conv_expand16_launch(int dt, const ConvArgs& a, hipStream_t st) {
 // covered shape, 0 none (conv_pipe16), -1 query.  Returns the previous mode.
 MAUV_API int mauv_set_expand16(int mode) {
   const int prev = mauv::g_expand16;
-  if (mode >= 0 && mode <= 2) mauv::g_expand16 = mode;
+  if (mode >= 0 && mode <= 3) mauv::g_expand16 = mode;
   else if (mode != -1) {
     mauv::set_error("set_expand16: mode 0, 1, 2 or -1 (query)");
     return mauv::kErrArg;

@@ -23,7 +23,10 @@ def main():
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--arms", default="0,2", help="mauv_set_expand16 modes to compare "
+                    "(0: conv_pipe16, 2: every covered shape through conv_expand16)")
     a = ap.parse_args()
+    ARMS = [int(v) for v in a.arms.split(",")]
     dt = {"bf16": torch.bfloat16, "f16": torch.float16}[a.dtype]
     G, B = a.G, a.B
     torch.manual_seed(0)
@@ -33,7 +36,7 @@ def main():
             if R == 1 and st == 1 and Cin in (64, 128, 256) and Cout == 4 * Cin:
                 shapes.setdefault((Cin, Cout, H, name.endswith("c3")), []).append(f"{trunk}:{name}")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    res = {k: {0: [], 1: []} for k in shapes}
+    res = {k: {arm: [] for arm in ARMS} for k in shapes}
     for rnd in range(a.rounds):
         for key in shapes:
             Cin, Cout, H, xb = key
@@ -45,9 +48,9 @@ def main():
             x_bn = (torch.rand(G, Cin, device="cuda") + 0.5,
                     torch.randn(G, Cin, device="cuda") * 0.1, 1) if xb else None
             outs = {}
-            for arm in ((0, 1) if rnd % 2 == 0 else (1, 0)):
+            for arm in (ARMS if rnd % 2 == 0 else ARMS[::-1]):
                 y = torch.empty(G, B, H, H, Cout, device="cuda", dtype=dt)
-                prev = ops.set_expand16(2 * arm)   # 0: conv_pipe16, 2: every covered shape
+                prev = ops.set_expand16(arm)
                 try:
                     fn = lambda: ops.conv2d_fwd(x, w, y, G, B, H, H, Cin, Cout, 1, 1, 0,
                                                 x_bn=x_bn, stats=stats)
@@ -61,22 +64,21 @@ def main():
                     ops.set_expand16(prev)
                 res[key][arm].append(e0.elapsed_time(e1) / a.reps)
                 outs[arm] = y
-            if not torch.equal(outs[0], outs[1]):
+            if any(not torch.equal(outs[ARMS[0]], outs[arm]) for arm in ARMS):
                 print(f"OUTPUT DIFFERS {key}", flush=True)
             del x, w, outs
-    tot = {0: 0.0, 1: 0.0}
-    print(f"{'Cin,Cout,H,xbn':22s} {'n':>3s} {'pipe16 ms':>10s} {'expand ms':>10s} {'GB/s':>7s} "
-          f"{'GB/s e':>7s} {'speedup':>8s}  layers")
-    for key, v in sorted(shapes.items(), key=lambda kv: -min(res[kv[0]][0])):
+    tot = {arm: 0.0 for arm in ARMS}
+    print(f"{'Cin,Cout,H,xbn':22s} {'n':>3s} " + " ".join(f"{'ms@' + str(x):>9s}" for x in ARMS) +
+          " " + " ".join(f"{'GB/s@' + str(x):>9s}" for x in ARMS) + "  layers")
+    for key, v in sorted(shapes.items(), key=lambda kv: -min(res[kv[0]][ARMS[0]])):
         Cin, Cout, H, xb = key
         nb = 2 * G * B * H * H * (Cin + Cout)
-        t0, t1 = min(res[key][0]), min(res[key][1])
-        tot[0] += t0 * len(v)
-        tot[1] += t1 * len(v)
-        print(f"{str(key):22s} {len(v):3d} {t0:10.3f} {t1:10.3f} {nb / t0 / 1e6:7.0f} "
-              f"{nb / t1 / 1e6:7.0f} {t0 / t1:8.3f}  {' '.join(v[:4])}")
-    print(f"TOTAL (x occurrences): pipe16 {tot[0]:.2f} ms, expand {tot[1]:.2f} ms "
-          f"({tot[0] / tot[1]:.3f}x)")
+        t = {arm: min(res[key][arm]) for arm in ARMS}
+        for arm in ARMS:
+            tot[arm] += t[arm] * len(v)
+        print(f"{str(key):22s} {len(v):3d} " + " ".join(f"{t[x]:9.3f}" for x in ARMS) + " " +
+              " ".join(f"{nb / t[x] / 1e6:9.0f}" for x in ARMS) + f"  {' '.join(v[:4])}")
+    print("TOTAL (x occurrences): " + ", ".join(f"mode {x} {tot[x]:.2f} ms" for x in ARMS))
 
 
 if __name__ == "__main__":
