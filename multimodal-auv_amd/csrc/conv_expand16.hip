@@ -282,18 +282,13 @@ static bool expand_dt(const ConvArgs& a, hipStream_t st) {
   return false;
 }
 
-// where it measured faster than the implicit GEMM (tools/expand_ab.py):
-// K = 128 (1.12-1.21x); K = 256 only with >= 8 row pairs per block (f16 inference chunk 1.18-1.19x,
-// the bf16 training slice's 2-3 pairs per block 0.85-0.93x: the 128-register weight fragments and
-// the prologue are not amortised); K = 64 never (0.85-0.91x: eight MFMAs per tile, two blocks per
-// CU against conv_pipe16's four)
-static bool expand_wins(const ConvArgs& a) {
-  if (a.K == 128) return true;
-  if (a.K != 256) return false;
-  const int ncg = a.N / 512, units = a.G * ncg, npairs = (a.M + 127) / 128;
-  const int slots = (2 * 256 + units - 1) / units;
-  return npairs >= 8 * slots;
-}
+// where it measured faster than the implicit GEMM (tools/expand_ab.py): K = 128
+// (1.22-1.32x).  The rule depends on the shape only, never on the MC group count: its BN
+// statistics (Chan-merged 64-row halves) differ from the implicit GEMM's in the last bits, and an
+// MC chunk size must not change a sample's result (test_configs4_gpu: chunking is exact) — so
+// K = 256, faster only at inference-chunk sizes (1.19x at G = 20, 0.84-0.95x at the training
+// slice), stays on the implicit GEMM; K = 64 never wins (0.86-0.96x)
+static bool expand_wins(const ConvArgs& a) { return a.K == 128; }
 
 bool conv_expand16_launch(int dt, const ConvArgs& a, hipStream_t st) {
   if (!g_expand16) return false;
