@@ -55,6 +55,20 @@ __device__ __forceinline__ u32x4 bn_relu8(u32x4 v, const floatx8& sc, const floa
   return o;
 }
 
+// Chan et al.'s merge of two row sets' (count, mean, M2) into the first: the 16-bit forwards'
+// statistics partials combine their 64-row halves with exactly these operations
+__device__ __forceinline__ void stats_merge(float na, float ma, float qa, float nb, float mb,
+                                            float qb, float& mean, float& m2) {
+  if (nb > 0.f) {
+    const float n = na + nb, d = mb - ma;
+    mean = __builtin_fmaf(d, nb / n, ma);
+    m2 = __builtin_fmaf(d * d, na * nb / n, qa + qb);
+  } else {
+    mean = ma;
+    m2 = qa;
+  }
+}
+
 template <int MODE, int DT, int BM, int BN, int MI, int NI, int WGM, int WGN, int SCRATCH,
           bool BP = false>
 __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI][NI], void* smem,
@@ -64,15 +78,15 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
   const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
   float* red = (float*)smem;  // LDS is free: the main loop ended with a barrier
   if (MODE == FWD && a.st_mean) {
-    // per-tile BN statistics of y from the fp32 accumulators (tile mean, then M2 around it),
-    // one partial per SR = min(BM, 128) rows (the granularity the host sizes them with).  Each
-    // 32-row accumulator group (mi) of each wave is summed on its own and the groups of a
-    // partial are added in row order — the same float operations whatever the tile's wave
-    // layout (a 128 x 128 tile of 32-row waves, a 256-row tile of 128-row waves), so every
-    // kernel that shares this epilogue writes bit-identical statistics for the same rows
+    // BN statistics of y from the fp32 accumulators, one partial per SR = min(BM, 128) rows (the
+    // granularity the host sizes them with), in the canonical form every 16-bit forward kernel
+    // writes (conv_expand16 included, so a shape's statistics do not depend on the kernel that
+    // ran it): each 32-row group summed on its own (lane order, then across the wave halves),
+    // per 64-row half the mean of its two group sums and M2 around that mean (fma per row),
+    // the halves of a partial merged by Chan's formula (stats_merge)
     constexpr int SR = BM > 128 ? 128 : BM, SUB = BM / SR;
     constexpr int VW = WGM * MI, VPS = VW / SUB;  // 32-row groups: of the tile, of a partial
-    static_assert(VW % SUB == 0, "whole 32-row groups per statistics sub-tile");
+    static_assert(VW % SUB == 0 && VPS % 2 == 0, "whole 64-row halves per statistics partial");
     const int tcol = wn * WN + li;
     float s1[MI][NI], s2[MI][NI], mean[MI][NI];
 #pragma unroll
@@ -97,15 +111,12 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
     __syncthreads();
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
-      const int vsub = (wm * MI + mi) / VPS;
-      const int nvalid = min(SR, a.M - (m0 + vsub * SR));
+      const int g0 = (wm * MI + mi) & ~1;  // the first group of this group's 64-row half
+      const int nh = max(0, min(64, a.M - (m0 + 32 * g0)));
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) {
-        float t = 0.f;
-#pragma unroll
-        for (int w = 0; w < VPS; ++w) t += red[(vsub * VPS + w) * BN + tcol + ni * 32];
-        mean[mi][ni] = t / (float)(nvalid > 0 ? nvalid : 1);
-      }
+      for (int ni = 0; ni < NI; ++ni)
+        mean[mi][ni] = (red[g0 * BN + tcol + ni * 32] + red[(g0 + 1) * BN + tcol + ni * 32]) /
+                       (float)(nh > 0 ? nh : 1);
     }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
@@ -116,7 +127,7 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
           const int row = m0 + wm * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           if (row < a.M) {
             const float d = acc[mi][ni][r] - mean[mi][ni];
-            s2[mi][ni] += d * d;
+            s2[mi][ni] = __builtin_fmaf(d, d, s2[mi][ni]);
           }
         }
         s2[mi][ni] += __shfl_xor(s2[mi][ni], 32, 64);
@@ -131,18 +142,23 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
     __syncthreads();
     const int col = tid % BN, sb = tid / BN, nv = min(SR, a.M - (m0 + sb * SR));
     if (tid < SUB * BN && n0 + col < a.N && nv > 0) {
-      float t1 = 0.f, t2 = 0.f;
+      float hn[2], hm[2], hq[2];
 #pragma unroll
-      for (int w = 0; w < VPS; ++w) {
-        t1 += red[(sb * VPS + w) * BN + col];
-        t2 += red[VW * BN + (sb * VPS + w) * BN + col];
+      for (int h = 0; h < VPS / 2; ++h) {
+        const int gA = sb * VPS + 2 * h;
+        const int nh = max(0, min(64, a.M - (m0 + 32 * gA)));
+        hn[h] = (float)nh;
+        hm[h] = (red[gA * BN + col] + red[(gA + 1) * BN + col]) / (float)(nh > 0 ? nh : 1);
+        hq[h] = red[VW * BN + gA * BN + col] + red[VW * BN + (gA + 1) * BN + col];
       }
+      float mu = hm[0], m2 = hq[0];
+      if constexpr (VPS / 2 == 2) stats_merge(hn[0], hm[0], hq[0], hn[1], hm[1], hq[1], mu, m2);
       const int mt = m0 / SR + sb;
       const int cn = n0 + col;
       const int gc = a.cpg ? cn / a.cpg : g, cc = a.cpg ? cn % a.cpg : cn;
       const long long so = ((long long)gc * a.st_nblk + a.st_base + mt) * (a.cpg ? a.cpg : a.N) + cc;
-      a.st_mean[so] = t1 / (float)nv;
-      a.st_m2[so] = t2;
+      a.st_mean[so] = mu;
+      a.st_m2[so] = m2;
       if (cc == 0) a.st_cnt[(long long)gc * a.st_nblk + a.st_base + mt] = (float)nv;
     }
     __syncthreads();  // red is overwritten by the staged store below

@@ -12,9 +12,10 @@
 // other is multiplied, each wave reads 2 A fragments per 16-deep k-step for 2 x WN/32 MFMAs
 // (0.5-1 read per MFMA), and the epilogue parks the wave's 64 x WN tile as 16-bit words in a
 // wave-private LDS region and stores 16-byte rows.  Outputs are bit-identical to conv_pipe16
-// (same MFMA chain over k, same rounding); the BN statistics are one partial per 128 rows as
-// the host sizes them (mauv_conv2d_fwd_stat_blocks), each the pair's two 64-row partials (tile
-// mean, M2 around it) merged by Chan's formula.
+// (same MFMA chain over k, same rounding), and so are the BN statistics: one partial per 128
+// rows as the host sizes them (mauv_conv2d_fwd_stat_blocks), in epilogue16's canonical form —
+// each 64-row tile's half partial (32-row group sums, the half's mean, M2 around it) merged
+// with the pair's other half by stats_merge.
 #include "conv_common.h"
 #include "conv_epi16.h"
 
@@ -41,7 +42,7 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
   constexpr int RLD = K + 8, A_SZ = BM * RLD;  // A row image [64][K + 8] (u16), two of them
   constexpr int PLD = WN + 8, P_SZ = BM * PLD;  // a wave's parked output tile [64][WN + 8]
   constexpr int CPW = BM * WN / 8 / 64;         // 16-byte output chunks per lane per tile
-  static_assert(NVA >= 1 && NT % KQ == 0 && CPW >= 1, "tile geometry");
+  static_assert(NVA >= 1 && NT % KQ == 0 && CPW >= 1 && MI == 2, "tile geometry");
   constexpr int XS = XBN ? 2 * K : 0;  // the pending BN's scale / shift (floats)
   __shared__ __attribute__((aligned(16))) u16 smem[2 * A_SZ + NW * P_SZ + 2 * XS];
   float* xbn = (float*)(smem + 2 * A_SZ + NW * P_SZ);
@@ -137,26 +138,26 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
       if (i + 2 < ntl) load_a(tile_of(i + 2));
     }
 
-    // ---- BN statistics: 64-row partial per column, merged with the pair's other half ----
+    // ---- BN statistics: the 64-row half's partial (epilogue16's canonical form: 32-row group
+    // sums, the half's mean, M2 per group around it), merged with the pair's other half ----
     const int nval = min(BM, a.M - t * BM);  // may be <= 0: the second half past M
     if (a.st_mean) {
-      // row (r & 3) + 8 (r >> 2) + 4 lh + 32 mi of the tile is valid iff (r & 3) + 8 (r >> 2)
-      // < lim - 32 mi: immediates against one per-lane limit
       float s1[NI], m2[NI];
       if constexpr (K <= 128) {
-        // rows past M hold exact zeros (their A rows were loaded and transformed as 0): the sums
-        // need no mask; on a partial tile those rows are set to the mean before the M2 pass
+        // rows past M hold exact zeros (their A rows were loaded and transformed as 0): the
+        // sums need no mask; on a partial tile those rows are set to the mean before the M2
+        // pass (each then adds an exact 0)
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
-          float sum = 0.f;
+          float sg[MI];
 #pragma unroll
           for (int mi = 0; mi < MI; ++mi) {
             float p = 0.f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) p += acc[mi][ni][r];
-            sum += p + __shfl_xor(p, 32, 64);
+            sg[mi] = p + __shfl_xor(p, 32, 64);
           }
-          s1[ni] = sum / (float)(nval > 0 ? nval : 1);
+          s1[ni] = (sg[0] + sg[1]) / (float)(nval > 0 ? nval : 1);
         }
         if (nval < BM) {  // block-uniform
           const int lim = nval - 4 * lh;
@@ -170,40 +171,45 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
         }
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
-          float q = 0.f;
+          float qg[MI];
 #pragma unroll
-          for (int mi = 0; mi < MI; ++mi)
+          for (int mi = 0; mi < MI; ++mi) {
+            float q = 0.f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const float d = acc[mi][ni][r] - s1[ni];
-              q += d * d;
+              q = __builtin_fmaf(d, d, q);
             }
-          m2[ni] = q + __shfl_xor(q, 32, 64);
+            qg[mi] = q + __shfl_xor(q, 32, 64);
+          }
+          m2[ni] = qg[0] + qg[1];
         }
-      } else {  // measured: the form below runs the K = 256 kernel (255 VGPRs) 1.5x faster
+      } else {  // measured: the masked form runs the K = 256 kernel (255 VGPRs) 1.5x faster
         const bool full = nval >= BM;
         const int lim = nval - 4 * lh;
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
-          float sum = 0.f;
+          float sg[MI], qg[MI];
 #pragma unroll
           for (int mi = 0; mi < MI; ++mi) {
             float p = 0.f;
 #pragma unroll
             for (int r = 0; r < 16; ++r)
               p += (full || (r & 3) + 8 * (r >> 2) < lim - 32 * mi) ? acc[mi][ni][r] : 0.f;
-            sum += p + __shfl_xor(p, 32, 64);
+            sg[mi] = p + __shfl_xor(p, 32, 64);
           }
-          s1[ni] = sum / (float)(nval > 0 ? nval : 1);
-          float q = 0.f;
+          s1[ni] = (sg[0] + sg[1]) / (float)(nval > 0 ? nval : 1);
 #pragma unroll
-          for (int mi = 0; mi < MI; ++mi)
+          for (int mi = 0; mi < MI; ++mi) {
+            float q = 0.f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const float d = acc[mi][ni][r] - s1[ni];
-              q += (full || (r & 3) + 8 * (r >> 2) < lim - 32 * mi) ? d * d : 0.f;
+              q = (full || (r & 3) + 8 * (r >> 2) < lim - 32 * mi) ? __builtin_fmaf(d, d, q) : q;
             }
-          m2[ni] = q + __shfl_xor(q, 32, 64);
+            qg[mi] = q + __shfl_xor(q, 32, 64);
+          }
+          m2[ni] = qg[0] + qg[1];
         }
       }
       const float n1 = (float)(nval > 0 ? nval : 0);
@@ -212,23 +218,18 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) { hmean[ni] = s1[ni]; hm2[ni] = m2[ni]; }
       } else {
-        const float n = hn + n1;
         const int pr = t >> 1;
         if (lh == 0) {
 #pragma unroll
           for (int ni = 0; ni < NI; ++ni) {
-            float mean = hmean[ni], M2 = hm2[ni];
-            if (n1 > 0.f) {  // Chan et al.: merge (hn, hmean, hm2) with (n1, s1, m2)
-              const float d = s1[ni] - hmean[ni];
-              mean = hmean[ni] + d * (n1 / n);
-              M2 = hm2[ni] + m2[ni] + d * d * (hn * n1 / n);
-            }
+            float mean, M2;
+            stats_merge(hn, hmean[ni], hm2[ni], n1, s1[ni], m2[ni], mean, M2);
             const long long so = ((long long)g * a.st_nblk + a.st_base + pr) * a.N + nw0 + ni * 32 + li;
             a.st_mean[so] = mean;
             a.st_m2[so] = M2;
           }
         }
-        if (tid == 0 && cg == 0) a.st_cnt[(long long)g * a.st_nblk + a.st_base + pr] = n;
+        if (tid == 0 && cg == 0) a.st_cnt[(long long)g * a.st_nblk + a.st_base + pr] = hn + n1;
       }
     }
 
@@ -283,12 +284,18 @@ static bool expand_dt(const ConvArgs& a, hipStream_t st) {
 }
 
 // where it measured faster than the implicit GEMM (tools/expand_ab.py): K = 128
-// (1.22-1.32x).  The rule depends on the shape only, never on the MC group count: its BN
-// statistics (Chan-merged 64-row halves) differ from the implicit GEMM's in the last bits, and an
-// MC chunk size must not change a sample's result (test_configs4_gpu: chunking is exact) — so
-// K = 256, faster only at inference-chunk sizes (1.19x at G = 20, 0.84-0.95x at the training
-// slice), stays on the implicit GEMM; K = 64 never wins (0.86-0.96x)
-static bool expand_wins(const ConvArgs& a) { return a.K == 128; }
+// (1.22-1.32x); K = 256 with >= 8 row pairs per block (1.19-1.20x at the inference chunk; the
+// training slice's 2-3 pairs per block do not amortise the 128-register weight fragments:
+// 0.84-0.95x); K = 64 never (0.86-0.96x).  Outputs AND statistics are bit-identical to the
+// implicit GEMM's (epilogue16's canonical statistics), so a rule that depends on the MC group
+// count cannot change a sample's result with the chunk size
+static bool expand_wins(const ConvArgs& a) {
+  if (a.K == 128) return true;
+  if (a.K != 256) return false;
+  const int ncg = a.N / 512, units = a.G * ncg, npairs = (a.M + 127) / 128;
+  const int slots = (2 * 256 + units - 1) / units;
+  return npairs >= 8 * slots;
+}
 
 bool conv_expand16_launch(int dt, const ConvArgs& a, hipStream_t st) {
   if (!g_expand16) return false;
