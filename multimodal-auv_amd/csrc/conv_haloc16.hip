@@ -1,0 +1,264 @@
+// 16-bit 3x3 / stride-1 / pad-1 forwards over C = 128 / 256 / 512 channels (the conv2 of the
+// layer-2..4 bottlenecks, pending bn1 + ReLU on load) through an LDS image of the input rows,
+// one 64-channel chunk at a time — conv_halo16.hip (C = 64) generalised.
+//
+// The implicit GEMM stages a tap-shifted A tile per (tap, channel chunk): every input pixel is
+// loaded and BN-transformed nine times.  Here a block of 128 consecutive output pixels x 128
+// output channels walks the input channels in chunks of 64: per chunk it stages, once, the
+// input rows its pixels read (+ one halo row each side, a zero column at either end; the
+// pending BN applied by bn_relu8 on the way in), then the nine taps' 128 x 64 weight slices
+// (double-buffered, the next slice in registers one tap ahead); the next chunk's rows are in
+// registers while the current chunk's taps run.  Accumulation order is (chunk, tap, k): it is
+// not the implicit GEMM's (tap, chunk, k), so outputs agree with it to fp32 summation order
+// (routing is by shape only, mauv_set_haloc16); the statistics epilogue is epilogue16's.
+#include "conv_common.h"
+#include "conv_epi16.h"
+
+namespace mauv {
+
+namespace {
+
+constexpr int kHc = 72;        // LDS pitch of a weight row, 16-bit words (144 B)
+constexpr int kHcPx = 256;     // LDS pixel slots of one 64-channel image chunk (32 KB)
+constexpr int kMaxHcC = 512;   // channels
+constexpr unsigned kOOBc = 0x7ffffff0u;
+// 128-B pixels (64 channels), 16-byte chunk c of pixel p in slot c ^ ((p >> 1) & 7): every
+// ds_read_b128 fragment conflict-free for any first pixel (conv_halo16.hip's layout)
+__device__ __forceinline__ int cslot(int p, int c) { return p * 64 + 8 * (c ^ ((p >> 1) & 7)); }
+__device__ __forceinline__ u32x4 cload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
+}  // namespace
+
+// MI = 1: 4 x 2 waves of 32 x 64 over a 128-pixel x 128-channel tile (512 threads, the default);
+// MI = 2: 2 x 2 waves of 64 x 64 (256 threads: one A and one B fragment read per MFMA instead of
+// 1.5, but half the waves to hide LDS and barrier latency: 3-4 % slower on every routed shape,
+// profiles/round5/haloc16_modes_ab_*.txt).  Two blocks per CU either way.
+template <int DT, bool XBN, int MI>
+__global__ __launch_bounds__(256 * (3 - MI)) __attribute__((amdgpu_waves_per_eu(6 - 2 * MI)))
+void conv_haloc16(const ConvArgs a) {
+  constexpr int WGM = 4 / MI, WGN = 2, NT = 64 * WGM * WGN, BM = 128, BN = 128, WN = 64, NI = 2;
+  constexpr int WM = 32 * MI;
+  constexpr int IMG = kHcPx * 64, WB = BN * kHc;  // 16-bit words
+  constexpr int NCH = kHcPx * 8 / NT;               // 16-byte image chunks per thread
+  constexpr int NWJ = BN * 8 / NT;                  // 16-byte weight chunks per thread and tap
+  __shared__ __attribute__((aligned(16))) u16 smem[IMG + 2 * WB];
+  __shared__ float xbn[2 * kMaxHcC];
+  u16* img = smem;
+  u16* wbuf = smem + IMG;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
+  int m0, n0, g;
+  conv_block_tile<BM, BN>(a, m0, n0, g);
+  const int C = a.Cin, W = a.W, H = a.H, W2 = W + 2, BH = a.B * H;
+  const int R0 = __builtin_amdgcn_readfirstlane(m0 / W);
+  const int R1 = __builtin_amdgcn_readfirstlane((min(a.M, m0 + BM) - 1) / W);
+  const int nhr = R1 - R0 + 3;  // LDS rows incl. the two halo rows (host-checked: fits kHcPx)
+
+  const u16* xg = (const u16*)a.x + (long long)g * a.xs_g;
+  const u16* wg = (const u16*)a.w + (long long)g * a.ws_g;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)xg, (short)0, (int)((long long)a.B * a.xs_b * 2), 0x00020000);
+  if constexpr (XBN) {
+    for (int i = tid; i < C; i += NT) {
+      xbn[i] = a.xsc[g * C + i];
+      xbn[kMaxHcC + i] = a.xsh[g * C + i];
+    }
+  }
+  const unsigned rfloor = a.xrelu ? 0u : 0x80008000u;
+
+  // ---- one 64-channel chunk of the input rows: chunk q = (LDS row hr, column iw, cq) ----
+  const unsigned nch = (unsigned)(nhr * W * 8);
+  u32x4 v[NCH];
+  auto load_img = [&](int cc) {
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const unsigned q = (unsigned)(tid + NT * j);
+      const unsigned hr = udiv16(q, a.m16_w), rem = q - hr * (unsigned)(W * 8);
+      const int iw = (int)(rem >> 3), cq = (int)(rem & 7);
+      const int gr = R0 - 1 + (int)hr;  // flattened image row b * H + ih
+      const unsigned b = udiv16((unsigned)gr, a.m16_h);
+      const int ih = gr - (int)b * H;
+      const bool ok = (q < nch) & ((unsigned)gr < (unsigned)BH);
+      const unsigned off = (unsigned)((b * a.xs_b + ih * a.xs_h + iw * a.xs_w + 64 * cc + 8 * cq) * 2);
+      v[j] = cload(rx, sel_off(ok, off, kOOBc));
+    }
+  };
+  auto store_img = [&](int cc) {
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const unsigned q = (unsigned)(tid + NT * j);
+      if (q < nch) {
+        const unsigned hr = udiv16(q, a.m16_w), rem = q - hr * (unsigned)(W * 8);
+        const int iw = (int)(rem >> 3), cq = (int)(rem & 7);
+        u32x4 t = v[j];
+        if constexpr (XBN) {
+          const int gr = R0 - 1 + (int)hr;
+          const int ch = 64 * cc + 8 * cq;
+          t = bn_relu8<DT>(t, ldf8(xbn + ch), ldf8(xbn + kMaxHcC + ch), rfloor,
+                           (unsigned)gr < (unsigned)BH);
+        }
+        *(u32x4*)(img + cslot((int)hr * W2 + iw + 1, cq)) = t;
+      }
+    }
+  };
+  // weight slice of (chunk cc, tap t): rows n0 + (tid >> 3) + NT / 8 j of w[n][r][s][c], channels
+  // 64 cc + 8 (tid & 7) .. + 7, as a row image [128][kHc]
+  const int wr = tid >> 3, wq = tid & 7;
+  u32x4 wv[NWJ];
+  auto load_w = [&](int cc, int t) {
+#pragma unroll
+    for (int j = 0; j < NWJ; ++j) {
+      const int n = n0 + wr + NT / 8 * j;
+      wv[j] = n < a.N ? *(const u32x4*)(wg + (long long)n * 9 * C + t * C + 64 * cc + 8 * wq)
+                      : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store_w = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < NWJ; ++j)
+      *(u32x4*)(wbuf + buf * WB + (wr + NT / 8 * j) * kHc + 8 * wq) = wv[j];
+  };
+
+  // the zero columns 0 and W + 1 of every LDS row (no chunk writes them)
+  for (int q = tid; q < nhr * 16; q += NT) {
+    const int hr = q >> 4, side = (q >> 3) & 1, cq = q & 7;
+    *(u32x4*)(img + cslot(hr * W2 + side * (W + 1), cq)) = u32x4{0u, 0u, 0u, 0u};
+  }
+  load_img(0);
+  load_w(0, 0);
+  if constexpr (XBN) __syncthreads();  // xbn staged
+  store_img(0);
+  store_w(0);
+  const int nchunk = C / 64;
+  if (nchunk > 1) load_img(1);
+  load_w(0, 1);
+
+  // ---- this lane's output pixels (row li of each of its wave's 32-pixel fragments) ----
+  int hb[MI], ohs[MI];
+  bool mok[MI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi) {
+    const int m = m0 + wm * WM + mi * 32 + li;
+    mok[mi] = m < a.M;
+    const int gr_m = mok[mi] ? m / W : R0;
+    const int ow = mok[mi] ? m - gr_m * W : 0;
+    ohs[mi] = gr_m - (gr_m / H) * H;
+    hb[mi] = (gr_m - R0) * W2 + ow;  // LDS pixel of tap (0, 0)
+  }
+  __syncthreads();
+
+  floatx16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  int wb = 0;  // weight buffer of the current tap
+  for (int cc = 0; cc < nchunk; ++cc) {
+    // unrolled nine times, the taps' address and prefetch registers spill (MI = 1 at 128 VGPRs,
+    // MI = 2 at 256)
+#pragma unroll (MI == 1 ? 1 : 3)
+    for (int t = 0; t < 9; ++t) {
+      const int r = t / 3, s = t % 3;
+      const u16* wcur = wbuf + wb * WB;
+      const u16* ap[MI];
+      int sw[MI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const int pix = (mok[mi] & ((unsigned)(ohs[mi] + r - 1) < (unsigned)H)) ? hb[mi] + r * W2 + s
+                                                                                : 0;
+        ap[mi] = img + pix * 64;
+        sw[mi] = (pix >> 1) & 7;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        u32x4 af[MI], bq[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) af[mi] = *(const u32x4*)(ap[mi] + 8 * ((2 * ks + lh) ^ sw[mi]));
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) bq[ni] = row_frag_ld<kHc>(wcur, wn * WN + ni * 32, ks, li, lh);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = H16<DT>::mfma(af[mi], bq[ni], acc[mi][ni]);
+      }
+      // the next tap's slice (chunk cc, tap t + 1; or chunk cc + 1, tap 0) into the other buffer
+      const bool more = t < 8 || cc + 1 < nchunk;
+      if (more) store_w(wb ^ 1);
+      if (t < 8) {
+        if (t + 2 < 9) load_w(cc, t + 2);
+        else if (cc + 1 < nchunk) load_w(cc + 1, 0);
+      } else if (cc + 1 < nchunk) {
+        load_w(cc + 1, 1);
+      }
+      if (t == 8 && cc + 1 < nchunk) {
+        __syncthreads();  // every wave is done with this chunk's image
+        store_img(cc + 1);
+        if (cc + 2 < nchunk) load_img(cc + 2);
+      }
+      __syncthreads();
+      wb ^= 1;
+    }
+  }
+
+  epilogue16<FWD, DT, BM, BN, MI, NI, WGM, WGN, (IMG + 2 * WB) * 2>(a, acc, smem, m0, n0, g);
+}
+
+// rows of the flattened B*H image rows a 128-pixel tile touches, at most
+static int haloc_rows(int W) { return 128 % W == 0 ? 128 / W : 128 / W + 2; }
+
+// mauv_set_haloc16: 1 (default) routes the covered forwards here (32 x 64 wave tiles, 512
+// threads), 2 the same with 64 x 64 wave tiles (256 threads; measured 3-4 % slower), 0 keeps the
+// implicit GEMM
+int g_haloc16 = 1;
+
+// true: launched
+bool conv_haloc16_launch(int dt, const ConvArgs& a0, hipStream_t st) {
+  if (!g_haloc16) return false;
+  if (a0.R != 3 || a0.S != 3 || a0.stride != 1 || a0.pad != 1 || a0.cpg || a0.Ho != a0.H ||
+      a0.Wo != a0.W || a0.Cin % 64 || a0.Cin < 128 || a0.Cin > kMaxHcC || a0.N % 128 ||
+      a0.W > 512 || a0.H > 4096 || (long long)a0.B * a0.H >= (1 << 17))
+    return false;
+  if (a0.xs_c != 1 || a0.xs_w % 8 || a0.xs_h % 8 || a0.xs_b % 8 || a0.xs_g % 8) return false;
+  if ((long long)a0.B * a0.xs_b * 2 > 0x7fff0000LL) return false;  // 31-bit buffer offsets
+  if ((haloc_rows(a0.W) + 2) * (a0.W + 2) > kHcPx) return false;
+  ConvArgs a = a0;
+  a.m16_w = m16_div((unsigned)(a.W * 8));
+  a.m16_h = m16_div((unsigned)a.H);
+  const dim3 grid(ceil_div(a.M, 128) * (a.N / 128), a.G);
+  const bool xb = a.xsc != nullptr;
+#define HC_GO(D, X, MI_) \
+  hipLaunchKernelGGL((conv_haloc16<D, X, MI_>), grid, dim3(256 * (3 - MI_)), 0, st, a)
+#define HC_MI(D, X) \
+  if (g_haloc16 == 2) HC_GO(D, X, 2); else HC_GO(D, X, 1)
+  if (dt == DT_BF16) {
+    if (xb) HC_MI(DT_BF16, true);
+    else HC_MI(DT_BF16, false);
+  } else {
+    if (xb) HC_MI(DT_F16, true);
+    else HC_MI(DT_F16, false);
+  }
+#undef HC_MI
+#undef HC_GO
+  return true;
+}
+
+}  // namespace mauv
+
+// Route 16-bit 3x3 / stride-1 forwards over 128-512 channels through conv_haloc16 (1, default:
+// 32 x 64 wave tiles; 2: 64 x 64 wave tiles) or the implicit GEMM (0); -1 queries.  Returns the
+// previous setting.
+MAUV_API int mauv_set_haloc16(int on) {
+  const int prev = mauv::g_haloc16;
+  if (on >= 0 && on <= 2) mauv::g_haloc16 = on;
+  else if (on != -1) {
+    mauv::set_error("set_haloc16: 0, 1, 2 or -1 (query)");
+    return mauv::kErrArg;
+  }
+  return prev;
+}

@@ -36,6 +36,7 @@ SIGNATURES = {
     "mauv_set_big16": [I, I],
     "mauv_set_dma16": [I, I],
     "mauv_set_expand16": [I],
+    "mauv_set_haloc16": [I],
     # conv_gemm16.hip
     "mauv_conv2d_fwd_h16": [I, P, P, P, P, I, P, P] + [I] * 10 + [P, P, P, P],
     "mauv_conv2d_fwd_fold_h16": [I] + [P] * 10 + [I] * 6 + [P, P, P, P],

@@ -137,6 +137,15 @@ def set_expand16(mode=None):
     return rc
 
 
+def set_haloc16(mode=None):
+    """Route 16-bit 3x3 / stride-1 forwards over 128-512 channels through the chunked LDS
+    row-image kernel (conv_haloc16.hip): 1 / True (default, 32 x 64 wave tiles), 2 (64 x 64 wave
+    tiles), 0 / False (the implicit GEMM), None keep.  Returns the previous mode."""
+    rc = lib.mauv_set_haloc16(-1 if mode is None else int(mode))
+    check(0 if rc >= 0 else rc, "set_haloc16")
+    return rc
+
+
 def set_dma16(mode=None, min_k=0):
     """Route 16-bit forwards through the 128 x 128 LDS-DMA tiles: 1 (default) where they measured
     faster, 2 (or True) every forward they cover with K >= min_k, 0 (or False) none; None /
