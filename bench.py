@@ -525,8 +525,9 @@ def main():
         if not args.no_roofline:
             bf16["roofline"] = roofline_step(
                 step, peak=BF16_MFMA_PEAK_TF, traffic="bf16", suffix="_bfloat16",
-                kernel="16-bit convs of one step (conv_pipe16 / conv_halo16 / conv_big16: "
-                       "implicit-GEMM fwd+dgrad+wgrad, stems as one GEMM over shared im2col rows); "
+                kernel="16-bit convs of one step (conv_pipe16 / conv_halo16 / conv_haloc16 / "
+                       "conv_big16 / conv_expand16: implicit-GEMM fwd+dgrad+wgrad, stems as "
+                       "one GEMM over shared im2col rows); "
                        "the conv1 launches that also form the previous block output: 'fold'")
         set_precision(model.module if world > 1 else model,
                       torch.bfloat16 if args.dtype == "bf16" else None)

@@ -19,10 +19,10 @@ def family(name):
         return "conv_fold16"     # conv1 forming the previous block output (its own family)
     if "conv_gemm_f32" in name or "conv_split_f32" in name:
         return "conv_f32"        # the fp32 conv family: split kernels + stems on conv_gemm_f32
-    if any(k in name for k in ("conv_gemm_h16", "conv_pipe16", "conv_halo16", "conv_big16",
-                               "conv_expand16")):
-        return "conv_h16"        # the 16-bit conv family: pipelined, halo, 256-row, expansion
-                                 # + fallback shapes
+    if any(k in name for k in ("conv_gemm_h16", "conv_pipe16", "conv_halo16", "conv_haloc16",
+                               "conv_big16", "conv_expand16")):
+        return "conv_h16"        # the 16-bit conv family: pipelined, halo (64 and 128-512
+                                 # channels), 256-row, expansion + fallback shapes
     return name.split("(")[0].replace("void ", "")
 
 
@@ -63,7 +63,7 @@ def main(fetch_dir, write_dir, out_json, fam=None):
                      key=lambda k: rows[k]["launches"])
     conv = rows[fam]
     res = {"kernel": {"conv_f32": "conv_f32 (conv_split_f32 + stem conv_gemm_f32)",
-                      "conv_h16": "conv_h16 (conv_pipe16 + conv_halo16 + conv_big16 + conv_expand16 + conv_gemm_h16)"}[fam],
+                      "conv_h16": "conv_h16 (conv_pipe16 + conv_halo16 + conv_haloc16 + conv_big16 + conv_expand16 + conv_gemm_h16)"}[fam],
            "bytes_per_launch": round(conv["bytes_per_launch"]),
            "launches": conv["launches"], "per_family": rows,
            "method": "2*FETCH_SIZE + WRITE_SIZE (rocprofv3 PMC, separate passes, KiB units)",

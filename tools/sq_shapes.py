@@ -26,7 +26,7 @@ def load(d):
     with open(f"{d}/run_counter_collection.csv") as f:
         for r in csv.DictReader(f):
             n = r["Kernel_Name"]
-            if not any(k in n for k in ("conv_pipe16", "conv_split", "conv_gemm", "conv_expand16", "conv_big16")):
+            if not any(k in n for k in ("conv_pipe16", "conv_split", "conv_gemm", "conv_expand16", "conv_big16", "conv_haloc16")):
                 continue
             did = int(r["Dispatch_Id"])
             per[did][r["Counter_Name"]] = per[did].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
