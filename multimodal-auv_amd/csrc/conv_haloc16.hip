@@ -33,8 +33,10 @@ __device__ __forceinline__ u32x4 cload(__amdgpu_buffer_rsrc_t r, unsigned off) {
 
 // MI = 1: 4 x 2 waves of 32 x 64 over a 128-pixel x 128-channel tile (512 threads, the default);
 // MI = 2: 2 x 2 waves of 64 x 64 (256 threads: one A and one B fragment read per MFMA instead of
-// 1.5, but half the waves to hide LDS and barrier latency: 3-4 % slower on every routed shape,
-// profiles/round5/haloc16_modes_ab_*.txt).  Two blocks per CU either way.
+// 1.5, but half the waves to cover LDS and barrier latency: 1-3 % slower over the routed shapes,
+// profiles/round5/haloc16_unroll_ab_*.txt).  Two blocks per CU either way.  The per-thread
+// global offsets are fixed over the chunks and taps (the chunk / tap part is a scalar offset),
+// which keeps the nine unrolled taps within 128 VGPRs (MI = 1).
 template <int DT, bool XBN, int MI>
 __global__ __launch_bounds__(256 * (3 - MI)) __attribute__((amdgpu_waves_per_eu(6 - 2 * MI)))
 void conv_haloc16(const ConvArgs a) {
@@ -70,51 +72,65 @@ void conv_haloc16(const ConvArgs a) {
   const unsigned rfloor = a.xrelu ? 0u : 0x80008000u;
 
   // ---- one 64-channel chunk of the input rows: chunk q = (LDS row hr, column iw, cq) ----
+  // Per thread, fixed over the chunks: its NCH 16-byte pieces' input offsets (the chunk's 128 B
+  // come as the scalar offset; out-of-image rows and pieces past the image get an offset past
+  // the buffer: zeros), LDS slots (-1: no piece) and in-image bits.  cq = tid & 7 for every j.
   const unsigned nch = (unsigned)(nhr * W * 8);
+  const int cq = tid & 7;
+  unsigned goff[NCH];
+  int lslot[NCH];
+  unsigned rowok = 0;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const unsigned q = (unsigned)(tid + NT * j);
+    const unsigned hr = udiv16(q, a.m16_w), rem = q - hr * (unsigned)(W * 8);
+    const int iw = (int)(rem >> 3);
+    const int gr = R0 - 1 + (int)hr;  // flattened image row b * H + ih
+    const unsigned b = udiv16((unsigned)gr, a.m16_h);
+    const int ih = gr - (int)b * H;
+    const bool in = (unsigned)gr < (unsigned)BH;
+    const bool ok = (q < nch) & in;
+    goff[j] = sel_off(ok, (unsigned)((b * a.xs_b + ih * a.xs_h + iw * a.xs_w + 8 * cq) * 2), kOOBc);
+    lslot[j] = q < nch ? cslot((int)hr * W2 + iw + 1, cq) : -1;
+    rowok |= (unsigned)in << j;
+  }
   u32x4 v[NCH];
   auto load_img = [&](int cc) {
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {
-      const unsigned q = (unsigned)(tid + NT * j);
-      const unsigned hr = udiv16(q, a.m16_w), rem = q - hr * (unsigned)(W * 8);
-      const int iw = (int)(rem >> 3), cq = (int)(rem & 7);
-      const int gr = R0 - 1 + (int)hr;  // flattened image row b * H + ih
-      const unsigned b = udiv16((unsigned)gr, a.m16_h);
-      const int ih = gr - (int)b * H;
-      const bool ok = (q < nch) & ((unsigned)gr < (unsigned)BH);
-      const unsigned off = (unsigned)((b * a.xs_b + ih * a.xs_h + iw * a.xs_w + 64 * cc + 8 * cq) * 2);
-      v[j] = cload(rx, sel_off(ok, off, kOOBc));
-    }
+    for (int j = 0; j < NCH; ++j)
+      v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)goff[j],
+                                                                             128 * cc, 0));
   };
   auto store_img = [&](int cc) {
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
-      const unsigned q = (unsigned)(tid + NT * j);
-      if (q < nch) {
-        const unsigned hr = udiv16(q, a.m16_w), rem = q - hr * (unsigned)(W * 8);
-        const int iw = (int)(rem >> 3), cq = (int)(rem & 7);
+      if (lslot[j] >= 0) {
         u32x4 t = v[j];
         if constexpr (XBN) {
-          const int gr = R0 - 1 + (int)hr;
           const int ch = 64 * cc + 8 * cq;
-          t = bn_relu8<DT>(t, ldf8(xbn + ch), ldf8(xbn + kMaxHcC + ch), rfloor,
-                           (unsigned)gr < (unsigned)BH);
+          t = bn_relu8<DT>(t, ldf8(xbn + ch), ldf8(xbn + kMaxHcC + ch), rfloor, (rowok >> j) & 1);
         }
-        *(u32x4*)(img + cslot((int)hr * W2 + iw + 1, cq)) = t;
+        *(u32x4*)(img + lslot[j]) = t;
       }
     }
   };
   // weight slice of (chunk cc, tap t): rows n0 + (tid >> 3) + NT / 8 j of w[n][r][s][c], channels
-  // 64 cc + 8 (tid & 7) .. + 7, as a row image [128][kHc]
+  // 64 cc + 8 (tid & 7) .. + 7, as a row image [128][kHc]; (tap, chunk) as the scalar offset
   const int wr = tid >> 3, wq = tid & 7;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)wg, (short)0, (int)((long long)a.N * 9 * C * 2), 0x00020000);
+  unsigned woff[NWJ];
+#pragma unroll
+  for (int j = 0; j < NWJ; ++j) {
+    const int n = n0 + wr + NT / 8 * j;
+    woff[j] = sel_off(n < a.N, (unsigned)((n * 9 * C + 8 * wq) * 2), kOOBc);
+  }
   u32x4 wv[NWJ];
   auto load_w = [&](int cc, int t) {
 #pragma unroll
-    for (int j = 0; j < NWJ; ++j) {
-      const int n = n0 + wr + NT / 8 * j;
-      wv[j] = n < a.N ? *(const u32x4*)(wg + (long long)n * 9 * C + t * C + 64 * cc + 8 * wq)
-                      : u32x4{0u, 0u, 0u, 0u};
-    }
+    for (int j = 0; j < NWJ; ++j)
+      wv[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rw, (int)woff[j], (t * C + 64 * cc) * 2, 0));
   };
   auto store_w = [&](int buf) {
 #pragma unroll
@@ -160,9 +176,7 @@ void conv_haloc16(const ConvArgs a) {
 
   int wb = 0;  // weight buffer of the current tap
   for (int cc = 0; cc < nchunk; ++cc) {
-    // unrolled nine times, the taps' address and prefetch registers spill (MI = 1 at 128 VGPRs,
-    // MI = 2 at 256)
-#pragma unroll (MI == 1 ? 1 : 3)
+#pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int r = t / 3, s = t % 3;
       const u16* wcur = wbuf + wb * WB;
@@ -213,7 +227,7 @@ void conv_haloc16(const ConvArgs a) {
 static int haloc_rows(int W) { return 128 % W == 0 ? 128 / W : 128 / W + 2; }
 
 // mauv_set_haloc16: 1 (default) routes the covered forwards here (32 x 64 wave tiles, 512
-// threads), 2 the same with 64 x 64 wave tiles (256 threads; measured 3-4 % slower), 0 keeps the
+// threads), 2 the same with 64 x 64 wave tiles (256 threads; measured 1-3 % slower), 0 keeps the
 // implicit GEMM
 int g_haloc16 = 1;
 
@@ -225,7 +239,9 @@ bool conv_haloc16_launch(int dt, const ConvArgs& a0, hipStream_t st) {
       a0.W > 512 || a0.H > 4096 || (long long)a0.B * a0.H >= (1 << 17))
     return false;
   if (a0.xs_c != 1 || a0.xs_w % 8 || a0.xs_h % 8 || a0.xs_b % 8 || a0.xs_g % 8) return false;
-  if ((long long)a0.B * a0.xs_b * 2 > 0x7fff0000LL) return false;  // 31-bit buffer offsets
+  if ((long long)a0.B * a0.xs_b * 2 > 0x7fff0000LL ||
+      (long long)a0.N * 9 * a0.Cin * 2 > 0x7fff0000LL)
+    return false;  // 31-bit buffer offsets
   if ((haloc_rows(a0.W) + 2) * (a0.W + 2) > kHcPx) return false;
   ConvArgs a = a0;
   a.m16_w = m16_div((unsigned)(a.W * 8));
@@ -235,7 +251,8 @@ bool conv_haloc16_launch(int dt, const ConvArgs& a0, hipStream_t st) {
 #define HC_GO(D, X, MI_) \
   hipLaunchKernelGGL((conv_haloc16<D, X, MI_>), grid, dim3(256 * (3 - MI_)), 0, st, a)
 #define HC_MI(D, X) \
-  if (g_haloc16 == 2) HC_GO(D, X, 2); else HC_GO(D, X, 1)
+  if (g_haloc16 == 2) HC_GO(D, X, 2); \
+  else HC_GO(D, X, 1)
   if (dt == DT_BF16) {
     if (xb) HC_MI(DT_BF16, true);
     else HC_MI(DT_BF16, false);

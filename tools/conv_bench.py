@@ -68,11 +68,15 @@ def main():
     ap.add_argument("--fused", action="store_true",
                     help="as in the model: BN+ReLU applied on load (fwd, wgrad) and BN "
                          "statistics partials from the fwd epilogue")
+    ap.add_argument("--haloc16", type=int, default=None,
+                    help="mauv_set_haloc16 mode for the run (0: the implicit GEMM)")
     ap.add_argument("--expand16", type=int, default=None,
                     help="mauv_set_expand16 mode for the run (0: the implicit GEMM)")
     a = ap.parse_args()
     if a.expand16 is not None:
         ops.set_expand16(a.expand16)
+    if a.haloc16 is not None:
+        ops.set_haloc16(a.haloc16)
     global REPS
     REPS = a.reps
     G, B, dev = a.G, a.B, "cuda"
