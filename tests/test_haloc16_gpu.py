@@ -27,6 +27,7 @@ CASES = [
     (1, 2, 7, 7, 512, 512, True),       # layer-4 form at 7 x 7: four column tiles, M = 98
     (3, 1, 32, 32, 128, 128, True),     # W = 32: four rows per tile
     (1, 5, 4, 4, 256, 128, True),       # W = 4: 32 rows per tile, 8 images in one tile
+    (2, 2, 8, 8, 128, 128, "norelu"),   # a pending BN without the ReLU
 ]
 
 
@@ -35,7 +36,8 @@ def _run(dt, G, B, H, W, C, N, xbn, haloc):
     torch.manual_seed(5)
     x = torch.randn(G, B, H, W, C, device=dev).to(dt)
     w = (torch.randn(G, N, 3, 3, C, device=dev) / (9 * C) ** 0.5).to(dt)
-    x_bn = (torch.rand(G, C, device=dev) + 0.5, torch.randn(G, C, device=dev) * 0.3, 1) \
+    relu = xbn != "norelu"
+    x_bn = (torch.rand(G, C, device=dev) + 0.5, torch.randn(G, C, device=dev) * 0.3, int(relu)) \
         if xbn else None
     nblk = ops.fwd_stat_blocks(G, B, H, W, C, N, 3, 1, 1)
     stats = tuple(torch.full(s, float("nan"), device=dev) for s in ((G, nblk, N), (G, nblk, N),
@@ -51,8 +53,9 @@ def _run(dt, G, B, H, W, C, N, xbn, haloc):
     # one rounding to the 16-bit format, then ReLU)
     xt = x.float()
     if xbn:
-        xt = torch.relu((xt * x_bn[0][:, None, None, None] + x_bn[1][:, None, None, None]).to(dt)
-                        .float())
+        xt = (xt * x_bn[0][:, None, None, None] + x_bn[1][:, None, None, None]).to(dt).float()
+        if relu:
+            xt = torch.relu(xt)
     y64 = torch.stack([
         F.conv2d(xt[g].double().permute(0, 3, 1, 2), w[g].double().permute(0, 3, 1, 2), padding=1)
         .permute(0, 2, 3, 1) for g in range(G)]).reshape(G, B * H * W, N)
@@ -62,7 +65,7 @@ def _run(dt, G, B, H, W, C, N, xbn, haloc):
 @pytest.mark.parametrize("mode", [1, 2], ids=["w32x64", "w64x64"])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "G{}B{}H{}W{}C{}N{}{}".format(
-    *c[:6], "x" if c[6] else ""))
+    *c[:6], {True: "x", False: "", "norelu": "xn"}[c[6]]))
 def test_haloc16_matches_float64_and_implicit_gemm(case, dt, mode):
     G, B, H, W, C, N, xbn = case
     y0, st0, nblk, _ = _run(dt, G, B, H, W, C, N, xbn, 0)
