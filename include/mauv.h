@@ -117,10 +117,10 @@ int mauv_set_dma16(int mode, int min_k);
 // covered shape, 0 none, -1 query.  Returns the previous mode.  (Replaces nothing in the
 // reference: a routing switch for A/Bs.)
 int mauv_set_expand16(int mode);
-// Route 16-bit 3x3 / stride-1 forwards over 128-512 channels through the chunked LDS row-image
-// kernel (conv_haloc16.hip): 1 (default) with 32 x 64 wave tiles, 2 with 64 x 64 wave tiles, 0 not
-// at all (the implicit GEMM), -1 query.  Returns the previous setting.  (Replaces nothing in the
-// reference: a routing switch for A/Bs.)
+// Route 16-bit 3x3 / stride-1 forwards and data gradients over 128-512 channels through the
+// chunked LDS row-image kernel (conv_haloc16.hip): 1 (default) with 32 x 64 wave tiles, 2 with
+// 64 x 64 wave tiles, 3 the forwards only, 0 not at all (the implicit GEMM), -1 query.  Returns
+// the previous setting.  (Replaces nothing in the reference: a routing switch for A/Bs.)
 int mauv_set_haloc16(int on);
 
 /* ---- 16-bit implicit-GEMM convs (conv_gemm16.hip) -----------------------------------------

@@ -170,9 +170,10 @@ bool conv_big16_fold_launch(int dt, const ConvArgs& a, hipStream_t st);
 // 1x1 / stride-1 forwards over K = 64 / 128 / 256 channels into N >= 256 outputs, weight-
 // stationary (conv_expand16.hip); false: shape not covered (or mauv_set_expand16(0))
 bool conv_expand16_launch(int dt, const ConvArgs& a, hipStream_t st);
-// 3x3 / stride-1 forwards over 128-512 channels through an LDS image of the input rows, 64
-// channels at a time (conv_haloc16.hip); false: shape not covered (or mauv_set_haloc16(0))
-bool conv_haloc16_launch(int dt, const ConvArgs& a, hipStream_t st);
+// 3x3 / stride-1 forwards and data gradients over 128-512 channels through an LDS image of the
+// input (dy) rows, 64 channels at a time (conv_haloc16.hip); false: shape not covered (or
+// switched off, mauv_set_haloc16)
+bool conv_haloc16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
 // 3x3 / stride-1 forwards and data gradients over 64 -> 64 channels through an LDS image of the
 // input rows (conv_halo16.hip); false: shape not covered (or mauv_set_halo3(0))
 bool conv_halo16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);

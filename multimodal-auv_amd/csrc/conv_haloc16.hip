@@ -37,16 +37,20 @@ __device__ __forceinline__ u32x4 cload(__amdgpu_buffer_rsrc_t r, unsigned off) {
 // profiles/round5/haloc16_unroll_ab_*.txt).  Two blocks per CU either way.  The per-thread
 // global offsets are fixed over the chunks and taps (the chunk / tap part is a scalar offset),
 // which keeps the nine unrolled taps within 128 VGPRs (MI = 1).
-template <int DT, bool XBN, int MI>
+// MODE = DGRAD: dx = the same 3x3 / stride-1 correlation of dy (C = Cout channels, the image)
+// with the taps mirrored; the weight slice of a tap is w[co][r][s][ci] for 64 co (k) x 128 ci
+// (n), staged as a column image and read with col_frag (conv_halo16.hip's data gradient).
+template <int MODE, int DT, bool XBN, int MI>
 __global__ __launch_bounds__(256 * (3 - MI)) __attribute__((amdgpu_waves_per_eu(6 - 2 * MI)))
 void conv_haloc16(const ConvArgs a) {
   constexpr int WGM = 4 / MI, WGN = 2, NT = 64 * WGM * WGN, BM = 128, BN = 128, WN = 64, NI = 2;
   constexpr int WM = 32 * MI;
-  constexpr int IMG = kHcPx * 64, WB = BN * kHc;  // 16-bit words
+  constexpr int WLD = MODE == FWD ? kHc : BN + 32;  // weight image: rows (FWD) / columns
+  constexpr int IMG = kHcPx * 64, WB = (MODE == FWD ? BN : 64) * WLD;  // 16-bit words
   constexpr int NCH = kHcPx * 8 / NT;               // 16-byte image chunks per thread
   constexpr int NWJ = BN * 8 / NT;                  // 16-byte weight chunks per thread and tap
   __shared__ __attribute__((aligned(16))) u16 smem[IMG + 2 * WB];
-  __shared__ float xbn[2 * kMaxHcC];
+  __shared__ float xbn[XBN ? 2 * kMaxHcC : 1];
   u16* img = smem;
   u16* wbuf = smem + IMG;
 
@@ -54,15 +58,18 @@ void conv_haloc16(const ConvArgs a) {
   const int wm = wave / WGN, wn = wave % WGN, li = lane & 31, lh = lane >> 5;
   int m0, n0, g;
   conv_block_tile<BM, BN>(a, m0, n0, g);
-  const int C = a.Cin, W = a.W, H = a.H, W2 = W + 2, BH = a.B * H;
+  const int C = MODE == FWD ? a.Cin : a.Cout, W = a.W, H = a.H, W2 = W + 2, BH = a.B * H;
   const int R0 = __builtin_amdgcn_readfirstlane(m0 / W);
   const int R1 = __builtin_amdgcn_readfirstlane((min(a.M, m0 + BM) - 1) / W);
   const int nhr = R1 - R0 + 3;  // LDS rows incl. the two halo rows (host-checked: fits kHcPx)
 
-  const u16* xg = (const u16*)a.x + (long long)g * a.xs_g;
+  // the image's source: x (FWD, strided NHWC) or dy (DGRAD, dense [B*H*W][Cout])
+  const long long nin = MODE == FWD ? (long long)a.B * a.xs_b : (long long)BH * W * C;
+  const u16* xg = MODE == FWD ? (const u16*)a.x + (long long)g * a.xs_g
+                              : (const u16*)a.dy + (long long)g * nin;
   const u16* wg = (const u16*)a.w + (long long)g * a.ws_g;
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)xg, (short)0, (int)((long long)a.B * a.xs_b * 2), 0x00020000);
+      (void*)xg, (short)0, (int)(nin * 2), 0x00020000);
   if constexpr (XBN) {
     for (int i = tid; i < C; i += NT) {
       xbn[i] = a.xsc[g * C + i];
@@ -90,7 +97,10 @@ void conv_haloc16(const ConvArgs a) {
     const int ih = gr - (int)b * H;
     const bool in = (unsigned)gr < (unsigned)BH;
     const bool ok = (q < nch) & in;
-    goff[j] = sel_off(ok, (unsigned)((b * a.xs_b + ih * a.xs_h + iw * a.xs_w + 8 * cq) * 2), kOOBc);
+    const unsigned off = MODE == FWD
+        ? (unsigned)((b * a.xs_b + ih * a.xs_h + iw * a.xs_w + 8 * cq) * 2)
+        : (unsigned)(((gr * W + iw) * C + 8 * cq) * 2);
+    goff[j] = sel_off(ok, off, kOOBc);
     lslot[j] = q < nch ? cslot((int)hr * W2 + iw + 1, cq) : -1;
     rowok |= (unsigned)in << j;
   }
@@ -114,28 +124,37 @@ void conv_haloc16(const ConvArgs a) {
       }
     }
   };
-  // weight slice of (chunk cc, tap t): rows n0 + (tid >> 3) + NT / 8 j of w[n][r][s][c], channels
-  // 64 cc + 8 (tid & 7) .. + 7, as a row image [128][kHc]; (tap, chunk) as the scalar offset
-  const int wr = tid >> 3, wq = tid & 7;
+  // weight slice of (chunk cc, tap t), (tap, chunk) as the scalar offset.  FWD: rows
+  // n0 + (tid >> 3) + NT / 8 j of w[n][r][s][c], channels 64 cc + 8 (tid & 7) .. + 7, as a row
+  // image [128][kHc].  DGRAD: rows co = 64 cc + (idx >> 4) of w[co][r][s][ci], input channels
+  // n0 + 8 (idx & 15) .. + 7 (idx = tid + NT j), as a column image [64 k][BN + 32].
+  const int wr = MODE == FWD ? tid >> 3 : tid >> 4, wq = MODE == FWD ? tid & 7 : tid & 15;
+  constexpr int WRS = MODE == FWD ? NT / 8 : NT / 16;  // rows per j
+  const int wstride = MODE == FWD ? 9 * C : 9 * a.N;  // elements between weight rows
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)wg, (short)0, (int)((long long)a.N * 9 * C * 2), 0x00020000);
+      (void*)wg, (short)0, (int)((long long)a.N * 9 * (MODE == FWD ? C : a.Cout) * 2),
+      0x00020000);
   unsigned woff[NWJ];
 #pragma unroll
   for (int j = 0; j < NWJ; ++j) {
-    const int n = n0 + wr + NT / 8 * j;
-    woff[j] = sel_off(n < a.N, (unsigned)((n * 9 * C + 8 * wq) * 2), kOOBc);
+    const int row = wr + WRS * j;
+    if constexpr (MODE == FWD)
+      woff[j] = sel_off(n0 + row < a.N, (unsigned)(((n0 + row) * wstride + 8 * wq) * 2), kOOBc);
+    else
+      woff[j] = (unsigned)((row * wstride + n0 + 8 * wq) * 2);
   }
   u32x4 wv[NWJ];
   auto load_w = [&](int cc, int t) {
+    const int so = MODE == FWD ? (t * C + 64 * cc) * 2 : (64 * cc * 9 * a.N + t * a.N) * 2;
 #pragma unroll
     for (int j = 0; j < NWJ; ++j)
       wv[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            rw, (int)woff[j], (t * C + 64 * cc) * 2, 0));
+                                            rw, (int)woff[j], so, 0));
   };
   auto store_w = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < NWJ; ++j)
-      *(u32x4*)(wbuf + buf * WB + (wr + NT / 8 * j) * kHc + 8 * wq) = wv[j];
+      *(u32x4*)(wbuf + buf * WB + (wr + WRS * j) * WLD + 8 * wq) = wv[j];
   };
 
   // the zero columns 0 and W + 1 of every LDS row (no chunk writes them)
@@ -178,7 +197,8 @@ void conv_haloc16(const ConvArgs a) {
   for (int cc = 0; cc < nchunk; ++cc) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      const int r = t / 3, s = t % 3;
+      // the image pixel of tap t (DGRAD: mirrored; the weight slice is tap t's)
+      const int r = MODE == FWD ? t / 3 : 2 - t / 3, s = MODE == FWD ? t % 3 : 2 - t % 3;
       const u16* wcur = wbuf + wb * WB;
       const u16* ap[MI];
       int sw[MI];
@@ -195,7 +215,10 @@ void conv_haloc16(const ConvArgs a) {
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi) af[mi] = *(const u32x4*)(ap[mi] + 8 * ((2 * ks + lh) ^ sw[mi]));
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) bq[ni] = row_frag_ld<kHc>(wcur, wn * WN + ni * 32, ks, li, lh);
+        for (int ni = 0; ni < NI; ++ni) {
+          if constexpr (MODE == FWD) bq[ni] = row_frag_ld<kHc>(wcur, wn * WN + ni * 32, ks, li, lh);
+          else bq[ni] = col_frag(wcur, WLD, wn * WN + ni * 32, ks, lane);
+        }
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -220,45 +243,56 @@ void conv_haloc16(const ConvArgs a) {
     }
   }
 
-  epilogue16<FWD, DT, BM, BN, MI, NI, WGM, WGN, (IMG + 2 * WB) * 2>(a, acc, smem, m0, n0, g);
+  epilogue16<MODE, DT, BM, BN, MI, NI, WGM, WGN, (IMG + 2 * WB) * 2>(a, acc, smem, m0, n0, g);
 }
 
 // rows of the flattened B*H image rows a 128-pixel tile touches, at most
 static int haloc_rows(int W) { return 128 % W == 0 ? 128 / W : 128 / W + 2; }
 
-// mauv_set_haloc16: 1 (default) routes the covered forwards here (32 x 64 wave tiles, 512
-// threads), 2 the same with 64 x 64 wave tiles (256 threads; measured 1-3 % slower), 0 keeps the
-// implicit GEMM
+// mauv_set_haloc16: 1 (default) routes the covered forwards and data gradients here (32 x 64
+// wave tiles, 512 threads), 2 the same with 64 x 64 wave tiles (256 threads; measured 1-3 %
+// slower), 3 the forwards only (32 x 64), 0 neither (the implicit GEMM)
 int g_haloc16 = 1;
 
-// true: launched
-bool conv_haloc16_launch(int dt, const ConvArgs& a0, hipStream_t st) {
-  if (!g_haloc16) return false;
+// true: launched.  FWD: the pending BN (xsc) on load; DGRAD: the stride-1 data gradient
+// without the BN-partials epilogue (addend / accumulate / mask forms through epilogue16)
+bool conv_haloc16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
+  if (!g_haloc16 || (mode == DGRAD && g_haloc16 == 3)) return false;
+  const int C = mode == FWD ? a0.Cin : a0.Cout;  // the image's channels
   if (a0.R != 3 || a0.S != 3 || a0.stride != 1 || a0.pad != 1 || a0.cpg || a0.Ho != a0.H ||
-      a0.Wo != a0.W || a0.Cin % 64 || a0.Cin < 128 || a0.Cin > kMaxHcC || a0.N % 128 ||
-      a0.W > 512 || a0.H > 4096 || (long long)a0.B * a0.H >= (1 << 17))
+      a0.Wo != a0.W || C % 64 || C < 128 || C > kMaxHcC || a0.N % 128 || a0.W > 512 ||
+      a0.H > 4096 || (long long)a0.B * a0.H >= (1 << 17))
     return false;
-  if (a0.xs_c != 1 || a0.xs_w % 8 || a0.xs_h % 8 || a0.xs_b % 8 || a0.xs_g % 8) return false;
-  if ((long long)a0.B * a0.xs_b * 2 > 0x7fff0000LL ||
-      (long long)a0.N * 9 * a0.Cin * 2 > 0x7fff0000LL)
-    return false;  // 31-bit buffer offsets
+  if (mode == FWD) {
+    if (a0.xs_c != 1 || a0.xs_w % 8 || a0.xs_h % 8 || a0.xs_b % 8 || a0.xs_g % 8) return false;
+    if ((long long)a0.B * a0.xs_b * 2 > 0x7fff0000LL) return false;  // 31-bit buffer offsets
+  } else {
+    if (mode != DGRAD || a0.bp_p1 || a0.xsc || a0.N != a0.Cin) return false;
+    if ((long long)a0.B * a0.H * a0.W * C * 2 > 0x7fff0000LL) return false;
+  }
+  if ((long long)a0.N * 9 * C * 2 > 0x7fff0000LL) return false;
   if ((haloc_rows(a0.W) + 2) * (a0.W + 2) > kHcPx) return false;
   ConvArgs a = a0;
   a.m16_w = m16_div((unsigned)(a.W * 8));
   a.m16_h = m16_div((unsigned)a.H);
   const dim3 grid(ceil_div(a.M, 128) * (a.N / 128), a.G);
   const bool xb = a.xsc != nullptr;
-#define HC_GO(D, X, MI_) \
-  hipLaunchKernelGGL((conv_haloc16<D, X, MI_>), grid, dim3(256 * (3 - MI_)), 0, st, a)
-#define HC_MI(D, X) \
-  if (g_haloc16 == 2) HC_GO(D, X, 2); \
-  else HC_GO(D, X, 1)
-  if (dt == DT_BF16) {
-    if (xb) HC_MI(DT_BF16, true);
-    else HC_MI(DT_BF16, false);
-  } else {
-    if (xb) HC_MI(DT_F16, true);
-    else HC_MI(DT_F16, false);
+#define HC_GO(MD, D, X, MI_) \
+  hipLaunchKernelGGL((conv_haloc16<MD, D, X, MI_>), grid, dim3(256 * (3 - MI_)), 0, st, a)
+#define HC_MI(MD, D, X) \
+  if (g_haloc16 == 2) HC_GO(MD, D, X, 2); \
+  else HC_GO(MD, D, X, 1)
+  if (mode == FWD) {
+    if (dt == DT_BF16) {
+      if (xb) HC_MI(FWD, DT_BF16, true);
+      else HC_MI(FWD, DT_BF16, false);
+    } else {
+      if (xb) HC_MI(FWD, DT_F16, true);
+      else HC_MI(FWD, DT_F16, false);
+    }
+  } else {  // no pending BN on a data gradient's input
+    if (dt == DT_BF16) HC_MI(DGRAD, DT_BF16, false);
+    else HC_MI(DGRAD, DT_F16, false);
   }
 #undef HC_MI
 #undef HC_GO
@@ -267,14 +301,14 @@ bool conv_haloc16_launch(int dt, const ConvArgs& a0, hipStream_t st) {
 
 }  // namespace mauv
 
-// Route 16-bit 3x3 / stride-1 forwards over 128-512 channels through conv_haloc16 (1, default:
-// 32 x 64 wave tiles; 2: 64 x 64 wave tiles) or the implicit GEMM (0); -1 queries.  Returns the
-// previous setting.
+// Route 16-bit 3x3 / stride-1 forwards and data gradients over 128-512 channels through
+// conv_haloc16 (1, default: 32 x 64 wave tiles; 2: 64 x 64 wave tiles; 3: the forwards only) or
+// the implicit GEMM (0); -1 queries.  Returns the previous setting.
 MAUV_API int mauv_set_haloc16(int on) {
   const int prev = mauv::g_haloc16;
-  if (on >= 0 && on <= 2) mauv::g_haloc16 = on;
+  if (on >= 0 && on <= 3) mauv::g_haloc16 = on;
   else if (on != -1) {
-    mauv::set_error("set_haloc16: 0, 1, 2 or -1 (query)");
+    mauv::set_error("set_haloc16: 0, 1, 2, 3 or -1 (query)");
     return mauv::kErrArg;
   }
   return prev;

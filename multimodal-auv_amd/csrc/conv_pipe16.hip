@@ -455,7 +455,7 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
     }
     if (a.Cin % 64 || !xs8 || (a.xsc && a.Cin > kMaxXbn16)) return false;
     if (conv_halo16_launch(FWD, dt, a, st)) return true;
-    if (conv_haloc16_launch(dt, a, st)) return true;
+    if (conv_haloc16_launch(FWD, dt, a, st)) return true;
     if (conv_expand16_launch(dt, a, st)) return true;
     if (g_dma16 == 2 && a.K >= g_dma16_k && conv_dma128_launch(dt, a, st)) return true;
     if (big16() && a.K >= big16_min_k() && (big16() == 2 || big16_wins(a)) &&
@@ -467,6 +467,7 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
   } else if (mode == DGRAD) {
     if (a.Cout % 64 || a.Cin % 8) return false;
     if (conv_halo16_launch(DGRAD, dt, a, st)) return true;
+    if (conv_haloc16_launch(DGRAD, dt, a, st)) return true;
     pipe16_dt<DGRAD, false>(dt, a, st);
   } else {
     if (a.Cout % 8 || a.Cin % 8 || !xs8 || a.kchunk % 64) return false;

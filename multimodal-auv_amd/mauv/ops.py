@@ -139,8 +139,9 @@ def set_expand16(mode=None):
 
 def set_haloc16(mode=None):
     """Route 16-bit 3x3 / stride-1 forwards over 128-512 channels through the chunked LDS
-    row-image kernel (conv_haloc16.hip): 1 / True (default, 32 x 64 wave tiles), 2 (64 x 64 wave
-    tiles), 0 / False (the implicit GEMM), None keep.  Returns the previous mode."""
+    row-image kernel (conv_haloc16.hip), and the stride-1 data gradients of the same shapes:
+    1 / True (default, 32 x 64 wave tiles), 2 (64 x 64 wave tiles), 3 (the forwards only),
+    0 / False (the implicit GEMM), None keep.  Returns the previous mode."""
     rc = lib.mauv_set_haloc16(-1 if mode is None else int(mode))
     check(0 if rc >= 0 else rc, "set_haloc16")
     return rc

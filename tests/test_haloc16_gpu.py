@@ -100,4 +100,56 @@ def test_haloc16_switch_round_trip():
     assert ops.set_haloc16(None) == 1
     ops.set_haloc16(2)
     assert ops.set_haloc16(None) == 2
+    ops.set_haloc16(3)
+    assert ops.set_haloc16(None) == 3
     ops.set_haloc16(prev)
+
+
+DGRAD_CASES = [
+    # (G, B, H, W, C (= Cin = Cout), form)
+    (2, 2, 8, 8, 128, "plain"),
+    (1, 3, 10, 12, 256, "addend"),       # tiles spanning partial rows, M = 360 ragged
+    (2, 2, 7, 7, 512, "accumulate"),
+    (3, 1, 16, 16, 128, "mask"),         # addend counted under ReLU-mask bits
+]
+
+
+@pytest.mark.parametrize("mode", [1, 2], ids=["w32x64", "w64x64"])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("case", DGRAD_CASES, ids=lambda c: "G{}B{}H{}W{}C{}-{}".format(*c))
+def test_haloc16_dgrad_matches_float64_and_implicit_gemm(case, dt, mode):
+    """The 3x3 / stride-1 data gradients over 128-512 channels (mode 1 / 2) against the
+    implicit GEMM (mode 3: forwards only) and, plain, against float64: dx within one 16-bit
+    rounding step of the output scale; the addend / accumulate / mask forms through the same
+    epilogue."""
+    from mauv import ops
+    G, B, H, W, C, form = case
+    torch.manual_seed(7)
+    dy = torch.randn(G, B, H, W, C, device=dev).to(dt)
+    w = (torch.randn(G, C, 3, 3, C, device=dev) / (9 * C) ** 0.5).to(dt)
+    add = torch.randn(G, B, H, W, C, device=dev).to(dt) if form in ("addend", "mask") else None
+    mask = (torch.randint(0, 256, (G * B * H * W * C // 8,), device=dev, dtype=torch.uint8)
+            if form == "mask" else None)
+    base = torch.randn(G, B, H, W, C, device=dev).to(dt) if form == "accumulate" else None
+    outs = []
+    for m in (3, mode):
+        dx = base.clone() if base is not None else torch.empty(G, B, H, W, C, device=dev,
+                                                                dtype=dt)
+        prev = ops.set_haloc16(m)
+        try:
+            ops.conv2d_bwd_data(dy, w, dx, G, B, H, W, C, C, 3, 1, 1, addend=add,
+                                accumulate=form == "accumulate", addend_mask=mask)
+        finally:
+            ops.set_haloc16(prev)
+        torch.cuda.synchronize()
+        outs.append(dx.double())
+    ulp = 2.0 ** (-8 if dt == torch.bfloat16 else -11)
+    scale = outs[0].abs().max().item() + 1e-30
+    assert torch.isfinite(outs[1]).all()
+    assert (outs[1] - outs[0]).abs().max().item() <= 4 * ulp * scale
+    if form == "plain":
+        ref = torch.stack([
+            F.conv_transpose2d(dy[g].double().permute(0, 3, 1, 2),
+                               w[g].double().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+            for g in range(G)])
+        assert (outs[1] - ref).abs().max().item() <= 2 * ulp * (ref.abs().max().item() + 1e-30)

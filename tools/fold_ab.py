@@ -24,12 +24,13 @@ from mauv.models import define_models, DEFAULT_PRIOR  # noqa: E402
 
 def _set(flag, on):
     """An engine switch (engine.FOLD, ...) or a library routing switch named ops.set_<flag>
-    (e.g. --flag expand16)."""
+    (e.g. --flag expand16; --flag haloc16:3 sets mode 3 instead of 0 for the "off" arm)."""
     from mauv import ops
-    if hasattr(engine, flag):
-        setattr(engine, flag, on)
+    name, _, off = flag.partition(":")
+    if hasattr(engine, name):
+        setattr(engine, name, on)
     else:
-        getattr(ops, "set_" + flag)(1 if on else 0)   # 1: the library's default routing
+        getattr(ops, "set_" + name)(1 if on else int(off or 0))   # 1: the default routing
 
 
 def main():
