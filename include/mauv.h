@@ -33,6 +33,49 @@ extern "C" {
 const char* mauv_last_error(void);
 int mauv_abi_version(void);
 
+/* Kernel routing: ONE process-wide record, the only state the library keeps besides the
+ * thread-local error message.  Every launch reads it; change it only while no other thread of
+ * the process launches (a test or an A/B run between launches, or once at start-up).  Each
+ * field selects between kernels that compute the same operation (outputs bit-identical, or — for
+ * f32_math and the reparam backward — the same fp32 maths in another summation order); none
+ * replaces a reference call site, so the defaults need never change.
+ *   f32_math        arithmetic of the fp32 convs (mauv_conv2d_*_f32, mauv_stem_fwd_f32):
+ *                   6 split (default): every fp32 operand split exactly into three bf16 planes
+ *                   x = h + m + l, the six plane products h*h, h*m, m*h, h*l, l*h, m*m on
+ *                   v_mfma_f32_32x32x16_bf16 with fp32 accumulation — the dropped terms are
+ *                   <= 2^-24 |a*b|: fp32-grade results at 2.67x the f32-MFMA rate;
+ *                   5 split1 (one accumulator everywhere); 3 split3 (planes h, m; products
+ *                   h*h, h*m, m*h: ~2^-16 |a*b|, opt-in); 0 exact (v_mfma_f32_32x32x2_f32).
+ *                   Initial value from MAUV_F32_MATH=split|split1|split3|exact.
+ *   halo3           16-bit 3x3 / stride-1 convs over 64 -> 64 channels through an LDS image of
+ *                   the input rows (conv_halo16.hip): 1 (default) / 0 the implicit GEMM.
+ *   big16, big16_min_k  16-bit forwards on 256-row LDS-DMA tiles (conv_big16.hip): 1 (default)
+ *                   the shapes where they measured faster (1x1, no pending BN, K >= 512,
+ *                   N >= 256, >= 512 tiles), 2 every covered forward with K >= big16_min_k
+ *                   (default 512), 0 none.
+ *   haloc16         16-bit 3x3 / stride-1 forwards and data gradients over 128-512 channels
+ *                   through the chunked LDS row image (conv_haloc16.hip): 1 (default) with
+ *                   32 x 64 wave tiles, 2 with 64 x 64 wave tiles, 3 the forwards only, 0 none.
+ *   expand16        16-bit 1x1 expansion forwards (K = 64 / 128 / 256) through the
+ *                   weight-stationary kernel (conv_expand16.hip): 1 (default) where it measured
+ *                   faster, 2 every covered shape, 3 as 2 with 32-column waves at K = 128, 0 none.
+ *   reparam_kernels bit 0: sampling by (output channel, channel range) blocks with vector KRSC
+ *                   stores (bit-identical to the per-element kernel); bit 1: the reparameterisation
+ *                   backward with 16-byte slab loads (another fixed sum order).  Default 3.
+ * mauv_set_route validates every field and changes nothing on an error (-1). */
+typedef struct MauvRoute {
+  int f32_math;
+  int halo3;
+  int big16;
+  int big16_min_k;
+  int haloc16;
+  int expand16;
+  int reparam_kernels;
+  int reserved[9];
+} MauvRoute;
+int mauv_get_route(MauvRoute* out);
+int mauv_set_route(const MauvRoute* in);
+
 /* ---- implicit-GEMM convolution on MFMA (conv_gemm.hip) ---------------------------------
  * Replaces F.conv2d inside bayesian-torch Conv2dReparameterization.forward for every conv of
  * the three torchvision ResNet-50 trunks (models/base_models.py:15-18,
@@ -81,47 +124,7 @@ int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strides, const
                                const float* x_shift, int x_relu, const float* dy, float* ws,
                                int splits, int G, int B, int H, int W, int Cin, int Cout, int R,
                                int S, int stride, int pad, hipStream_t stream);
-/* Arithmetic of the three fp32 conv entry points above (process-wide; initial value from
- * MAUV_F32_MATH=split|split3|exact):
- *   6 split (default): every fp32 operand is split exactly into three bf16 planes
- *     x = h + m + l and the six plane products h*h, h*m, m*h, h*l, l*h, m*m run on
- *     v_mfma_f32_32x32x16_bf16 with fp32 accumulation (h*h in its own accumulator on the
- *     four-wave tiles; one accumulator on the default eight-wave tiles); the dropped terms
- *     are <= 2^-24 |a*b| — fp32-grade results at 2.67x the f32-MFMA rate;
- *   5 split1: the same with one accumulator everywhere;
- *   3 split3: planes (h, m), products h*h, h*m, m*h (~2^-16 |a*b|; opt-in);
- *   0 exact: v_mfma_f32_32x32x2_f32 (an fmaf chain).
- * mode -1 queries.  Returns the previous mode, or < 0 for an invalid mode. */
-int mauv_set_f32_math(int mode);
-
-/* 3x3 / stride-1 / pad-1 16-bit forwards over 64 -> 64 channels (every bottleneck's layer-1
- * conv2) through an LDS image of the input rows each block's pixels touch (conv_halo16.hip;
- * bit-identical to the implicit GEMM): 1 (default) routes them there, 0 to the implicit GEMM,
- * -1 queries.  Returns the previous setting. */
-int mauv_set_halo3(int on);
-/* 16-bit forwards on 256-row block tiles with LDS-DMA operands (conv_big16.hip; same operands
- * and k order as the implicit GEMM, bit-identical outputs): mode 1 (default) routes the shapes
- * where it measured faster (1x1, no pending BN, K >= 512, N >= 256, >= 512 tiles), 2 every
- * forward it covers with K = R*S*Cin >= min_k, 0 none; -1 keeps; min_k <= 0 keeps the
- * threshold (512).  Returns the previous mode. */
-int mauv_set_big16(int mode, int min_k);
-/* 16-bit forwards on 128 x 128 tiles of four waves with LDS-DMA operands (conv_big16.hip,
-   conv_dma128_launch; same operands and k order as the implicit GEMM: bit-identical outputs and
-   statistics): mode 1 (default) = where measured faster, 2 = every covered forward with
-   K >= min_k, 0 = none; -1 queries.  Returns the previous mode.  Replaces nothing in the
-   reference (F.conv2d under Conv2dReparameterization, models/base_models.py:74-90). */
-int mauv_set_dma16(int mode, int min_k);
-// Route 16-bit 1x1 / stride-1 expansion forwards (K = 64 / 128 / 256 input channels, N a multiple
-// of 256 / 512 outputs: the bottleneck conv3s, the layer-1 downsample) through the
-// weight-stationary kernel (conv_expand16.hip): 1 (default) where it measured faster, 2 every
-// covered shape, 0 none, -1 query.  Returns the previous mode.  (Replaces nothing in the
-// reference: a routing switch for A/Bs.)
-int mauv_set_expand16(int mode);
-// Route 16-bit 3x3 / stride-1 forwards and data gradients over 128-512 channels through the
-// chunked LDS row-image kernel (conv_haloc16.hip): 1 (default) with 32 x 64 wave tiles, 2 with
-// 64 x 64 wave tiles, 3 the forwards only, 0 not at all (the implicit GEMM), -1 query.  Returns
-// the previous setting.  (Replaces nothing in the reference: a routing switch for A/Bs.)
-int mauv_set_haloc16(int on);
+/* Their arithmetic: MauvRoute.f32_math (housekeeping section). */
 
 /* ---- 16-bit implicit-GEMM convs (conv_gemm16.hip) -----------------------------------------
  * Same three GEMM views on v_mfma_f32_32x32x16_{bf16,f16}: dtype 0 = bf16 (BASELINE configs[2]
@@ -130,12 +133,17 @@ int mauv_set_haloc16(int on);
  * partials and weight-gradient slabs fp32.  Cin and Cout must be multiples of 8 (the stems
  * run as GEMMs over im2col rows, mauv_stem_*; their former 8-channel padded form remains
  * valid), dgrad needs Cout % 32 == 0; x strides
- * are channel-contiguous multiples of 8.  Statistics partials: mauv_conv2d_fwd_stat_blocks. */
+ * are channel-contiguous multiples of 8.  Statistics partials: mauv_conv2d_fwd_stat_blocks.
+ * y_shift (nullable, [Cout] fp32): y is STORED centred, y[.., c] = round16(conv - y_shift[c]),
+ * while the statistics partials stay those of the uncentred conv output; pass the consuming
+ * BatchNorm's running mean here and to mauv_bn_stats_finalize — the 16-bit rounding error of the
+ * stored tensor then scales with the batch spread |y - mean| instead of |y|, the error the BN's
+ * 1/std amplifies when a channel's mean is large. */
 int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_strides,
                         const float* x_scale, const float* x_shift, int x_relu, const void* w,
                         void* y, int G, int B, int H, int W, int Cin, int Cout, int R, int S,
                         int stride, int pad, float* st_mean, float* st_m2, float* st_cnt,
-                        hipStream_t stream);
+                        const float* y_shift, hipStream_t stream);
 /* A bottleneck's conv1 (1x1, stride 1, no padding) whose input is the previous bottleneck's
  * output, formed while conv1's tiles are loaded (replaces bn3 + residual add + ReLU, the
  * `out += identity; out = relu(out)` of torchvision's Bottleneck.forward under
@@ -147,12 +155,13 @@ int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_strides,
  * statistics partials exactly mauv_conv2d_fwd_h16's on that `out`.  y, res: contiguous
  * [G][B][H][W][Cin]; Cin % 64 == 0, Cin <= 2048.  Returns 0 when launched, 1 when the shape is
  * outside the kernel (nothing launched: run mauv_bn_apply, then mauv_conv2d_fwd_h16), < 0 on an
- * argument error. */
+ * argument error.  y1_shift: mauv_conv2d_fwd_h16's y_shift for y1. */
 int mauv_conv2d_fwd_fold_h16(int dtype, const void* y, const float* scale, const float* shift,
                              const void* res, const float* res_scale, const float* res_shift,
                              void* out, unsigned char* out_mask, const void* w, void* y1, int G,
                              int B, int H, int W, int Cin, int Cout, float* st_mean,
-                             float* st_m2, float* st_cnt, hipStream_t stream);
+                             float* st_m2, float* st_cnt, const float* y1_shift,
+                             hipStream_t stream);
 int mauv_conv2d_bwd_data_h16(int dtype, const void* dy, const void* w, void* dx,
                              const void* addend, int accumulate, int G, int B, int H, int W,
                              int Cin, int Cout, int R, int S, int stride, int pad,
@@ -197,12 +206,7 @@ int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride, long lon
                      unsigned long long seed, unsigned long long sample0, unsigned int layer,
                      int G, int Cout, int Cin, int RS, int dw_cin, float* dmu, float* drho,
                      long long fixed_sample, hipStream_t stream);
-/* Kernel forms of the two calls above (process-wide; defaults 1, or MAUV_SAMPLE_BLK /
- * MAUV_REPARAM_BWD4 = 0 at load): bit 0 = sampling by (output channel, channel range) blocks
- * with vector KRSC stores (bit-identical to the per-element kernel), bit 1 = the backward with
- * 16-byte slab loads (deterministic; a different fixed sum order).  -1 queries.  Returns the
- * previous mask. */
-int mauv_set_reparam_kernels(int mask);
+/* Their kernel forms: MauvRoute.reparam_kernels (housekeeping section). */
 /* 16-bit sampled weights (dtype 0 = bf16, 1 = f16) for the 16-bit convs: KRSC with cin_pad
  * (>= Cin) input channels; pad channels are not written (zero-fill them once).  The sampling
  * arithmetic is fp32, only the stored weight is rounded.  out_gstride 0 = Cout*RS*cin_pad. */
@@ -289,14 +293,18 @@ int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const float* ga
                       hipStream_t stream);
 /* statistics from per-m-tile partials written by mauv_conv2d_fwd_f32's epilogue: Chan merge,
  * mean/invstd/scale/shift [G][C], sequential running-stat update (run_* nullable);
- * workspace: mauv_bn_stats_workspace_floats(G, nblk, C) floats (G*C when nblk <= 512; larger
- * partial counts are merged in segments) */
+ * workspace: mauv_bn_stats_workspace_floats(G, nblk, C) floats (2*G*C when nblk <= 128*64;
+ * larger partial counts are merged in segments).  y_shift (nullable, [C]): the centre the 16-bit
+ * forward stored y with (mauv_conv2d_fwd_h16) — mean and shift then describe the stored values
+ * (mean = mu - y_shift, shift = beta - mean*scale) for every consumer of that tensor, while the
+ * running mean is updated with the true mu; y_shift may alias run_mean (it is read before the
+ * update). */
 long long mauv_bn_stats_workspace_floats(int G, int nblk, int C);
 int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, const float* pm2,
                            const float* pcnt, const float* gamma, const float* beta,
                            float* run_mean, float* run_var, float momentum, float eps,
                            float* workspace, float* mean, float* invstd, float* scale,
-                           float* shift, hipStream_t stream);
+                           float* shift, const float* y_shift, hipStream_t stream);
 /* out = [relu](y*scale + shift (+ res')); res' = res*res_scale + res_shift when res_scale is
  * non-NULL — the bottleneck's downsample BatchNorm applied inside the residual add (its output
  * is never materialised). */
@@ -397,7 +405,8 @@ int mauv_stem_im2col(int dtype, const float* x, int B, int C, int H, int W, int 
 int mauv_stem_fwd_f32(const float* cols, const float* w, float* y, int G, int M, int Kp,
                       int Cout, float* st_mean, float* st_m2, float* st_cnt, hipStream_t stream);
 int mauv_stem_fwd_h16(int dtype, const void* cols, const void* w, void* y, int G, int M, int Kp,
-                      int Cout, float* st_mean, float* st_m2, float* st_cnt, hipStream_t stream);
+                      int Cout, float* st_mean, float* st_m2, float* st_cnt, const float* y_shift,
+                      hipStream_t stream);
 
 /* ---- fusion head + MC head (head.hip) ----------------------------------------------------
  * AdditiveAttention.forward (models/base_models.py:43-52) epilogues around the q|k|v and

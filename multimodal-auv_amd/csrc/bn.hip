@@ -113,6 +113,28 @@ __device__ __forceinline__ void chan_merge(double& nn, double& mu, double& mm, d
 // M2 = sum [M2_b + n_b*(mean_b - mean)^2] (double; no divisions in the loops).
 constexpr int FIN_L = 16;
 
+// The finalized statistics of channel c of group g.  With ysh (the centre the 16-bit forward
+// epilogue subtracted before storing y, ConvArgs::ysh) mean / shift describe the STORED values
+// y - ysh, which every consumer (BN on load, the BN backward's xhat) reads: mean_out = mu - ysh,
+// shift = beta - mean_out * scale; the running statistics take the true mean mu (uvar_out[G*C + ...],
+// bn_running_kernel).
+__device__ __forceinline__ void stats_out(int G, int g, int c, int C, double nn, double mu,
+                                          double mm,
+                                          const float* gamma, const float* beta, float eps,
+                                          const float* ysh, float* mean_out, float* invstd_out,
+                                          float* scale_out, float* shift_out, float* ws) {
+  const double var = mm / nn;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * invstd;
+  const float ms = (float)(ysh ? mu - (double)ysh[c] : mu);
+  mean_out[g * C + c] = ms;
+  invstd_out[g * C + c] = invstd;
+  scale_out[g * C + c] = sc;
+  shift_out[g * C + c] = beta[c] - ms * sc;
+  ws[g * C + c] = (float)(nn > 1.0 ? mm / (nn - 1.0) : var);   // unbiased variance
+  ws[(long long)G * C + g * C + c] = (float)mu;                  // true mean (running stats)
+}
+
 __device__ __forceinline__ double lane_sum16(double v, double (*red)[64], int tx, int ty) {
   red[ty][tx] = v;
   __syncthreads();
@@ -125,8 +147,8 @@ __device__ __forceinline__ double lane_sum16(double v, double (*red)[64], int tx
 __global__ __launch_bounds__(1024) void bn_stats_final(
     int G, int nblk, int C, const float* __restrict__ pmean, const float* __restrict__ pm2,
     const float* __restrict__ pcnt, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float eps, float* __restrict__ mean_out,
-    float* __restrict__ invstd_out, float* __restrict__ scale_out,
+    const float* __restrict__ beta, float eps, const float* __restrict__ ysh,
+    float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale_out,
     float* __restrict__ shift_out, float* __restrict__ uvar_out) {
   const int g = blockIdx.y, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
@@ -151,14 +173,8 @@ __global__ __launch_bounds__(1024) void bn_stats_final(
   }
   const double mm = lane_sum16(q, red, tx, ty);
   if (ty != 0 || c >= C) return;
-  const double var = mm / nn;
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float sc = gamma[c] * invstd;
-  mean_out[g * C + c] = (float)mu;
-  invstd_out[g * C + c] = invstd;
-  scale_out[g * C + c] = sc;
-  shift_out[g * C + c] = beta[c] - (float)mu * sc;
-  uvar_out[g * C + c] = (float)(nn > 1.0 ? mm / (nn - 1.0) : var);
+  stats_out(G, g, c, C, nn, mu, mm, gamma, beta, eps, ysh, mean_out, invstd_out, scale_out,
+            shift_out, uvar_out);
 }
 
 // Large partial counts (an MC-batched inference chunk: tens of thousands of 128-row partials per
@@ -215,6 +231,7 @@ __global__ __launch_bounds__(256) void bn_stats_merge(int G, int S, int C,
                                                       const double* __restrict__ seg,
                                                       const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, float eps,
+                                                      const float* __restrict__ ysh,
                                                       float* __restrict__ mean_out,
                                                       float* __restrict__ invstd_out,
                                                       float* __restrict__ scale_out,
@@ -227,44 +244,42 @@ __global__ __launch_bounds__(256) void bn_stats_merge(int G, int S, int C,
     const double* o = seg + (((long long)g * S + s) * C + c) * 3;
     chan_merge(nn, mu, mm, o[0], o[1], o[2]);
   }
-  const double var = mm / nn;
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float sc = gamma[c] * invstd;
-  mean_out[g * C + c] = (float)mu;
-  invstd_out[g * C + c] = invstd;
-  scale_out[g * C + c] = sc;
-  shift_out[g * C + c] = beta[c] - (float)mu * sc;
-  uvar_out[g * C + c] = (float)(nn > 1.0 ? mm / (nn - 1.0) : var);
+  stats_out(G, g, c, C, nn, mu, mm, gamma, beta, eps, ysh, mean_out, invstd_out, scale_out,
+            shift_out, uvar_out);
 }
 
-// stage 2 dispatch: ws holds uvar [G][C] floats, then (segmented path) the segment triples
+// stage 2 dispatch: ws holds uvar [G][C] and the true means [G][C] (stats_out), then
+// (segmented path) the segment triples
 static void stats_final(int G, int nblk, int C, const float* pmean, const float* pm2,
                         const float* pcnt, const float* gamma, const float* beta, float eps,
-                        float* mean, float* invstd, float* scale, float* shift, float* ws,
-                        hipStream_t stream) {
+                        const float* ysh, float* mean, float* invstd, float* scale, float* shift,
+                        float* ws, hipStream_t stream) {
   const int S = stat_segs(nblk);
   if (S == 1) {
     hipLaunchKernelGGL(bn_stats_final, dim3((C + 63) / 64, G), dim3(1024), 0, stream, G, nblk, C,
-                       pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift, ws);
+                       pmean, pm2, pcnt, gamma, beta, eps, ysh, mean, invstd, scale, shift, ws);
     return;
   }
-  double* seg = (double*)(((uintptr_t)(ws + (long long)G * C) + 7) & ~(uintptr_t)7);
+  double* seg = (double*)(((uintptr_t)(ws + 2LL * G * C) + 7) & ~(uintptr_t)7);
   hipLaunchKernelGGL(bn_stats_seg, dim3((C + 63) / 64, G, S), dim3(1024), 0, stream, nblk, C,
                      stat_seg_len(nblk), pmean, pm2, pcnt, seg);
   hipLaunchKernelGGL(bn_stats_merge, dim3((C + 255) / 256, G), dim3(256), 0, stream, G, S, C, seg,
-                     gamma, beta, eps, mean, invstd, scale, shift, ws);
+                     gamma, beta, eps, ysh, mean, invstd, scale, shift, ws);
 }
 static long long stats_ws_floats(int G, int nblk, int C) {
   const int S = stat_segs(nblk);
-  return (long long)G * C + (S > 1 ? 6LL * G * S * C + 2 : 0);
+  return 2LL * G * C + (S > 1 ? 6LL * G * S * C + 2 : 0);
 }
 
-// Stage 3: the G running-stat updates, in MC-sample order (= G sequential forward calls).
-__global__ void bn_running_kernel(int G, int C, const float* __restrict__ mean,
-                                  const float* __restrict__ uvar, float* __restrict__ run_mean,
-                                  float* __restrict__ run_var, float momentum) {
+// Stage 3: the G running-stat updates, in MC-sample order (= G sequential forward calls), from
+// stage 2's workspace: uvar [G][C], then the true means [G][C].
+__global__ void bn_running_kernel(int G, int C, const float* __restrict__ ws,
+                                  float* __restrict__ run_mean, float* __restrict__ run_var,
+                                  float momentum) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
+  const float* uvar = ws;
+  const float* mean = ws + (long long)G * C;
   float rm = run_mean[c], rv = run_var[c];
   for (int g = 0; g < G; ++g) {
     rm = (1.f - momentum) * rm + momentum * mean[g * C + c];
@@ -744,11 +759,11 @@ MAUV_API int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const 
   hipLaunchKernelGGL(bn_stats_partial, dim3(nblk, G), dim3(256), 0, stream, y, M, C, rpb, rm,
                      pmean, pm2, pcnt);
   float* uvar = pcnt + (long long)G * nblk;
-  stats_final(G, nblk, C, pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift, uvar,
-              stream);
+  stats_final(G, nblk, C, pmean, pm2, pcnt, gamma, beta, eps, nullptr, mean, invstd, scale, shift,
+              uvar, stream);
   if (run_mean && run_var)
-    hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
-                       mean, uvar, run_mean, run_var, momentum);
+    hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C, uvar,
+                       run_mean, run_var, momentum);
   if (out) {
     launch_apply<SF32>(y, scale, shift, res, nullptr, nullptr, relu, out, G, M, C, stream);
   }
@@ -760,13 +775,13 @@ MAUV_API int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, 
                                     const float* pcnt, const float* gamma, const float* beta,
                                     float* run_mean, float* run_var, float momentum, float eps,
                                     float* workspace, float* mean, float* invstd, float* scale,
-                                    float* shift, hipStream_t stream) {
+                                    float* shift, const float* y_shift, hipStream_t stream) {
   if (G <= 0 || nblk <= 0 || C <= 0) { set_error("bn_stats_finalize: bad shape"); return kErrArg; }
-  stats_final(G, nblk, C, pmean, pm2, pcnt, gamma, beta, eps, mean, invstd, scale, shift,
+  stats_final(G, nblk, C, pmean, pm2, pcnt, gamma, beta, eps, y_shift, mean, invstd, scale, shift,
               workspace, stream);
   if (run_mean && run_var)
     hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, G, C,
-                       mean, workspace, run_mean, run_var, momentum);
+                       workspace, run_mean, run_var, momentum);
   return check_launch("bn_stats_finalize");
 }
 

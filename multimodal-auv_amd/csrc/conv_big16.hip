@@ -84,22 +84,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrcb(const void* p, long long
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(nelem * 2), 0x00020000);
 }
 
-// NW = 8: 256-row tiles (BN = 256: 2 x 4 waves of 128 x 64; BN <= 128: 4 x 2 waves);
-// NW = 4: 128 x 128 tiles as 2 x 2 waves of 64 x 64 (16 MFMAs per wave per 64-deep stage, two
-// blocks per CU)
-template <int BM, int BN, int NW>
+// 8 waves on 256-row tiles: BN = 256 as 2 x 4 waves of 128 x 64, BN <= 128 as 4 x 2 waves
+template <int BN>
 struct WavesB {
-  static constexpr int M = NW == 4 ? 2 : (BN == 256 ? 2 : 4), N = NW / M;
+  static constexpr int M = BN == 256 ? 2 : 4, N = 8 / M;
 };
 
 }  // namespace
 
 // RES (fold, 1x1 stride-1 only): 0 = off; 1 = A is relu(x*xsc + xsh + rs) (identity residual),
 // 2 = relu(x*xsc + xsh + rs*rs_sc + rs_sh); the column-tile-0 blocks write A through to fout
-template <int DT, int BM, int BN, bool XBN, int RES = 0, int NW = 8>
-__global__ __launch_bounds__(64 * NW, 2) void conv_big16(const ConvArgs a) {
-  constexpr int NT = 64 * NW;
-  constexpr int WGM = WavesB<BM, BN, NW>::M, WGN = WavesB<BM, BN, NW>::N;
+template <int DT, int BM, int BN, bool XBN, int RES = 0>
+__global__ __launch_bounds__(512, 2) void conv_big16(const ConvArgs a) {
+  constexpr int NW = 8, NT = 64 * NW;
+  constexpr int WGM = WavesB<BN>::M, WGN = WavesB<BN>::N;
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 32, NI = WN / 32;
   constexpr int A_B = BM * 128, B_B = BN * 128, STG = A_B + B_B;  // bytes
   constexpr int RA = BM / NW, RB = BN / NW, JA = RA / 8, JB = RB / 8, J = JA + JB;
@@ -107,9 +105,8 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_big16(const ConvArgs a) {
   constexpr int XS = RES ? kMaxFold : kMaxXbnB;  // stride of the parameter tables
   constexpr int XOFF = 2 * STG;
   constexpr int XB = RES ? (RES == 2 ? 4 : 2) * kMaxFold * 4 : (XBN ? 2 * kMaxXbnB * 4 : 0);
-  // epilogue16's staging: per wave row (PR rows a pass); the 128-row tiles park the whole tile
-  // at once (one pass; 68 KB, still two blocks per CU)
-  constexpr int PR = NW == 4 ? BM : BM / WGM, EPI = PR * (BN + 4) * 4;
+  // epilogue16's staging: per wave row (PR rows a pass)
+  constexpr int PR = BM / WGM, EPI = PR * (BN + 4) * 4;
   constexpr int LDSB = XOFF + XB > EPI ? XOFF + XB : EPI;
   static_assert(LDSB <= 160 * 1024, "LDS");
   constexpr int TCH = BM * 8 / NT;  // A chunks each thread transforms per stage (XBN)
@@ -297,8 +294,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_big16(const ConvArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
-  epilogue16<FWD, DT, BM, BN, MI, NI, WGM, WGN, NW == 4 ? LDSB : 2 * STG>(a, acc, smem, m0, n0,
-                                                                            g);
+  epilogue16<FWD, DT, BM, BN, MI, NI, WGM, WGN, 2 * STG>(a, acc, smem, m0, n0, g);
 }
 
 // true: launched (a = conv_pipe16_launch's prepared FWD arguments)
@@ -322,26 +318,6 @@ bool conv_big16_launch(int dt, const ConvArgs& a, hipStream_t st) {
   else MAUV_BIG_DT(DT_F16);
 #undef MAUV_BIG_DT
 #undef MAUV_BIG_LAUNCH
-  return true;
-}
-
-// true: launched.  The same kernel on 128 x 128 tiles of four waves (a = conv_pipe16_launch's
-// prepared FWD arguments): the long-K forwards where conv_pipe16's register-staged tiles leave the
-// matrix cores waiting on load latency
-bool conv_dma128_launch(int dt, const ConvArgs& a, hipStream_t st) {
-  if (a.cpg || a.Cin % 64 || a.K != a.R * a.S * a.Cin || a.xs_c != 1 || a.xs_w % 8 ||
-      a.xs_h % 8 || a.xs_b % 8 || a.xs_g % 8 || (a.xsc && a.Cin > kMaxXbnB))
-    return false;
-  if ((long long)a.B * a.xs_b * 2 > 0x7fff0000LL || a.ws_g * 2 > 0x7fff0000LL) return false;
-  if (a.M <= 64 || a.N <= 64) return false;  // 128-row statistics partials; 64-wide N: pipe16
-  const dim3 grid(ceil_div(a.M, 128) * ceil_div(a.N, 128), a.G);
-  if (dt == DT_BF16) {
-    if (a.xsc) hipLaunchKernelGGL((conv_big16<DT_BF16, 128, 128, true, 0, 4>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((conv_big16<DT_BF16, 128, 128, false, 0, 4>), grid, dim3(256), 0, st, a);
-  } else {
-    if (a.xsc) hipLaunchKernelGGL((conv_big16<DT_F16, 128, 128, true, 0, 4>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((conv_big16<DT_F16, 128, 128, false, 0, 4>), grid, dim3(256), 0, st, a);
-  }
   return true;
 }
 

@@ -45,6 +45,11 @@ struct ConvArgs {
   // FWD epilogue BN statistics partials [G][st_nblk][N] (+ counts [G][st_nblk])
   float *st_mean, *st_m2, *st_cnt;
   int st_nblk, st_base;
+  // 16-bit FWD: the stored output is y - ysh[channel] (nullable, [N] or [cpg]; the consuming
+  // BatchNorm's running mean): the 16-bit rounding error then scales with |y - ysh| (the batch
+  // spread) instead of |y|, which the BN's 1/std amplifies when a channel's mean is large; the
+  // statistics partials stay those of y (mauv_bn_stats_finalize takes the same ysh)
+  const float* ysh;
   // DGRAD epilogue BN-backward partials [G][bp_nblk][N]: sum dz, sum dz*xhat
   const float *bp_y, *bp_out, *bp_sc, *bp_sh, *bp_mean, *bp_invstd;
   int bp_relu;
@@ -163,19 +168,18 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
 // 16-bit forwards on 256-row tiles with LDS-DMA operands (conv_big16.hip); false: not covered
 bool conv_big16_launch(int dt, const ConvArgs& a, hipStream_t st);
 // the same kernel on 128 x 128 tiles of four waves; false: not covered
-bool conv_dma128_launch(int dt, const ConvArgs& a, hipStream_t st);
 // the same kernel forming the previous block's output on load (ConvArgs::rs / fout); false:
 // shape not covered (nothing launched)
 bool conv_big16_fold_launch(int dt, const ConvArgs& a, hipStream_t st);
 // 1x1 / stride-1 forwards over K = 64 / 128 / 256 channels into N >= 256 outputs, weight-
-// stationary (conv_expand16.hip); false: shape not covered (or mauv_set_expand16(0))
+// stationary (conv_expand16.hip); false: shape not covered (or MauvRoute.expand16 = 0)
 bool conv_expand16_launch(int dt, const ConvArgs& a, hipStream_t st);
 // 3x3 / stride-1 forwards and data gradients over 128-512 channels through an LDS image of the
 // input (dy) rows, 64 channels at a time (conv_haloc16.hip); false: shape not covered (or
-// switched off, mauv_set_haloc16)
+// switched off, MauvRoute.haloc16)
 bool conv_haloc16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
 // 3x3 / stride-1 forwards and data gradients over 64 -> 64 channels through an LDS image of the
-// input rows (conv_halo16.hip); false: shape not covered (or mauv_set_halo3(0))
+// input rows (conv_halo16.hip); false: shape not covered (or MauvRoute.halo3 = 0)
 bool conv_halo16_launch(int mode, int dt, const ConvArgs& a, hipStream_t st);
 
 __device__ __forceinline__ floatx4 bn_act(floatx4 v, floatx4 sc, floatx4 sh, int relu) {

@@ -262,6 +262,12 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
 #pragma unroll
       for (int e = 0; e < 4; ++e) { f[e] = v0[e]; f[4 + e] = v1[e]; }
       const int kk = k % PFD;
+      if constexpr (MODE == FWD) {
+        if (a.ysh) {  // centred storage (ConvArgs::ysh): one fp32 subtraction, then the rounding
+          const int ch = a.cpg ? (n0 + 8 * cc) % a.cpg : n0 + 8 * cc;
+          f -= ldf8(a.ysh + ch);
+        }
+      }
       if constexpr (MODE == DGRAD) {
         if (addp) {
           floatx8 av = unpack8<DT>(PF ? pa[kk] : *(const u32x4*)(addp + o));

@@ -233,7 +233,11 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
       }
     }
 
-    // ---- 16-bit output: park the wave's 64 x WN tile, store 16-byte rows ----
+    // ---- 16-bit output: park the wave's 64 x WN tile (centred by ysh: ConvArgs), store
+    // 16-byte rows ----
+    float ctr[NI];
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) ctr[ni] = a.ysh ? a.ysh[nw0 + ni * 32 + li] : 0.f;
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -241,7 +245,7 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           park[(mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * PLD + ni * 32 + li] =
-              H16<DT>::from_f(acc[mi][ni][r]);
+              H16<DT>::from_f(acc[mi][ni][r] - ctr[ni]);
     __syncthreads();  // parked tiles and the next A image visible; every wave done with `buf`
     u16* outp = (u16*)a.out + (long long)g * a.out_sg;
 #pragma unroll
@@ -254,9 +258,9 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
   }
 }
 
-// Route: 1 (default) = the shapes where it measured faster (expand_wins), 2 = every shape the
-// kernel covers, 0 = none (conv_pipe16's short-K form)
-int g_expand16 = 1;
+// MauvRoute.expand16: 1 (default) = the shapes where it measured faster (expand_wins), 2 = every
+// shape the kernel covers, 3 = as 2 with 32-column waves for K = 128 (the A/B of §2.28's wave
+// width), 0 = none (conv_pipe16's short-K form)
 
 template <int DT, int K, int WN>
 static void launch_expand(const ConvArgs& a, hipStream_t st) {
@@ -275,7 +279,7 @@ static bool expand_dt(const ConvArgs& a, hipStream_t st) {
   switch (a.K) {
     case 64: launch_expand<DT, 64, 32>(a, st); return true;
     case 128:
-      if (g_expand16 == 3) launch_expand<DT, 128, 32>(a, st);
+      if (g_route.expand16 == 3) launch_expand<DT, 128, 32>(a, st);
       else launch_expand<DT, 128, 64>(a, st);
       return true;
     case 256: launch_expand<DT, 256, 64>(a, st); return true;
@@ -298,7 +302,8 @@ static bool expand_wins(const ConvArgs& a) {
 }
 
 bool conv_expand16_launch(int dt, const ConvArgs& a, hipStream_t st) {
-  if (!g_expand16) return false;
+  const int route = g_route.expand16;
+  if (!route) return false;
   if (a.R != 1 || a.S != 1 || a.stride != 1 || a.pad != 0 || a.cpg || a.Ho != a.H || a.Wo != a.W)
     return false;
   const int K = a.Cin;
@@ -310,21 +315,8 @@ bool conv_expand16_launch(int dt, const ConvArgs& a, hipStream_t st) {
       a.xs_b != (long long)a.H * a.W * K || (long long)a.M * K * 2 > 0x7fff0000LL)
     return false;
   if (a.st_mean && (!a.st_m2 || !a.st_cnt)) return false;
-  if (g_expand16 == 1 && !expand_wins(a)) return false;
+  if (route == 1 && !expand_wins(a)) return false;
   return dt == DT_BF16 ? expand_dt<DT_BF16>(a, st) : expand_dt<DT_F16>(a, st);
 }
 
 }  // namespace mauv
-
-// Route 16-bit 1x1 / stride-1 expansion forwards (K = 64 / 128 / 256, N a multiple of 256 /
-// 512) through the weight-stationary kernel: 1 (default) where it measured faster, 2 every
-// covered shape, 0 none (conv_pipe16), -1 query.  Returns the previous mode.
-MAUV_API int mauv_set_expand16(int mode) {
-  const int prev = mauv::g_expand16;
-  if (mode >= 0 && mode <= 3) mauv::g_expand16 = mode;
-  else if (mode != -1) {
-    mauv::set_error("set_expand16: mode 0, 1, 2 or -1 (query)");
-    return mauv::kErrArg;
-  }
-  return prev;
-}

@@ -21,7 +21,7 @@
 // k-major ([k][row], rows contiguous) so each MFMA operand is one conflict-free ds_read_b32;
 // MFMA v_mfma_f32_32x32x2_f32 (exact fp32, fmaf-chain numerics).
 //
-// Arithmetic of the fp32 products (mauv_set_f32_math; template parameter SPL):
+// Arithmetic of the fp32 products (MauvRoute.f32_math; template parameter SPL):
 //   SPL = 0  exact  — v_mfma_f32_32x32x2_f32 (f32 MFMA = the f32 vector rate, 157 TF/s);
 //   SPL = 6  split  (default) — every staged fp32 operand element is written to LDS as three
 //            bf16 planes, x = h + m + l exactly (h16.h split_bf16), and each 32x32x16 k-step
@@ -546,16 +546,9 @@ void conv_gemm_f32(const ConvArgs a) {
 // exact mode: DGRAD uses row images + b128 operand reads (measured on the bench workload:
 // DGRAD +3.5 %, FWD -2 %); a 32-deep tile measured slower (2 vs 3 blocks per CU) and was removed
 
-// fp32 product arithmetic (file header): 6 = split (default), 3 = split3, 0 = exact.
-// Initial value from MAUV_F32_MATH=split|split3|exact; mauv_set_f32_math changes it.
-static int g_f32_math = -1;
-static int f32_math() {
-  if (g_f32_math < 0) {
-    const char* e = getenv("MAUV_F32_MATH");
-    g_f32_math = !e ? 6 : !strcmp(e, "exact") ? 0 : !strcmp(e, "split3") ? 3 : !strcmp(e, "split1") ? 5 : 6;
-  }
-  return g_f32_math;
-}
+// fp32 product arithmetic (file header): 6 = split (default), 5 = split1, 3 = split3, 0 = exact
+// (MauvRoute.f32_math; initial value from MAUV_F32_MATH, capi.cpp)
+static int f32_math() { return g_route.f32_math; }
 
 template <int MODE, int BM, int BN, bool VA, bool VB>
 static void launch(const ConvArgs& a, hipStream_t st) {
@@ -732,17 +725,6 @@ MAUV_API int mauv_conv2d_bwd_data_f32(const float* dy, const float* w, float* dx
   return check_launch("conv2d_bwd_data");
 }
 
-// Arithmetic of the fp32 convs (file header): 0 exact, 6 split (default), 3 split3; -1 only
-// queries.  Returns the previous mode.
-MAUV_API int mauv_set_f32_math(int mode) {
-  const int prev = f32_math();
-  if (mode == 0 || mode == 3 || mode == 5 || mode == 6) g_f32_math = mode;
-  else if (mode != -1) {
-    set_error("set_f32_math: mode must be 0 (exact), 6 (split), 3 (split3) or -1 (query)");
-    return kErrArg;
-  }
-  return prev;
-}
 
 // Number of per-m-tile BN statistic partials the fused epilogues write (host sizing helpers).
 MAUV_API int mauv_conv2d_fwd_stat_blocks(int G, int B, int H, int W, int Cin, int Cout, int R,

@@ -51,6 +51,7 @@ struct ConvArgs16 {
   int xrelu;
   float *st_mean, *st_m2, *st_cnt;  // FWD epilogue BN statistics partials
   int st_nblk;
+  const float* ysh;                 // FWD: centred storage (conv_common.h ConvArgs::ysh)
 };
 
 constexpr int HBK = 32;
@@ -451,6 +452,9 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(const ConvArgs16 a) {
           if (a.addend) f += unpack8<DT>(*(const u32x4*)(a.addend + o));
           if (a.accumulate) f += unpack8<DT>(*(const u32x4*)(outp + o));
         }
+        if constexpr (MODE == H_FWD) {
+          if (a.ysh) f -= ldf8(a.ysh + col);
+        }
         *(u32x4*)(outp + o) = pack8<DT>(f);
       }
       __syncthreads();
@@ -511,6 +515,7 @@ static ConvArgs pipe_args(const ConvArgs16& h) {
   a.ph = h.ph; a.pw = h.pw; a.Hc = h.Hc; a.Wc = h.Wc; a.r0 = h.r0; a.s0 = h.s0; a.nr = h.nr;
   a.ns = h.ns; a.xsc = h.xsc; a.xsh = h.xsh; a.xrelu = h.xrelu;
   a.st_mean = h.st_mean; a.st_m2 = h.st_m2; a.st_cnt = h.st_cnt; a.st_nblk = h.st_nblk;
+  a.ysh = h.ysh;
   return a;
 }
 
@@ -534,7 +539,8 @@ MAUV_API int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_st
                                  const float* x_scale, const float* x_shift, int x_relu,
                                  const void* w, void* y, int G, int B, int H, int W, int Cin,
                                  int Cout, int R, int S, int stride, int pad, float* st_mean,
-                                 float* st_m2, float* st_cnt, hipStream_t stream) {
+                                 float* st_m2, float* st_cnt, const float* y_shift,
+                                 hipStream_t stream) {
   if (int e = check_shape16("conv2d_fwd_h16", dtype, G, B, Cin, Cout, x_strides)) return e;
   if (!aligned16(x) || !aligned16(w)) { set_error("conv2d_fwd_h16: x, w must be 16-B aligned"); return kErrArg; }
   ConvArgs16 a = make_args16(G, B, H, W, Cin, Cout, R, S, stride, pad, x_strides);
@@ -544,6 +550,7 @@ MAUV_API int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_st
   a.out_sg = (long long)a.M * a.N;
   a.st_mean = st_mean; a.st_m2 = st_m2; a.st_cnt = st_cnt;
   a.st_nblk = ceil_div(a.M, conv_tile_rows(a.M));
+  a.ysh = y_shift;
   if (conv_pipe16_launch(FWD, dtype, pipe_args(a), stream)) {}
   else if (Cin % HBK == 0) dispatch16<H_FWD, true>(dtype, a, stream);
   else dispatch16<H_FWD, false>(dtype, a, stream);
@@ -562,7 +569,7 @@ MAUV_API int mauv_conv2d_fwd_fold_h16(int dtype, const void* y, const float* sca
                                       const void* w, void* y1, int G, int B, int H, int W,
                                       int Cin, int Cout,
                                       float* st_mean, float* st_m2, float* st_cnt,
-                                      hipStream_t stream) {
+                                      const float* y1_shift, hipStream_t stream) {
   if (int e = check_shape16("conv2d_fwd_fold_h16", dtype, G, B, Cin, Cout, nullptr)) return e;
   if (!y || !scale || !shift || !res || !out || !w || !y1 || !res_scale != !res_shift) {
     set_error("conv2d_fwd_fold_h16: y, scale, shift, res, out, w, y1 required; res_scale and "
@@ -580,6 +587,7 @@ MAUV_API int mauv_conv2d_fwd_fold_h16(int dtype, const void* y, const float* sca
   h.out_sg = (long long)h.M * h.N;
   h.st_mean = st_mean; h.st_m2 = st_m2; h.st_cnt = st_cnt;
   h.st_nblk = ceil_div(h.M, conv_tile_rows(h.M));
+  h.ysh = y1_shift;
   ConvArgs a = pipe_args(h);
   a.rs = res; a.rs_sc = res_scale; a.rs_sh = res_shift; a.fout = out; a.fmask = out_mask;
   if (!conv_big16_fold_launch(dtype, a, stream)) return 1;
@@ -590,7 +598,7 @@ MAUV_API int mauv_conv2d_fwd_fold_h16(int dtype, const void* y, const float* sca
 // shared im2col rows with the G weight sets stacked along N; Kp % 64 == 0.
 MAUV_API int mauv_stem_fwd_h16(int dtype, const void* cols, const void* w, void* y, int G,
                                int M, int Kp, int Cout, float* st_mean, float* st_m2,
-                               float* st_cnt, hipStream_t stream) {
+                               float* st_cnt, const float* y_shift, hipStream_t stream) {
   if (int e = check_shape16("stem_fwd_h16", dtype, G, 1, Kp, Cout, nullptr)) return e;
   if (M <= 0 || Kp % 64) { set_error("stem_fwd_h16: needs M > 0 and Kp % 64 == 0"); return kErrArg; }
   if (!aligned16(cols) || !aligned16(w)) { set_error("stem_fwd_h16: cols, w must be 16-B aligned"); return kErrArg; }
@@ -600,6 +608,7 @@ MAUV_API int mauv_stem_fwd_h16(int dtype, const void* cols, const void* w, void*
   h.out_sg = (long long)M * Cout;
   h.st_mean = st_mean; h.st_m2 = st_m2; h.st_cnt = st_cnt;
   h.st_nblk = ceil_div(M, conv_tile_rows(M));
+  h.ysh = y_shift;
   ConvArgs a = pipe_args(h);
   a.cpg = Cout;
   // the pipelined kernel reads cols by a buffer descriptor (31-bit byte offsets): rows beyond

@@ -178,9 +178,8 @@ void conv_halo16(const ConvArgs a) {
   epilogue16<MODE, DT, BM, BN, 1, NI, WGM, WGN, (HALO + 2 * WB) * 2>(a, acc2, smem, m0, n0, g);
 }
 
-// mauv_set_halo3 (default on): the 3x3 C = 64 forwards take this kernel
-static int g_halo3 = 1;
-static int halo3() { return g_halo3; }
+// MauvRoute.halo3 (default on): the 3x3 C = 64 forwards and data gradients take this kernel
+static int halo3() { return g_route.halo3; }
 
 // rows of the flattened B*H image rows a BM-pixel tile touches, at most
 static int halo_rows(int BM, int W) { return BM % W == 0 ? BM / W : BM / W + 2; }
@@ -235,15 +234,3 @@ bool conv_halo16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
 }
 
 }  // namespace mauv
-
-// Route the 3x3 / stride-1 / 64 -> 64 16-bit forwards through conv_halo16 (1, default) or the
-// implicit GEMM (0); -1 queries.  Returns the previous setting.
-MAUV_API int mauv_set_halo3(int on) {
-  const int prev = mauv::halo3();
-  if (on == 0 || on == 1) mauv::g_halo3 = on;
-  else if (on != -1) {
-    mauv::set_error("set_halo3: 0, 1 or -1 (query)");
-    return mauv::kErrArg;
-  }
-  return prev;
-}

@@ -10,7 +10,7 @@
 // (double-buffered, the next slice in registers one tap ahead); the next chunk's rows are in
 // registers while the current chunk's taps run.  Accumulation order is (chunk, tap, k): it is
 // not the implicit GEMM's (tap, chunk, k), so outputs agree with it to fp32 summation order
-// (routing is by shape only, mauv_set_haloc16); the statistics epilogue is epilogue16's.
+// (routing is by shape only, MauvRoute.haloc16); the statistics epilogue is epilogue16's.
 #include "conv_common.h"
 #include "conv_epi16.h"
 
@@ -249,15 +249,15 @@ void conv_haloc16(const ConvArgs a) {
 // rows of the flattened B*H image rows a 128-pixel tile touches, at most
 static int haloc_rows(int W) { return 128 % W == 0 ? 128 / W : 128 / W + 2; }
 
-// mauv_set_haloc16: 1 (default) routes the covered forwards and data gradients here (32 x 64
+// MauvRoute.haloc16: 1 (default) routes the covered forwards and data gradients here (32 x 64
 // wave tiles, 512 threads), 2 the same with 64 x 64 wave tiles (256 threads; measured 1-3 %
 // slower), 3 the forwards only (32 x 64), 0 neither (the implicit GEMM)
-int g_haloc16 = 1;
 
 // true: launched.  FWD: the pending BN (xsc) on load; DGRAD: the stride-1 data gradient
 // without the BN-partials epilogue (addend / accumulate / mask forms through epilogue16)
 bool conv_haloc16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
-  if (!g_haloc16 || (mode == DGRAD && g_haloc16 == 3)) return false;
+  const int route = g_route.haloc16;
+  if (!route || (mode == DGRAD && route == 3)) return false;
   const int C = mode == FWD ? a0.Cin : a0.Cout;  // the image's channels
   if (a0.R != 3 || a0.S != 3 || a0.stride != 1 || a0.pad != 1 || a0.cpg || a0.Ho != a0.H ||
       a0.Wo != a0.W || C % 64 || C < 128 || C > kMaxHcC || a0.N % 128 || a0.W > 512 ||
@@ -267,7 +267,8 @@ bool conv_haloc16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
     if (a0.xs_c != 1 || a0.xs_w % 8 || a0.xs_h % 8 || a0.xs_b % 8 || a0.xs_g % 8) return false;
     if ((long long)a0.B * a0.xs_b * 2 > 0x7fff0000LL) return false;  // 31-bit buffer offsets
   } else {
-    if (mode != DGRAD || a0.bp_p1 || a0.xsc || a0.N != a0.Cin) return false;
+    // the torchvision bottleneck's stride-1 3x3 maps C -> C (the only form the tests cover)
+    if (mode != DGRAD || a0.bp_p1 || a0.xsc || a0.Cin != a0.Cout) return false;
     if ((long long)a0.B * a0.H * a0.W * C * 2 > 0x7fff0000LL) return false;
   }
   if ((long long)a0.N * 9 * C * 2 > 0x7fff0000LL) return false;
@@ -280,7 +281,7 @@ bool conv_haloc16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
 #define HC_GO(MD, D, X, MI_) \
   hipLaunchKernelGGL((conv_haloc16<MD, D, X, MI_>), grid, dim3(256 * (3 - MI_)), 0, st, a)
 #define HC_MI(MD, D, X) \
-  if (g_haloc16 == 2) HC_GO(MD, D, X, 2); \
+  if (route == 2) HC_GO(MD, D, X, 2); \
   else HC_GO(MD, D, X, 1)
   if (mode == FWD) {
     if (dt == DT_BF16) {
@@ -300,16 +301,3 @@ bool conv_haloc16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
 }
 
 }  // namespace mauv
-
-// Route 16-bit 3x3 / stride-1 forwards and data gradients over 128-512 channels through
-// conv_haloc16 (1, default: 32 x 64 wave tiles; 2: 64 x 64 wave tiles; 3: the forwards only) or
-// the implicit GEMM (0); -1 queries.  Returns the previous setting.
-MAUV_API int mauv_set_haloc16(int on) {
-  const int prev = mauv::g_haloc16;
-  if (on >= 0 && on <= 3) mauv::g_haloc16 = on;
-  else if (on != -1) {
-    mauv::set_error("set_haloc16: 0, 1, 2, 3 or -1 (query)");
-    return mauv::kErrArg;
-  }
-  return prev;
-}

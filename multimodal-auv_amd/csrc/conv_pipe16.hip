@@ -411,11 +411,10 @@ static void pipe16_dt(int dt, const ConvArgs& a, hipStream_t st) {
   else pipe16_tiles<MODE, DT_F16, XBN, STEM>(a, st);
 }
 
-// mauv_set_big16: 1 (default) = the forwards where the 256-row LDS-DMA kernel (conv_big16.hip)
-// measured faster take it; 2 = every forward it covers with K >= g_big16_k; 0 = none
-int g_big16 = 1, g_big16_k = 512;
-static int big16() { return g_big16; }
-static int big16_min_k() { return g_big16_k; }
+// MauvRoute.big16: 1 (default) = the forwards where the 256-row LDS-DMA kernel (conv_big16.hip)
+// measured faster take it; 2 = every forward it covers with K >= big16_min_k; 0 = none
+static int big16() { return g_route.big16; }
+static int big16_min_k() { return g_route.big16_min_k; }
 // measured (tools/fwd_ab.py): faster only on 1x1 forwards without a pending
 // BN over K >= 512 input channels into N >= 256 outputs with enough 256 x 256 tiles for two
 // rounds of the chip; the 3x3s and the 128-column / few-tile shapes of the training slice ran
@@ -424,16 +423,6 @@ static bool big16_wins(const ConvArgs& a) {
   const long long tiles = (long long)ceil_div(a.M, 256) * ceil_div(a.N, 256) * a.G;
   return a.R == 1 && a.S == 1 && !a.xsc && a.K >= 512 && a.N >= 256 && tiles >= 512;
 }
-
-// mauv_set_dma16: 1 (default) = the forwards where the 128 x 128 LDS-DMA tiles
-// (conv_dma128_launch) measured faster take them; 2 = every forward they cover with
-// K >= g_dma16_k; 0 = none
-int g_dma16 = 1, g_dma16_k = 512;
-// measured (tools/fwd_ab.py): with a pending BN (transformed in LDS after the
-// DMA lands, one extra barrier per stage) 3x3 / 1x1 forwards ran 1.1-1.4x slower than conv_pipe16;
-// without one, within +-8 % of conv_pipe16 (training slice) and slower than the 256-row tiles
-// where those are routed (inference chunk): no shape is routed to them by default
-static bool dma16_wins(const ConvArgs&) { return false; }
 
 bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
   const long long lim = 0x7fff0000LL / 2;  // elements addressable by a 31-bit byte offset
@@ -457,11 +446,9 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
     if (conv_halo16_launch(FWD, dt, a, st)) return true;
     if (conv_haloc16_launch(FWD, dt, a, st)) return true;
     if (conv_expand16_launch(dt, a, st)) return true;
-    if (g_dma16 == 2 && a.K >= g_dma16_k && conv_dma128_launch(dt, a, st)) return true;
     if (big16() && a.K >= big16_min_k() && (big16() == 2 || big16_wins(a)) &&
         conv_big16_launch(dt, a, st))
       return true;
-    if (g_dma16 == 1 && dma16_wins(a) && conv_dma128_launch(dt, a, st)) return true;
     if (a.xsc) pipe16_dt<FWD, true>(dt, a, st);
     else pipe16_dt<FWD, false>(dt, a, st);
   } else if (mode == DGRAD) {
@@ -483,31 +470,3 @@ bool conv_pipe16_launch(int mode, int dt, const ConvArgs& a0, hipStream_t st) {
 }
 
 }  // namespace mauv
-
-// Route 16-bit forwards through the 128 x 128 LDS-DMA tiles: mode 1 (default) where they
-// measured faster, 2 every forward they cover with K >= min_k, 0 none; -1 / min_k <= 0 query /
-// keep.  Returns the previous mode.
-MAUV_API int mauv_set_dma16(int mode, int min_k) {
-  const int prev = mauv::g_dma16;
-  if (mode >= 0 && mode <= 2) mauv::g_dma16 = mode;
-  else if (mode != -1) {
-    mauv::set_error("set_dma16: mode 0, 1, 2 or -1 (query)");
-    return mauv::kErrArg;
-  }
-  if (min_k > 0) mauv::g_dma16_k = min_k;
-  return prev;
-}
-
-// Route 16-bit forwards through conv_big16: mode 1 (default) where it measured faster, 2 every
-// forward it covers with K >= min_k, 0 none; mode -1 / min_k <= 0 query / keep.  Returns the
-// previous mode.
-MAUV_API int mauv_set_big16(int mode, int min_k) {
-  const int prev = mauv::g_big16;
-  if (mode >= 0 && mode <= 2) mauv::g_big16 = mode;
-  else if (mode != -1) {
-    mauv::set_error("set_big16: mode 0, 1, 2 or -1 (query)");
-    return mauv::kErrArg;
-  }
-  if (min_k > 0) mauv::g_big16_k = min_k;
-  return prev;
-}

@@ -4,7 +4,7 @@
 // (every conv of the path; the 1- and 3-channel stems through their STEM mode over images packed
 // to 4 zero-padded NHWC channels — other channel counts fall back to conv_gemm.hip).
 //
-// Arithmetic (conv_gemm.hip header, include/mauv.h mauv_set_f32_math): each fp32 operand
+// Arithmetic (conv_gemm.hip header, include/mauv.h MauvRoute.f32_math): each fp32 operand
 // element is split exactly into bf16 planes x = h + m + l and the product a.b is accumulated in
 // fp32 from h.h, h.m, m.h, h.l, l.h, m.m on v_mfma_f32_32x32x16_bf16 (dropped terms <= 2^-24
 // |a.b|).  With the MFMAs 2.67x cheaper than f32 MFMA, the staging becomes the bottleneck of a

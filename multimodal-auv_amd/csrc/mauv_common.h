@@ -19,6 +19,10 @@ void set_error(const std::string& s);
 // Launch-status check used by every C-ABI entry point: returns 0 or a negative code.
 int check_launch(const char* what);
 
+// Process-wide kernel routing (include/mauv.h MauvRoute): written only by mauv_set_route, read
+// by the launchers; the defaults are the measured-fastest routes (capi.cpp).
+extern MauvRoute g_route;
+
 constexpr int kErrArg = -1;      // invalid argument / unsupported shape
 constexpr int kErrLaunch = -2;   // hipGetLastError() after launch
 

@@ -386,9 +386,8 @@ static dim3 sample_grid(long long nq, int G) {
   return dim3(bx, (unsigned)(gy < 1 ? 1 : gy));
 }
 
-// Kernel forms (default 1 each; mauv_set_reparam_kernels): bit 0 = block-form sampling,
-// bit 1 = 16-byte reparam_bwd.
-static int g_sample_blk = 1, g_bwd4 = 1;
+// Kernel forms (MauvRoute.reparam_kernels, default 3): bit 0 = block-form sampling, bit 1 =
+// 16-byte reparam_bwd.
 
 // The block form when its layout conditions hold, else the element kernel.
 template <class S>
@@ -397,7 +396,7 @@ static void launch_sample(const float* mu, const float* rho, const float* eps,
                           const unsigned long long* base, unsigned int layer, int G, int Cout,
                           int Cin, int RS, int cin_pad, typename S::T* out, long long gs,
                           hipStream_t stream) {
-  const int blk = g_sample_blk;
+  const int blk = g_route.reparam_kernels & 1;
   const int align = (int)sizeof(typename S::T) * 4;
   if (blk && Cin % 4 == 0 && cin_pad % 4 == 0 && gs % 4 == 0 && RS <= 256 &&
       ((uintptr_t)out % align) == 0) {
@@ -517,7 +516,7 @@ MAUV_API int mauv_reparam_bwd(const float* dw, int splits, long long dw_gstride,
   if (RS > 49) { set_error("reparam_bwd: R*S > 49"); return kErrArg; }
   (void)nq;
   const int nt = (fixed_sample >= 0 ? G : 1) * splits;
-  const int v4 = mauv::g_bwd4;
+  const int v4 = (mauv::g_route.reparam_kernels >> 1) & 1;
   if (v4 && Cin % 4 == 0 && dw_cin % 4 == 0 && gs % 4 == 0 && ss % 4 == 0 &&
       ((uintptr_t)dw & 15) == 0 && nt <= RB4_TERMS &&
       (long long)(splits - 1) * ss + (long long)(G - 1) * gs + (long long)Cout * RS * dw_cin <
@@ -572,20 +571,4 @@ MAUV_API int mauv_philox_raw(unsigned long long seed, unsigned long long sample,
   hipLaunchKernelGGL(philox_raw_kernel, dim3((nq + 255) / 256), dim3(256), 0, stream, seed,
                      sample, layer, nq, (uint4*)out_u32x4, (floatx4*)out_normal4);
   return check_launch("philox_raw");
-}
-
-// Select the sampling / reparameterisation-backward kernel forms: bit 0 = block-form sampling
-// (reparam_sample_blk), bit 1 = 16-byte backward (reparam_bwd4); -1 queries.  Returns the
-// previous mask.  Sampling is bit-identical either way; the backward's sum order differs.
-MAUV_API int mauv_set_reparam_kernels(int mask) {
-  const int prev = mauv::g_sample_blk |
-                   (mauv::g_bwd4 << 1);
-  if (mask >= 0 && mask <= 3) {
-    mauv::g_sample_blk = mask & 1;
-    mauv::g_bwd4 = (mask >> 1) & 1;
-  } else if (mask != -1) {
-    mauv::set_error("set_reparam_kernels: mask 0..3 or -1 (query)");
-    return mauv::kErrArg;
-  }
-  return prev;
 }

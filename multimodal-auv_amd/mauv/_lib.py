@@ -24,6 +24,8 @@ U32 = ctypes.c_uint
 SIGNATURES = {
     "mauv_abi_version": [],
     "mauv_last_error": [],
+    "mauv_get_route": [P],
+    "mauv_set_route": [P],
     # conv_gemm.hip
     "mauv_conv2d_fwd_f32": [P, P, P, P, I, P, P, P] + [I] * 10 + [P, P, P, P],
     "mauv_conv2d_fwd_stat_blocks": [I] * 10,
@@ -31,15 +33,9 @@ SIGNATURES = {
     "mauv_conv2d_bwd_data_stat_blocks": [I] * 10,
     "mauv_conv2d_wgrad_splits": [I, I, I, I, I, I, I, I, I, I],
     "mauv_conv2d_bwd_weight_f32": [P, P, P, P, I, P, P] + [I] * 11 + [P],
-    "mauv_set_f32_math": [I],
-    "mauv_set_halo3": [I],
-    "mauv_set_big16": [I, I],
-    "mauv_set_dma16": [I, I],
-    "mauv_set_expand16": [I],
-    "mauv_set_haloc16": [I],
     # conv_gemm16.hip
-    "mauv_conv2d_fwd_h16": [I, P, P, P, P, I, P, P] + [I] * 10 + [P, P, P, P],
-    "mauv_conv2d_fwd_fold_h16": [I] + [P] * 10 + [I] * 6 + [P, P, P, P],
+    "mauv_conv2d_fwd_h16": [I, P, P, P, P, I, P, P] + [I] * 10 + [P, P, P, P, P],
+    "mauv_conv2d_fwd_fold_h16": [I] + [P] * 10 + [I] * 6 + [P, P, P, P, P],
     "mauv_conv2d_bwd_data_h16": [I, P, P, P, P, I] + [I] * 10 + [P],
     "mauv_conv2d_bwd_data_bn_h16": [I, P, P, P, P, I] + [I] * 10 + [P] * 8 + [I, P, P, P],
     "mauv_reparam_sample_ex": [I, P, P, P, ctypes.c_ulonglong, ctypes.c_ulonglong, P, ctypes.c_uint,
@@ -48,7 +44,6 @@ SIGNATURES = {
     # reparam.hip
     "mauv_reparam_sample": [P, P, P, U64, U64, U32, I, I, I, I, P, LL, P],
     "mauv_reparam_bwd": [P, I, LL, LL, P, P, P, U64, U64, U32, I, I, I, I, I, P, P, LL, P],
-    "mauv_set_reparam_kernels": [I],
     "mauv_reparam_sample_h16": [I, P, P, P, U64, U64, U32, I, I, I, I, I, P, LL, P],
     "mauv_reparam_sample_padded": [P, P, P, U64, U64, U32, I, I, I, I, I, P, LL, P],
     "mauv_kl_workspace_bytes": [I],
@@ -61,7 +56,7 @@ SIGNATURES = {
     # bn.hip
     "mauv_bn_workspace_floats": [I, LL, I],
     "mauv_bn_fwd_train": [P, I, LL, I, P, P, P, P, F, F, P, P, P, P, P, P, I, P, P],
-    "mauv_bn_stats_finalize": [I, I, I, P, P, P, P, P, P, P, F, F, P, P, P, P, P, P],
+    "mauv_bn_stats_finalize": [I, I, I, P, P, P, P, P, P, P, F, F, P, P, P, P, P, P, P],
     "mauv_bn_stats_workspace_floats": [I, I, I],
     "mauv_bn_apply": [P, P, P, P, P, P, I, P, I, LL, I, P],
     "mauv_bn_eval_params": [I, I, P, P, P, P, F, P, P, P],
@@ -87,7 +82,7 @@ SIGNATURES = {
     # stem.hip
     "mauv_stem_im2col": [I, P] + [I] * 9 + [P, P],
     "mauv_stem_fwd_f32": [P, P, P, I, I, I, I, P, P, P, P],
-    "mauv_stem_fwd_h16": [I, P, P, P, I, I, I, I, P, P, P, P],
+    "mauv_stem_fwd_h16": [I, P, P, P, I, I, I, I, P, P, P, P, P],
     # head.hip
     "mauv_attn_t": [P, I, I, P, P],
     "mauv_attn_t_bwd": [P, P, I, I, P, P],
@@ -111,6 +106,13 @@ SIGNATURES = {
 }
 _RESTYPES = {"mauv_last_error": ctypes.c_char_p, "mauv_bn_workspace_floats": LL,
              "mauv_bn_stats_workspace_floats": LL, "mauv_resize_workspace_bytes": LL}
+
+
+class MauvRoute(ctypes.Structure):
+    """include/mauv.h MauvRoute: the library's process-wide kernel routing."""
+    _fields_ = [("f32_math", I), ("halo3", I), ("big16", I), ("big16_min_k", I),
+                ("haloc16", I), ("expand16", I), ("reparam_kernels", I),
+                ("reserved", I * 9)]
 
 
 class MauvError(RuntimeError):

@@ -53,6 +53,10 @@ class DistributedMC(nn.Module):
                 dist.broadcast(t.data, src=dist.get_global_rank(group, 0) if group else 0,
                                group=group)
         st = root_state(module)
+        # training: each rank its own Philox stream (as each DataParallel replica samples its
+        # own epsilons); MC-sharded inference draws from the rank-0 stream instead
+        # (predict.mc_statistics), so a sharded prediction equals the single-rank one
+        st.shared_seed = st.seed
         st.seed = (st.seed + 0x9E3779B97F4A7C15 * (self.rank + 1)) % (1 << 62)
         self._pending = []      # async works of the trunk slices issued during backward
         self._done = []         # [start, end) arena ranges they cover

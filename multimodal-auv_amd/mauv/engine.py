@@ -53,6 +53,15 @@ FOLD_MIN_TILES = 512
 # (whose epilogue already adds the residual gradient; not where a downsample branch accumulates
 # into that dx afterwards).  Test hook like FOLD: the same sums in another fp32 order.
 BWD_PARTIALS_F32 = True
+# 16-bit trunks: a conv output consumed by a batch-statistics BatchNorm is stored centred,
+# y - c (ops.conv2d_fwd ysh; the finalize turns the statistics into those of the stored values
+# and updates the running mean with the true one), c = that BN's running mean as of the model's
+# last refresh_centres (the first 16-bit forward, and every multimodal_predict_and_save call /
+# training epoch).  The f16 / bf16 rounding error of the stored tensor then follows the batch
+# spread |y - mean| instead of |y|: the largest of the path's rounding points (DESIGN.md
+# §2.31).  Exact in real arithmetic; c changes only when refreshed, so a forward's result stays
+# a function of the weights, samples and inputs between refreshes.  Test hook like FOLD.
+CENTRE_Y = True
 _STREAMS = {}
 
 
@@ -138,6 +147,37 @@ class RootState:
         # parameter lists the entry points walk every call (named_parameters over 696 tensors:
         # ~1.3 ms of host time per step ahead of the first kernel); built once, like self.params
         self._plists = {}
+        # centred 16-bit storage (CENTRE_Y): the BatchNorms that track running statistics and one
+        # flat buffer of their running means as of the last refresh_centres (views per BN)
+        self.bns = [m for m in root.modules()
+                    if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)
+                    and m.track_running_stats and m.running_mean is not None]
+        self._centre_buf = None
+        self._centre_views = {}
+
+    def refresh_centres(self):
+        """Copy every tracked BatchNorm's running mean into the centre buffer (one launch)."""
+        if not self.bns:
+            return
+        dev = self.bns[0].running_mean.device
+        if self._centre_buf is None or self._centre_buf.device != dev:
+            n = sum(bn.running_mean.numel() for bn in self.bns)
+            self._centre_buf = torch.empty(n, device=dev)
+            off, views = 0, {}
+            for bn in self.bns:
+                c = bn.running_mean.numel()
+                views[id(bn)] = self._centre_buf[off:off + c]
+                off += c
+            self._centre_views = views
+        with torch.no_grad():
+            torch._foreach_copy_([self._centre_views[id(bn)] for bn in self.bns],
+                                 [bn.running_mean.detach() for bn in self.bns])
+
+    def centre(self, bn):
+        """bn's centre (the first call builds the buffer from the current running means)."""
+        if self._centre_buf is None or self._centre_buf.device != bn.running_mean.device:
+            self.refresh_centres()
+        return self._centre_views.get(id(bn))
 
     def plist(self, key, build):
         got = self._plists.get(key)
@@ -179,6 +219,12 @@ def root_state(root):
 
 def invalidate(root):
     root.__dict__.pop("_mauv_state", None)
+
+
+def refresh_centres(root):
+    """Take the 16-bit trunks' storage centres (CENTRE_Y) from the current BatchNorm running
+    means — the drop-in predictor does at every call, the training loops at every epoch."""
+    root_state(root).refresh_centres()
 
 
 def set_rho_grad_mode(root, mode):
@@ -403,6 +449,15 @@ class TrunkRunner(_Runner):
         self.join = join  # caller's stream when this trunk runs on a stream of its own
         self.dt = dtype   # activation / sampled-weight storage (fp32, bf16 or f16)
 
+    def _centre(self, bn):
+        """The centre the 16-bit conv feeding ``bn`` stores its output around (CENTRE_Y): bn's
+        running mean as of the last refresh_centres when bn normalises with batch statistics
+        and tracks running ones, else None (fp32 storage, eval-mode BN, untracked statistics)."""
+        if not CENTRE_Y or self.dt == torch.float32 or not bn.training or \
+                not bn.track_running_stats or bn.running_mean is None:
+            return None
+        return self.st.centre(bn)
+
     def _cin_pad(self, Cin):
         """The convs move 16-byte channel chunks: input channels pad to 8 (16-bit) or 4 (fp32)
         (every conv after the stems has Cin % 64 == 0)."""
@@ -410,10 +465,12 @@ class TrunkRunner(_Runner):
         return Cin if Cin % q == 0 else (Cin + q - 1) // q * q
 
     # ---- conv / bn units ----
-    def _conv(self, conv, x, B, H, W, x_strides=None, x_bn=None, bn_stats=True, fold=None):
+    def _conv(self, conv, x, B, H, W, x_strides=None, x_bn=None, bn_stats=True, fold=None,
+              ysh=None):
         """fold = (y3, scale, shift, res, res_bn, mask): x is the previous bottleneck's output,
         not yet materialised; this 1x1 conv forms it on load (ops.conv2d_fwd_fold; mask: its ReLU
-        bits too) and self.fold_out holds it afterwards."""
+        bits too) and self.fold_out holds it afterwards.  ysh: the stored output's centre
+        (_centre of the BN it feeds)."""
         G, Cin, Cout, k = self.G, conv.in_channels, conv.out_channels, conv.kernel_size
         st, pd = conv.stride[0], conv.padding[0]
         cp = self._cin_pad(Cin)
@@ -435,16 +492,16 @@ class TrunkRunner(_Runner):
             y3, sc, sh, res, res_bn, mask = fold
             x = torch.empty_like(y3)
             if not ops.conv2d_fwd_fold(y3, sc, sh, res, res_bn, x, w, y, G, B, H, W, Cin, Cout,
-                                       stats=stats, mask=mask):
+                                       stats=stats, mask=mask, ysh=ysh):
                 if mask is not None:
                     ops.bn_apply_mask(y3, sc, sh, res, x, mask, G, B * H * W, Cin, res_bn=res_bn)
                 else:
                     ops.bn_apply(y3, sc, sh, res, 1, x, G, B * H * W, Cin, res_bn=res_bn)
-                ops.conv2d_fwd(x, w, y, G, B, H, W, cp, Cout, k, st, pd, stats=stats)
+                ops.conv2d_fwd(x, w, y, G, B, H, W, cp, Cout, k, st, pd, stats=stats, ysh=ysh)
             self.fold_out = x
         else:
             ops.conv2d_fwd(x, w, y, G, B, H, W, cp, Cout, k, st, pd, x_strides=x_strides,
-                           x_bn=x_bn, stats=stats, alg_cin=Cin)
+                           x_bn=x_bn, stats=stats, alg_cin=Cin, ysh=ysh)
         rec = (conv, x, x_strides, x_bn, w, B, H, W) if self.save else None
         return y, rec, part
 
@@ -506,7 +563,7 @@ class TrunkRunner(_Runner):
                             accumulate=accumulate, addend_mask=addend_mask, bn=bn)
         return dx
 
-    def _stem(self, conv, x, B, H, W):
+    def _stem(self, conv, x, B, H, W, ysh=None):
         """conv1 over im2col rows of the images, shared by the G samples: one GEMM
         [M x Kp] . [Kp x G*Cout] (ops.stem_fwd); the sampled weights are the OIHW parameter
         rows [Cout][Cin*R*S] zero-padded to Kp."""
@@ -525,7 +582,7 @@ class TrunkRunner(_Runner):
         buf = torch.empty(2 * G * nblk * Cout + G * nblk, device=x.device)
         part = (buf[:G * nblk * Cout], buf[G * nblk * Cout:2 * G * nblk * Cout],
                 buf[2 * G * nblk * Cout:], nblk)
-        ops.stem_fwd(cols, w, y, G, M, Kp, Cout, part[:3], K)
+        ops.stem_fwd(cols, w, y, G, M, Kp, Cout, part[:3], K, ysh=ysh)
         rec = ("stem", conv, cols, M, Kp) if self.save else None
         return y, rec, part
 
@@ -545,8 +602,9 @@ class TrunkRunner(_Runner):
         self._reparam_bwd(conv, conv.mu_kernel, conv.rho_kernel, ws, splits, Cout, K, 1,
                           "kernel", dw_cin=Kp)
 
-    def _bn(self, bn, y, part, relu, res=None, materialize=True, res_bn=None):
-        """Statistics (from the conv epilogue partials) + optional materialised output."""
+    def _bn(self, bn, y, part, relu, res=None, materialize=True, res_bn=None, ysh=None):
+        """Statistics (from the conv epilogue partials) + optional materialised output.  ysh: the
+        centre y was stored with (its conv's; the statistics then describe the stored values)."""
         G, C = self.G, y.shape[-1]
         M = y.numel() // (G * C)
         stats = torch.empty(4, G, C, device=y.device)
@@ -561,7 +619,7 @@ class TrunkRunner(_Runner):
             ops.bn_stats_finalize(G, nblk, C, pm, pm2, pcnt, bn.weight, bn.bias,
                                   bn.running_mean if track else None,
                                   bn.running_var if track else None, bn.momentum, bn.eps, ws,
-                                  mean, invstd, scale, shift)
+                                  mean, invstd, scale, shift, ysh=ysh)
             if track:
                 pending = getattr(self, "_nbt", None)
                 if pending is None:
@@ -569,6 +627,8 @@ class TrunkRunner(_Runner):
                 else:   # one multi-tensor add per trunk forward (run_forward)
                     pending.append(bn.num_batches_tracked)
         else:
+            if ysh is not None:
+                raise RuntimeError("mauv: centred storage needs batch statistics (_centre)")
             ops.bn_eval_params(G, C, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                bn.eps, scale, shift)
         out = mask = None
@@ -631,14 +691,15 @@ class TrunkRunner(_Runner):
             raise ValueError(f"trunk expects {t.conv1.in_channels} input channels, got {Cin}")
         self.B = B
         recs = self.recs = []
-        y, rc, part = self._stem(t.conv1, x, B, H, W)
+        c0 = self._centre(t.bn1)
+        y, rc, part = self._stem(t.conv1, x, B, H, W, ysh=c0)
         H, W = y.shape[2], y.shape[3]
         Hp, Wp = ops.out_hw(H, 3, 2, 1), ops.out_hw(W, 3, 2, 1)
         p = torch.empty(G, B, Hp, Wp, 64, device=x.device, dtype=self.dt)
         idx = torch.empty(G, B, Hp, Wp, 64, dtype=torch.uint8, device=x.device) \
             if self.save else None
         # bn1 + relu applied inside the max-pool's loads
-        _, rb = self._bn(t.bn1, y, part, relu=True, materialize=False)
+        _, rb = self._bn(t.bn1, y, part, relu=True, materialize=False, ysh=c0)
         scale, shift, _ = self.last_lazy
         ops.maxpool_fwd(y, G * B, H, W, 64, p, idx, bn=(scale, shift, G))
         del y, part
@@ -651,26 +712,29 @@ class TrunkRunner(_Runner):
         fold_ok = FOLD and self.dt != torch.float32
         pend = None
         for i, blk in enumerate(blocks):
+            c1, c2, c3 = (self._centre(b) for b in (blk.bn1, blk.bn2, blk.bn3))
             if pend is not None:
-                y1, r1, p1 = self._conv(blk.conv1, None, B, H, W, fold=pend)
+                y1, r1, p1 = self._conv(blk.conv1, None, B, H, W, fold=pend, ysh=c1)
                 cur, pend, self.fold_out = self.fold_out, None, None
             else:
-                y1, r1, p1 = self._conv(blk.conv1, cur, B, H, W)
-            _, s1 = self._bn(blk.bn1, y1, p1, relu=True, materialize=False)
-            y2, r2, p2 = self._conv(blk.conv2, y1, B, H, W, x_bn=self.last_lazy)
+                y1, r1, p1 = self._conv(blk.conv1, cur, B, H, W, ysh=c1)
+            _, s1 = self._bn(blk.bn1, y1, p1, relu=True, materialize=False, ysh=c1)
+            y2, r2, p2 = self._conv(blk.conv2, y1, B, H, W, x_bn=self.last_lazy, ysh=c2)
             H2, W2 = y2.shape[2], y2.shape[3]
-            _, s2 = self._bn(blk.bn2, y2, p2, relu=True, materialize=False)
-            y3, r3, p3 = self._conv(blk.conv3, y2, B, H2, W2, x_bn=self.last_lazy)
+            _, s2 = self._bn(blk.bn2, y2, p2, relu=True, materialize=False, ysh=c2)
+            y3, r3, p3 = self._conv(blk.conv3, y2, B, H2, W2, x_bn=self.last_lazy, ysh=c3)
             rd = sd = res_bn = None
             if blk.downsample is not None:   # its BN is applied inside bn3's residual add
-                res, rd, pd_ = self._conv(blk.downsample[0], cur, B, H, W)
-                _, sd = self._bn(blk.downsample[1], res, pd_, relu=False, materialize=False)
+                cd = self._centre(blk.downsample[1])
+                res, rd, pd_ = self._conv(blk.downsample[0], cur, B, H, W, ysh=cd)
+                _, sd = self._bn(blk.downsample[1], res, pd_, relu=False, materialize=False,
+                                 ysh=cd)
                 res_bn = self.last_lazy[:2]
             else:
                 res = cur
             nxt = blocks[i + 1].conv1 if i + 1 < len(blocks) else None
             if fold_ok and nxt is not None and self._fold_fits(nxt, B, H2, W2):
-                _, s3 = self._bn(blk.bn3, y3, p3, relu=True, materialize=False)
+                _, s3 = self._bn(blk.bn3, y3, p3, relu=True, materialize=False, ysh=c3)
                 mask = None
                 if self.save:   # the backward reads the block output's ReLU bits (_bn's rule)
                     mask = torch.empty(y3.numel() // 8, dtype=torch.uint8, device=y3.device)
@@ -678,7 +742,7 @@ class TrunkRunner(_Runner):
                 pend = (y3,) + self.last_lazy[:2] + (res, res_bn, mask)
                 a3 = None
             else:
-                a3, s3 = self._bn(blk.bn3, y3, p3, relu=True, res=res, res_bn=res_bn)
+                a3, s3 = self._bn(blk.bn3, y3, p3, relu=True, res=res, res_bn=res_bn, ysh=c3)
             del res
             if self.save:
                 recs.append((r1, s1, r2, s2, r3, s3, rd, sd))

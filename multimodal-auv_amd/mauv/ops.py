@@ -8,7 +8,7 @@ import ctypes
 
 import torch
 
-from ._lib import lib, check
+from ._lib import lib, check, MauvRoute
 
 _LL5 = ctypes.c_longlong * 5
 
@@ -94,47 +94,71 @@ F32_MATH = {"exact": 0, "split3": 3, "split1": 5, "split": 6}
 _F32_NAMES = {v: k for k, v in F32_MATH.items()}
 
 
+def route():
+    """The library's kernel routing (include/mauv.h MauvRoute) as a dict of its fields."""
+    r = MauvRoute()
+    check(lib.mauv_get_route(ctypes.byref(r)), "get_route")
+    return {f: getattr(r, f) for f, _ in MauvRoute._fields_ if f != "reserved"}
+
+
+def set_route(**fields):
+    """Change the named MauvRoute fields (process-wide; between launches only, include/mauv.h);
+    returns the previous values of those fields."""
+    r = MauvRoute()
+    check(lib.mauv_get_route(ctypes.byref(r)), "get_route")
+    prev = {}
+    for k, v in fields.items():
+        if k == "reserved" or not hasattr(r, k):
+            raise ValueError(f"MauvRoute has no field {k!r}")
+        prev[k] = getattr(r, k)
+        setattr(r, k, int(v))
+    check(lib.mauv_set_route(ctypes.byref(r)), "set_route")
+    return prev
+
+
 def f32_math():
     """Arithmetic of the fp32 convs: "split" (default; exact three-way bf16 split of every
-    operand, six plane products on bf16 MFMA, fp32 accumulation), "split3" or "exact"
-    (v_mfma_f32_32x32x2_f32) — include/mauv.h mauv_set_f32_math."""
-    return _F32_NAMES[lib.mauv_set_f32_math(-1)]
+    operand, six plane products on bf16 MFMA, fp32 accumulation), "split1", "split3" or "exact"
+    (v_mfma_f32_32x32x2_f32) — include/mauv.h MauvRoute.f32_math."""
+    return _F32_NAMES[route()["f32_math"]]
 
 
 def set_f32_math(mode):
     """Select the fp32 conv arithmetic (process-wide); returns the previous mode."""
-    rc = lib.mauv_set_f32_math(F32_MATH[mode])
-    check(0 if rc >= 0 else rc, "set_f32_math")
-    return _F32_NAMES[rc]
+    return _F32_NAMES[set_route(f32_math=F32_MATH[mode])["f32_math"]]
+
+
+def _mode(mode, key):
+    """None: keep; True / False: 2 / 0 (big16, expand16) or 1 / 0; else the int."""
+    if mode is None:
+        return route()[key]
+    if mode is True:
+        return 2 if key in ("big16", "expand16") else 1
+    return 0 if mode is False else int(mode)
 
 
 def set_halo3(on):
-    """Route the 16-bit 3x3 / stride-1 64 -> 64 forwards through the LDS-row-image kernel
+    """Route the 16-bit 3x3 / stride-1 64 -> 64 convs through the LDS-row-image kernel
     (True, default) or the implicit GEMM (False); returns the previous setting."""
-    rc = lib.mauv_set_halo3(1 if on else 0)
-    check(0 if rc >= 0 else rc, "set_halo3")
-    return bool(rc)
+    return bool(set_route(halo3=1 if on else 0)["halo3"])
 
 
 def set_big16(mode=None, min_k=0):
     """Route 16-bit forwards through the 256-row LDS-DMA kernel: 1 (default) where it measured
     faster, 2 (or True) every forward it covers with K >= min_k, 0 (or False) none; None /
     min_k=0 keep.  Returns the previous mode (0 / 1 / 2)."""
-    m = -1 if mode is None else (2 if mode is True else (0 if mode is False else int(mode)))
-    rc = lib.mauv_set_big16(m, int(min_k))
-    check(0 if rc >= 0 else rc, "set_big16")
-    return rc
+    f = {"big16": _mode(mode, "big16")}
+    if min_k > 0:
+        f["big16_min_k"] = int(min_k)
+    return set_route(**f)["big16"]
 
 
 def set_expand16(mode=None):
     """Route 16-bit 1x1 / stride-1 expansion forwards (K = 64 / 128 / 256) through the
     weight-stationary kernel (conv_expand16.hip): 1 (default) where it measured faster, 2 (or
-    True) every shape it covers, 0 (or False) none (the implicit GEMM), None keep.  Returns the
-    previous mode (0 / 1 / 2)."""
-    m = -1 if mode is None else (2 if mode is True else (0 if mode is False else int(mode)))
-    rc = lib.mauv_set_expand16(m)
-    check(0 if rc >= 0 else rc, "set_expand16")
-    return rc
+    True) every shape it covers, 3 as 2 with 32-column waves at K = 128, 0 (or False) none (the
+    implicit GEMM), None keep.  Returns the previous mode."""
+    return set_route(expand16=_mode(mode, "expand16"))["expand16"]
 
 
 def set_haloc16(mode=None):
@@ -142,39 +166,26 @@ def set_haloc16(mode=None):
     row-image kernel (conv_haloc16.hip), and the stride-1 data gradients of the same shapes:
     1 / True (default, 32 x 64 wave tiles), 2 (64 x 64 wave tiles), 3 (the forwards only),
     0 / False (the implicit GEMM), None keep.  Returns the previous mode."""
-    rc = lib.mauv_set_haloc16(-1 if mode is None else int(mode))
-    check(0 if rc >= 0 else rc, "set_haloc16")
-    return rc
-
-
-def set_dma16(mode=None, min_k=0):
-    """Route 16-bit forwards through the 128 x 128 LDS-DMA tiles: 1 (default) where they measured
-    faster, 2 (or True) every forward they cover with K >= min_k, 0 (or False) none; None /
-    min_k=0 keep.  Returns the previous mode (0 / 1 / 2)."""
-    m = -1 if mode is None else (2 if mode is True else (0 if mode is False else int(mode)))
-    rc = lib.mauv_set_dma16(m, int(min_k))
-    check(0 if rc >= 0 else rc, "set_dma16")
-    return rc
+    return set_route(haloc16=_mode(mode, "haloc16"))["haloc16"]
 
 
 def set_reparam_kernels(sample_blk=None, bwd4=None):
     """Kernel forms of reparam_sample (block form, bit-identical) and reparam_bwd (16-byte slab
     loads); None keeps a setting.  Returns the previous (sample_blk, bwd4)."""
-    prev = lib.mauv_set_reparam_kernels(-1)
-    check(0 if prev >= 0 else prev, "set_reparam_kernels")
+    prev = route()["reparam_kernels"]
     sb = (prev & 1) if sample_blk is None else int(bool(sample_blk))
     b4 = (prev >> 1) & 1 if bwd4 is None else int(bool(bwd4))
-    rc = lib.mauv_set_reparam_kernels(sb | (b4 << 1))
-    check(0 if rc >= 0 else rc, "set_reparam_kernels")
+    set_route(reparam_kernels=sb | (b4 << 1))
     return bool(prev & 1), bool(prev & 2)
 
 
 def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_strides=None,
-               x_bn=None, stats=None, alg_cin=None):
+               x_bn=None, stats=None, alg_cin=None, ysh=None):
     """y[G][B*Ho*Wo][Cout] = conv(x'[g], w[g]) (+ bias[g]); w: [G][Cout][R][R][Cin].
     x_bn = (scale [G][Cin], shift [G][Cin], relu): x' = [relu](x*scale + shift) on load.
     stats = (mean, m2, cnt) partial buffers for the epilogue BN statistics (see
-    fwd_stat_blocks)."""
+    fwd_stat_blocks).  ysh ([Cout] fp32, 16-bit only): y is stored centred, y - ysh (the
+    consuming BN's running mean; bn_stats_finalize takes the same ysh)."""
     xs = None if x_strides is None else _LL5(*x_strides)
     sc, sh, rl = x_bn if x_bn is not None else (None, None, 0)
     sm, s2, sn = stats if stats is not None else (None, None, None)
@@ -185,15 +196,21 @@ def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_stri
     fl = 2.0 * G * B * Ho * Wo * Cout * R * R * (alg_cin or Cin)
     esz = w.element_size()
     nb = esz * (xg * B * H * W * Cin + G * Cout * R * R * Cin + G * B * Ho * Wo * Cout)
+    if ysh is not None and w.dtype not in H16:
+        raise ValueError("conv2d_fwd: ysh (centred storage) is for the 16-bit convs")
     if w.dtype in H16:
         assert bias is None, "16-bit convs carry no bias (the trunks' convs are bias=False)"
         _h16(w.dtype, w, y)
+        _f32(ysh)
+        if ysh is not None and ysh.numel() != Cout:
+            raise ValueError("conv2d_fwd: ysh needs Cout values")
         assert x.is_cuda and x.dtype == w.dtype and x.device.index == torch.cuda.current_device()
         with _Prof("fwd_" + str(w.dtype)[6:], fl, nb,
                    info=(G, B, H, W, Cin, Cout, R, stride, pad, x_bn is not None)):
             check(lib.mauv_conv2d_fwd_h16(H16[w.dtype], _p(x), xs, _p(sc), _p(sh), int(rl), _p(w),
                                           _p(y), G, B, H, W, Cin, Cout, R, R, stride, pad,
-                                          _p(sm), _p(s2), _p(sn), stream()), "conv2d_fwd_h16")
+                                          _p(sm), _p(s2), _p(sn), _p(ysh), stream()),
+                  "conv2d_fwd_h16")
         return
     _f32(w, y, bias)
     assert x.is_cuda and x.dtype == torch.float32 and x.device.index == torch.cuda.current_device()
@@ -204,18 +221,18 @@ def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_stri
 
 
 def conv2d_fwd_fold(y, scale, shift, res, res_bn, out, w, y1, G, B, H, W, Cin, Cout,
-                    stats=None, mask=None):
+                    stats=None, mask=None, ysh=None):
     """A bottleneck's 1x1 conv1 over the previous block's output formed on load
     (mauv_conv2d_fwd_fold_h16): out = relu(y*scale + shift + res'), res' = res or
     res*res_scale + res_shift (res_bn), is written through exactly as bn_apply would write it
     (mask: also its ReLU bits as bn_apply_mask writes them) and y1 = conv1x1(out) exactly as
-    conv2d_fwd would compute it.  True: done; False: the shape is outside the kernel and nothing
+    conv2d_fwd would compute it (ysh: y1 stored centred, as conv2d_fwd's).  True: done; False: the shape is outside the kernel and nothing
     ran (the caller runs bn_apply[_mask], then conv2d_fwd)."""
     rs, rh = res_bn if res_bn is not None else (None, None)
     if w.dtype not in H16:
         raise ValueError("conv2d_fwd_fold: 16-bit trunks only")
     _h16(w.dtype, y, res, out, w, y1)
-    _f32(scale, shift, rs, rh)
+    _f32(scale, shift, rs, rh, ysh)
     if mask is not None:
         _dev(torch.uint8, mask)
         if mask.numel() * 8 != out.numel():
@@ -229,7 +246,8 @@ def conv2d_fwd_fold(y, scale, shift, res, res_bn, out, w, y1, G, B, H, W, Cin, C
     with _Prof("fold_" + str(w.dtype)[6:], fl, nb, info=(G, B, H, W, Cin, Cout, 1, 1, 0, True)):
         rc = lib.mauv_conv2d_fwd_fold_h16(H16[w.dtype], _p(y), _p(scale), _p(shift), _p(res),
                                           _p(rs), _p(rh), _p(out), _p(mask), _p(w), _p(y1), G, B,
-                                          H, W, Cin, Cout, _p(sm), _p(s2), _p(sn), stream())
+                                          H, W, Cin, Cout, _p(sm), _p(s2), _p(sn), _p(ysh),
+                                          stream())
     if rc == 1:
         if PROFILE is not None:
             PROFILE.pop()
@@ -434,10 +452,14 @@ def bn_stats_workspace_floats(G, nblk, C):
 
 
 def bn_stats_finalize(G, nblk, C, pmean, pm2, pcnt, gamma, beta, run_mean, run_var, momentum,
-                      eps, ws, mean, invstd, scale, shift):
+                      eps, ws, mean, invstd, scale, shift, ysh=None):
+    """ysh: the centre the 16-bit forward stored y with (conv2d_fwd): mean / shift then describe
+    the stored values, the running mean the true one."""
+    _f32(ysh)
     check(lib.mauv_bn_stats_finalize(G, nblk, C, _p(pmean), _p(pm2), _p(pcnt), _p(gamma),
                                      _p(beta), _p(run_mean), _p(run_var), momentum, eps, _p(ws),
-                                     _p(mean), _p(invstd), _p(scale), _p(shift), stream()),
+                                     _p(mean), _p(invstd), _p(scale), _p(shift), _p(ysh),
+                                     stream()),
           "bn_stats_finalize")
 
 
@@ -604,20 +626,25 @@ def stem_im2col(x, B, C, H, W, R, stride, pad, Kp, cols):
                                stream()), "stem_im2col")
 
 
-def stem_fwd(cols, w, y, G, M, Kp, Cout, stats, alg_k):
+def stem_fwd(cols, w, y, G, M, Kp, Cout, stats, alg_k, ysh=None):
     """y[G][M][Cout] = cols[M][Kp] . w[g][Cout][Kp]^T for every g as one GEMM (weights stacked
     along N); stats = (mean, m2, cnt) partials as conv2d_fwd's.  alg_k: the stem's real
-    Cin*R*S (profiling counts algorithmic work, not the zero padding)."""
+    Cin*R*S (profiling counts algorithmic work, not the zero padding).  ysh: centred storage
+    (16-bit only, conv2d_fwd's)."""
     sm, s2, sn = stats
     fl = 2.0 * G * M * Cout * alg_k
     esz = w.element_size()
     nb = esz * (M * Kp + G * Cout * Kp + G * M * Cout)
     if w.dtype in H16:
         _h16(w.dtype, cols, w, y)
+        _f32(ysh)
         with _Prof("fwd_" + str(w.dtype)[6:], fl, nb, info=("stem", G, M, Kp, Cout)):
             check(lib.mauv_stem_fwd_h16(H16[w.dtype], _p(cols), _p(w), _p(y), G, M, Kp, Cout,
-                                        _p(sm), _p(s2), _p(sn), stream()), "stem_fwd_h16")
+                                        _p(sm), _p(s2), _p(sn), _p(ysh), stream()),
+                  "stem_fwd_h16")
         return
+    if ysh is not None:
+        raise ValueError("stem_fwd: ysh (centred storage) is for the 16-bit stems")
     _f32(cols, w, y)
     with _Prof("fwd", fl, nb, info=("stem", G, M, Kp, Cout)):
         check(lib.mauv_stem_fwd_f32(_p(cols), _p(w), _p(y), G, M, Kp, Cout, _p(sm), _p(s2),

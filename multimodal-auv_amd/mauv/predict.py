@@ -172,12 +172,34 @@ def mc_statistics(model, inputs, bathy, sss, num_mc, eps_h=1e-7, eps_pred=1e-8, 
                   group=None):
     """Fused MC statistics for one batch; with ``group`` (torch.distributed), the MC samples
     are sharded across ranks (each rank: full batch, ~num_mc/world samples; BN statistics
-    stay per-sample exactly as in the reference) and the sums all-reduced once."""
+    stay per-sample exactly as in the reference) and the sums all-reduced once.  Sharded, rank
+    r draws MC samples [s0 + sum of the lower ranks' counts, + its own count) of the rank-0
+    Philox stream (``shared_seed``, DistributedMC), s0 = the sample counter at the call (equal
+    on every rank of a rank-symmetric program): the union is exactly the single-rank draw, so
+    the statistics do not depend on the world size (up to the float64 sum order)."""
     B = inputs.shape[0]
     rank, world = (dist.get_rank(group), dist.get_world_size(group)) if group is not None \
         else (0, 1)
     local = local_mc_count(num_mc, rank, world)
     core = model if hasattr(model, "mc_forward") else unwrap(model)
+    st = root_state(unwrap(model))
+    shard = group is not None and world > 1 and getattr(st, "shared_seed", None) is not None
+    if shard:
+        s0, seed = st.offset, st.seed
+        st.seed = st.shared_seed
+        st.offset = s0 + sum(local_mc_count(num_mc, q, world) for q in range(rank))
+        try:
+            return _mc_statistics_local(model, core, inputs, bathy, sss, num_mc, local, eps_h,
+                                        eps_pred, chunk, group)
+        finally:
+            st.seed, st.offset = seed, s0 + num_mc
+    return _mc_statistics_local(model, core, inputs, bathy, sss, num_mc, local, eps_h, eps_pred,
+                                chunk, group)
+
+
+def _mc_statistics_local(model, core, inputs, bathy, sss, num_mc, local, eps_h, eps_pred, chunk,
+                         group):
+    B = inputs.shape[0]
     if chunk is None:
         dt = root_state(unwrap(model)).trunk_dtype()
         chunk = mc_chunk(model, B, max(local, 1), dtype=dt, device=inputs.device,
@@ -212,12 +234,13 @@ def multimodal_predict_and_save(multimodal_model, dataloader, device, csv_path,
                                 model_type="multimodal"):
     """inference/predictors.py:9-97 (model kept in .train(): BN uses batch statistics; MC
     passes under torch.amp.autocast as predictors.py:55 -> f16 trunks on a ROCm device)."""
-    from .train import loop_device, is_writer, _NullFile, _tile_to
+    from .train import loop_device, is_writer, _NullFile, _tile_to, refresh_centres_on_gpu
     device = torch.device(loop_device(multimodal_model, device))
     amp_device = "cuda" if device.type == "cuda" else "cpu"
     group = _shard_group(multimodal_model)
     writer = is_writer(multimodal_model)   # MC-sharded: every rank holds the same rows
     multimodal_model.train()
+    refresh_centres_on_gpu(multimodal_model)
     logging.info(f"CSV will be saved to: {csv_path}")
     with (open(csv_path, mode="w", newline="") if writer else _NullFile()) as fh:
         w = csv.writer(fh)

@@ -324,6 +324,16 @@ def _patch_tag(t, kind):
     return t.replace("patch_", "").replace(f"_{kind}", "") if t else "none"
 
 
+def refresh_centres_on_gpu(model):
+    """engine.refresh_centres for a model on a ROCm device (the 16-bit storage centres follow
+    the running means once per training epoch / predictor call)."""
+    from .engine import refresh_centres
+    core = unwrap(model)
+    p = next(core.parameters(), None)
+    if p is not None and p.is_cuda:
+        refresh_centres(core)
+
+
 def train_multimodal_model(multimodal_model, dataloader, criterion, optimizer, epoch, device,
                            model_type, total_num_epochs, num_mc, sum_writer,
                            bathy_patch_type=None, sss_patch_type=None, csv_path=""):
@@ -331,6 +341,7 @@ def train_multimodal_model(multimodal_model, dataloader, criterion, optimizer, e
     from .checkpointing import save_model
     multimodal_model.train()
     device = loop_device(multimodal_model, device)
+    refresh_centres_on_gpu(multimodal_model)
     writer = is_writer(multimodal_model)
     csv_path = str(Path(csv_path))
     sss_tag, bathy_tag = _patch_tag(sss_patch_type, "sss"), _patch_tag(bathy_patch_type, "bathy")
@@ -505,6 +516,7 @@ def train_unimodal_model(model, dataloader, criterion, optimizer, epoch, total_n
     model.train()
     device = loop_device(model, device)
     model.to(device)
+    refresh_centres_on_gpu(model)
     kl_w = kl_weight_for(epoch, total_num_epochs)
     new_file = not os.path.isfile(csv_path)
     try:

@@ -45,6 +45,21 @@ class EpsBridge:
         assert len(lst) >= G, (self.m_names[id(module)], name, len(lst), G)
         return torch.stack(lst[:G]).cuda().contiguous()
 
+    def sequential(self):
+        """A provider that hands out each layer's recorded draws in order across calls: MC
+        chunks (mc_statistics with chunk < N) get passes 0..c-1, c..2c-1, ... as the oracle's
+        sequential loop consumed them (``provider`` restarts at pass 0 on every call)."""
+        used = {}
+
+        def prov(module, name, G):
+            k = (self.m_names[id(module)], name)
+            i = used.get(k, 0)
+            lst = self.store[k]
+            assert len(lst) >= i + G, (k, len(lst), i, G)
+            used[k] = i + G
+            return torch.stack(lst[i:i + G]).cuda().contiguous()
+        return prov
+
 
 def oracle64(o, store, fn):
     """Run ``fn(o64)`` on a float64 copy of the oracle, replaying the recorded epsilons

@@ -49,23 +49,41 @@ def test_library_reports_gfx950_only():
 
 def test_abi_version_and_error_string():
     from mauv._lib import lib
-    assert lib.mauv_abi_version() == 3
+    assert lib.mauv_abi_version() == 4
     assert isinstance(lib.mauv_last_error(), bytes)
 
 
-def test_f32_math_mode_host_switch():
-    """mauv_set_f32_math is host-only state: default split (6), settable, bad modes rejected."""
-    from mauv._lib import lib
+def test_route_host_record():
+    """MauvRoute (include/mauv.h) is host-only state: the measured defaults, get / set round
+    trips through the ctypes Structure, and an invalid field changes nothing."""
+    from mauv import ops
+    from mauv._lib import lib, MauvRoute
+    assert ctypes.sizeof(MauvRoute) == 16 * 4
+    r = ops.route()
     if "MAUV_F32_MATH" not in os.environ:
-        assert lib.mauv_set_f32_math(-1) == 6
-    prev = lib.mauv_set_f32_math(0)
+        assert r["f32_math"] == 6
+    assert (r["halo3"], r["big16"], r["big16_min_k"], r["haloc16"], r["expand16"],
+            r["reparam_kernels"]) == (1, 1, 512, 1, 1, 3)
+    ops.set_f32_math("exact")
     try:
-        assert lib.mauv_set_f32_math(-1) == 0
-        assert lib.mauv_set_f32_math(3) == 0
-        assert lib.mauv_set_f32_math(7) < 0 and b"mode" in lib.mauv_last_error()
-        assert lib.mauv_set_f32_math(-1) == 3
+        assert ops.f32_math() == "exact"
+        assert ops.set_f32_math("split3") == "exact"
+        with pytest.raises(RuntimeError, match="f32_math"):
+            ops.set_route(f32_math=7)
+        with pytest.raises(RuntimeError, match="haloc16"):
+            ops.set_route(halo3=0, haloc16=9)   # rejected as a whole: halo3 stays 1
+        assert ops.route()["halo3"] == 1 and ops.f32_math() == "split3"
+        assert ops.set_expand16(3) == 1 and ops.set_expand16(None) == 3
+        assert ops.set_big16(True, 256) == 1 and ops.route()["big16_min_k"] == 256
+        with pytest.raises(ValueError):
+            ops.set_route(dma16=1)
+        bad = MauvRoute()
+        assert lib.mauv_get_route(ctypes.byref(bad)) == 0
+        bad.reparam_kernels = 4
+        assert lib.mauv_set_route(ctypes.byref(bad)) < 0 and b"reparam" in lib.mauv_last_error()
     finally:
-        lib.mauv_set_f32_math(prev)
+        ops.set_route(**r)
+    assert ops.route() == r
 
 
 def test_state_dict_compatible_with_reference_layout():

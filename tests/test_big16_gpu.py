@@ -17,26 +17,40 @@ DTYPES = [torch.bfloat16, torch.float16]
 ULP = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11}
 
 
-def _run(ops, x, w, G, B, H, W, Cin, Cout, R, st, pd, x_bn, big):
-    """big: "big16" (256-row tiles), "dma128" (128 x 128 four-wave tiles) or False (conv_pipe16)."""
+GUARD = 4096   # sentinel elements past the end of every output buffer
+
+
+def _guarded(n, dtype):
+    """A buffer of n elements followed by GUARD sentinel elements (NaN), as one allocation: the
+    kernels get the first n, and any write past them shows in the tail."""
+    buf = torch.full((n + GUARD,), float("nan"), device=dev, dtype=dtype)
+    return buf, buf[:n]
+
+
+def _run(ops, x, w, G, B, H, W, Cin, Cout, R, st, pd, x_bn, big, check_tail=True):
+    """big: "big16" (256-row tiles) or False (conv_pipe16).  Every output and statistics buffer
+    carries a NaN tail that must survive the launch (no write past its end)."""
     prev = ops.set_big16(2 if big in (True, "big16") else 0, 512)
-    prevd = ops.set_dma16(2 if big == "dma128" else 0, 512)
     try:
         Ho, Wo = ops.out_hw(H, R, st, pd), ops.out_hw(W, R, st, pd)
-        y = torch.full((G, B, Ho, Wo, Cout), float("nan"), device=dev, dtype=x.dtype)
         nblk = ops.fwd_stat_blocks(G, B, H, W, Cin, Cout, R, st, pd)
-        pm = torch.full((G, nblk, Cout), float("nan"), device=dev)
-        pm2 = torch.full((G, nblk, Cout), float("nan"), device=dev)
-        pc = torch.full((G, nblk), float("nan"), device=dev)
+        bufs = [_guarded(G * B * Ho * Wo * Cout, x.dtype), _guarded(G * nblk * Cout, torch.float32),
+                _guarded(G * nblk * Cout, torch.float32), _guarded(G * nblk, torch.float32)]
+        y = bufs[0][1].view(G, B, Ho, Wo, Cout)
+        pm, pm2 = bufs[1][1].view(G, nblk, Cout), bufs[2][1].view(G, nblk, Cout)
+        pc = bufs[3][1].view(G, nblk)
         ops.conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, st, pd, x_bn=x_bn, stats=(pm, pm2, pc))
         torch.cuda.synchronize()
+        if check_tail:
+            for full, body in bufs:
+                assert torch.isnan(full[body.numel():].float()).all().item(), \
+                    (big, "write past the end of an output buffer")
         return y, pm, pm2, pc
     finally:
         ops.set_big16(prev)
-        ops.set_dma16(prevd)
 
 
-@pytest.mark.parametrize("kern", ["big16", "dma128"])
+@pytest.mark.parametrize("kern", ["big16"])
 @pytest.mark.parametrize("dt", DTYPES, ids=["bf16", "f16"])
 @pytest.mark.parametrize("G,B,H,W,Cin,Cout,R,st,bn", [
     (2, 3, 8, 8, 512, 256, 3, 1, "relu"),     # layer-4-like 3x3, 256-wide tiles, ragged M
@@ -75,20 +89,26 @@ def test_big16_bit_identical_to_implicit_gemm(G, B, H, W, Cin, Cout, R, st, bn, 
     assert err <= 2 * ULP[dt] * ref.abs().max().item(), err
 
 
-def test_probe_fault_shape_through_every_forward_kernel():
-    """The shape at which gpurun_out/probe1.log faulted (G = 5, M = 16,384 per group as B = 64,
-    H = 256, W = 1; 1x1 1024 -> 512): the fault was torch.bmm's (hipblasLtMatmul returned
-    HIPBLAS_STATUS_INTERNAL_ERROR on this bf16 shape and its fallback raised the illegal address,
-    profiles/round5/probe_fault_trace.log).  Every 16-bit forward kernel of this
-    library at exactly that shape against fp32 torch on the CPU; no vendor GEMM is called."""
+@pytest.mark.parametrize("Cin,Cout,H", [(2048, 512, 64), (512, 2048, 64), (1024, 512, 256)],
+                         ids=["l4c1", "l4c3", "l4.0c1"])
+def test_probe_fault_shapes_through_every_forward_kernel(Cin, Cout, H):
+    """The three shapes of the round-5 probe run that ended in an illegal address (G = 5,
+    M = 16,384 rows per group as B = 64, H x W = H x 1 — profiles/round5/probe_fault_trace.log:
+    torch.bmm's hipblasLtMatmul returned HIPBLAS_STATUS_INTERNAL_ERROR on the third and its
+    fallback raised the fault; the probe's own kernels had run the first two).  Every 16-bit
+    forward kernel of this library at exactly those shapes, against fp32 torch on the CPU, with a
+    NaN tail behind every output buffer that must survive (an out-of-bounds write by
+    a kernel launched earlier in that process would have looked the same); no vendor GEMM is
+    called here.  tools/bmm_fault_probe.py runs torch.bmm alone at the third shape in a fresh
+    process."""
     from mauv import ops
-    G, B, H, W, Cin, Cout = 5, 64, 256, 1, 1024, 512
+    G, B, W = 5, 16384 // H, 1
     g = torch.Generator().manual_seed(3)
     A = (torch.rand(G, B * H * W, Cin, generator=g) * 2 - 1).to(torch.bfloat16)
     Wt = (torch.rand(G, Cout, Cin, generator=g) * 2 - 1).to(torch.bfloat16)
     ref = torch.stack([A[i].float() @ Wt[i].float().t() for i in range(G)])
     x, w = A.to(dev), Wt.reshape(G, Cout, 1, 1, Cin).to(dev)
-    for kern in (False, "big16", "dma128"):
+    for kern in (False, "big16"):
         y, _, _, _ = _run(ops, x, w, G, B, H, W, Cin, Cout, 1, 1, 0, None, kern)
         err = ((y.float().cpu().reshape(G, -1, Cout) - ref).abs().max() / ref.abs().max()).item()
         assert err <= 2 * ULP[torch.bfloat16], (kern, err)
@@ -101,6 +121,3 @@ def test_big16_switch_round_trip():
     assert ops.set_big16(True) == 0
     assert ops.set_big16(prev) == 2
     assert ops.set_big16(None) == 1
-    prev = ops.set_dma16(False)
-    assert prev == 1
-    assert ops.set_dma16(True) == 0 and ops.set_dma16(prev) == 2 and ops.set_dma16(None) == 1

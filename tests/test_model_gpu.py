@@ -371,6 +371,90 @@ def test_predict_uncertainty_parity(N, chunk):
     np.testing.assert_allclose(st["aleatoric"].cpu().numpy(), alea_o.numpy(), atol=1e-5)
 
 
+def test_predict_fp32_fitted_full_size():
+    """the fp32 predictor statistics at the configs[3] tile sizes (224 optical /
+    256 sonar), B=16, N=8, on a model fitted to the batch (tests.helpers.fit_model: the class
+    depends on the input and the softmax is peaked, logits up to tens — at random init the
+    probabilities are near uniform and an entropy check is weak), through mc_statistics with
+    chunk < N (the accumulate path), against the CPU oracle's predictors.py:73-84 maths and the
+    evaluation loop's predictive entropy (train/multimodal.py:305-306, eps 1e-8), with a float64
+    run of the oracle printed beside both.
+
+    Bars: aleatoric and predictive entropy |d| <= 1e-5 from the float64
+    truth (and within 2x the CPU oracle's own distance from it), variance |d| <= 1e-6 + 1e-3 |ref|
+    from float64 (2e-6 + 1e-3 |ref| from the CPU oracle: two fp32 errors), identical argmax,
+    logits |d| <= 1e-4 + 1e-4 |ref| from the CPU oracle."""
+    from mauv.engine import root_state
+    from mauv.predict import mc_statistics
+    from tests.helpers import fit_model, oracle_replay
+    B, N = 16, 8
+    o, m = build_pair()
+    batch = make_batches(SEED_DATA + 1, 1, B=B, S_opt=224, S_son=256)[0]
+    x, b, s = batch["main_image"], batch["bathy_image"], batch["sss_image"]
+    labels = torch.randint(0, 7, (B,), generator=torch.Generator().manual_seed(3))
+    fit_model(m, *_cuda(x, b, s), labels.cuda())
+    o.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    o_pre = copy.deepcopy(o)
+    bridge = EpsBridge(o, m, 7)
+    with bridge:
+        pred_o, var_o, alea_o, P = loops_ref.predict_batch(o, x, b, s, N)
+    bridge.collect()
+
+    def pent(P):   # train/multimodal.py:305-306: entropy of the MC-mean probability, eps 1e-8
+        pm = P.double().mean(0)
+        return -(pm * torch.log(pm + 1e-8)).sum(-1)
+
+    def run64(mm):
+        xs = [t.cuda().double() for t in (x, b, s)]
+        with torch.no_grad():
+            lg = torch.stack([mm(*xs) for _ in range(N)])
+        P64 = torch.softmax(lg, -1)
+        return lg.cpu(), loops_ref.mc_uncertainty_from_probs(P64.cpu()), P64.cpu()
+    _, (lg64, (pred64, var64, alea64), P64) = oracle_replay(o_pre, bridge.store, run64,
+                                                            dtype=torch.float64, device="cuda")
+    _, lg32 = oracle_replay(o_pre, bridge.store, lambda mm: torch.stack(
+        [mm(x, b, s) for _ in range(N)]).detach())
+    root_state(m).eps_provider = bridge.sequential()
+    with torch.no_grad():
+        st = mc_statistics(m, *_cuda(x, b, s), N, chunk=3)
+    root_state(m).eps_provider = bridge.provider
+    with torch.no_grad():
+        lgh = m.mc_forward(*_cuda(x, b, s), N).double().cpu()
+    pe_o, pe_64 = pent(P), pent(P64)
+    h = {k: st[k].double().cpu() for k in ("aleatoric", "var", "predictive_entropy")}
+    d = {
+        "logits": ((lgh - lg32.double()).abs().max().item(),
+                   (lg32.double() - lg64).abs().max().item(), (lgh - lg64).abs().max().item()),
+        "aleatoric": ((h["aleatoric"] - alea_o.double()).abs().max().item(),
+                      (alea_o.double() - alea64).abs().max().item(),
+                      (h["aleatoric"] - alea64).abs().max().item()),
+        "pred_entropy": ((h["predictive_entropy"] - pe_o).abs().max().item(),
+                         (pe_o - pe_64).abs().max().item(),
+                         (h["predictive_entropy"] - pe_64).abs().max().item()),
+        "variance": ((h["var"] - var_o.double()).abs().max().item(),
+                     (var_o.double() - var64).abs().max().item(),
+                     (h["var"] - var64).abs().max().item()),
+    }
+    print(f"\nfp32 predictor 224/256 B={B} N={N} fitted: {len(set(pred_o.tolist()))} classes, "
+          f"|logit| <= {lg32.abs().max():.1f}, aleatoric {alea_o.min():.4f}..{alea_o.max():.4f}")
+    for k, (hv, cv, h64) in d.items():
+        print(f"  {k:13s} max |d|: HIP vs CPU oracle {hv:.3e}; CPU oracle vs float64 {cv:.3e}; "
+              f"HIP vs float64 {h64:.3e}")
+    assert len(set(pred_o.tolist())) >= 3
+    assert torch.equal(st["pred"].cpu(), pred_o) and torch.equal(pred_o, pred64)
+    assert ((lgh - lg32.double()).abs() <= 1e-4 + 1e-4 * lg32.double().abs()).all(), d["logits"]
+    # the entropies against the float64 truth: SURVEY's 1e-5, and no further from it than 2x the
+    # reference's own fp32 CPU path (HIP vs the CPU oracle differ by the SUM of the two fp32
+    # errors: 1.5e-5 for the predictive entropy on this fitted model, HIP 7.1e-6 and the CPU
+    # oracle 8.2e-6 from float64 — profiles/round6/predict_fp32_fitted.log)
+    for k in ("aleatoric", "pred_entropy"):
+        hv, cv, h64 = d[k]
+        assert h64 <= 1e-5 and h64 <= 2 * cv + 1e-6, (k, d[k])
+    assert ((h["var"] - var64).abs() <= 1e-6 + 1e-3 * var64.abs()).all(), d["variance"]
+    assert ((h["var"] - var_o.double()).abs() <= 2e-6 + 1e-3 * var_o.double().abs()).all(), \
+        d["variance"]
+
+
 def test_full_resolution_forward():
     """224 optical + 256 sonar tiles (BASELINE shapes), B=2, N=2: logits parity."""
     from mauv.engine import root_state

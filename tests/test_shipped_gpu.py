@@ -112,9 +112,70 @@ def _h16_checks(m, res, tag):
     print(f"  gradient arena: finite, {_arena_ok(m):.3f} of the values non-zero")
 
 
+def _float64_truth(m, o32, lh, lo, B, S_opt, S_son, N):
+    """the configs[1] step judged against a float64 run of the oracle (on the
+    GPU, same weights and epsilons), not only against the fp32 oracle.  HIP's error must be as
+    small as the fp32 oracle's: per-tensor max-relative error median / p90 / max within 1.5x /
+    2x / 2x (+1e-4) of the fp32 oracle's (the bar tests/test_model_gpu.py applies at B = 2-3),
+    and each trunk's whole-gradient relative L2 error within 2x of the fp32 oracle's (+1e-6)."""
+    import gc
+    from tests.helpers import grad_error_profile
+    batch = make_batches(SEED_DATA, 1, B=B, S_opt=S_opt, S_son=S_son)[0]
+    x, b, s, y = batch["main_image"], batch["bathy_image"], batch["sss_image"], batch["label"]
+    tiny = make_batches(SEED_DATA, 1, B=1, S_opt=64, S_son=64)[0]
+    # the same epsilon record _step made (EpsBridge over the same layers and seed)
+    o, _ = build_pair()
+    bridge = EpsBridge(o, m, 5)
+    with bridge, torch.no_grad():
+        for _ in range(N):
+            o(tiny["main_image"], tiny["bathy_image"], tiny["sss_image"])
+    bridge.collect()
+
+    def loss64(mm):
+        xs = [t.cuda().double() for t in (x, b, s)]
+        lg = torch.stack([mm(*xs) for _ in range(N)])
+        loss = F.cross_entropy(lg.mean(0), y.cuda()) + bayes_ref.get_kl_loss(mm) / B * 0.5
+        loss.backward()
+        return lg.detach(), loss.detach()
+    gc.collect()
+    torch.cuda.empty_cache()
+    o64, (l64, loss_64) = oracle_replay(o, bridge.store, loss64, dtype=torch.float64,
+                                        device="cuda")
+    hip_p, cpu_p, tru_p = list(m.parameters()), list(o32.parameters()), list(o64.parameters())
+    h, c = grad_error_profile(hip_p, cpu_p, tru_p)
+    print(f"  vs float64: per-tensor max-rel gradient error median/p90/max HIP "
+          f"{h[0]:.3e}/{h[1]:.3e}/{h[2]:.3e}, fp32 oracle {c[0]:.3e}/{c[1]:.3e}/{c[2]:.3e}")
+    mp = list(m.named_parameters())
+    for tr in TRUNKS + ("head",):
+        pick = (lambda n, g=tr: n.startswith(g + ".")) if tr != "head" else \
+            (lambda n: not n.split(".")[0].endswith("_feat"))
+        eh, ec = [], []
+        for (n, ph), pc, pt in zip(mp, cpu_p, tru_p):
+            if pick(n) and pt.grad is not None:
+                t = pt.grad.detach()
+                eh.append(((ph.grad.detach().double() - t).norm() ** 2, t.norm() ** 2))
+                ec.append(((pc.grad.detach().double() - t).norm() ** 2).item())
+        num_h = sum(e[0].item() for e in eh)
+        den = sum(e[1].item() for e in eh)
+        rh, rc = (num_h / den) ** 0.5, (sum(ec) / den) ** 0.5
+        print(f"  {tr:17s} whole-gradient rel L2 error vs float64: HIP {rh:.3e} fp32 oracle "
+              f"{rc:.3e}")
+        assert rh <= 2.0 * rc + 1e-6, (tr, rh, rc)
+    dl_h = (lh.double() - l64).abs().max().item()
+    dl_c = (lo.double() - l64).abs().max().item()
+    print(f"  logits vs float64: HIP {dl_h:.3e} fp32 oracle {dl_c:.3e}")
+    assert dl_h <= 2.0 * dl_c + 1e-6 * max(1.0, l64.abs().max().item())
+    assert h[0] <= 1.5 * c[0] + 1e-4, (h, c)
+    assert h[1] <= 2.0 * c[1] + 1e-4, (h, c)
+    assert h[2] <= 2.0 * c[2] + 1e-4, (h, c)
+
+
 def test_configs1_fp32_step_b64():
     m, o32, res = _step(torch.float32, 64, 224, 256, 2, oracle_grads=True)
     _fp32_checks(m, o32, res, "configs[1] fp32 B=64 224/256 N=2")
+    lh, lo = res["hip"][0], res["fp32"][0]
+    del res
+    _float64_truth(m, o32, lh, lo, 64, 224, 256, 2)
 
 
 def test_configs2_bf16_step_b64():
