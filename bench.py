@@ -197,7 +197,7 @@ def pmc_traffic(family="fp32"):
         return None, None, None
     with open(files[-1]) as f:
         d = json.load(f)
-    return d["bytes_per_launch"], os.path.relpath(files[-1], REPO), d.get("library_sha16")
+    return d, os.path.relpath(files[-1], REPO), d.get("library_sha16")
 
 
 def library_sha16():
@@ -255,15 +255,23 @@ def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic="fp32", suffix="",
     tot_ms = sum(v[2] for v in by.values())
     n = sum(v[0] for v in by.values())
     achieved = tot_fl / (tot_ms * 1e-3) / 1e12
-    traffic, tsrc, tsha = pmc_traffic(traffic) if traffic else (None, None, None)
+    pmc, tsrc, tsha = pmc_traffic(traffic) if traffic else (None, None, None)
+    traffic = pmc["bytes_per_launch"] if pmc else None
+    pmc_launches = pmc.get("launches") if pmc else None
+    pfold = (pmc or {}).get("per_family", {}).get("conv_fold16")
     lsha = library_sha16()
+    alg = nbytes / max(n, 1)
     return {
         "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
         "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC)",
         "traffic_source": tsrc, "traffic_library_sha16": tsha, "library_sha16": lsha,
         "traffic_matches_library": tsha == lsha,
-        "algorithmic_bytes_per_launch": round(nbytes / max(n, 1)),
+        "algorithmic_bytes_per_launch": round(alg),
+        # the PMC summary covers the same launch set as `launches` (the fold family apart): the
+        # ratio is then HBM bytes moved per algorithmic byte of this family
+        "traffic_launches": pmc_launches,
+        "traffic_ratio": round(traffic / alg, 3) if traffic and alg else None,
         "kernel": kernel,
         "launches": n, "avg_launch_us": round(tot_ms * 1e3 / max(n, 1), 2),
         "algorithmic_gflop_per_launch": round(tot_fl / max(n, 1) / 1e9, 3),
@@ -280,6 +288,11 @@ def roofline_step(step_fn, peak=FP32_MFMA_PEAK_TF, traffic="fp32", suffix="",
             "launches": fold[0], "gflop": round(fold[1] / 1e9, 1), "ms": round(fold[3], 2),
             "algorithmic_gbytes": round(fold[2] / 1e9, 2),
             "tbytes_per_s": round(fold[2] / (fold[3] * 1e-3) / 1e12, 2),
+            "algorithmic_bytes_per_launch": round(fold[2] / fold[0]),
+            "traffic": round(pfold["bytes_per_launch"]) if pfold else None,
+            "traffic_launches": pfold["launches"] if pfold else None,
+            "traffic_ratio": round(pfold["bytes_per_launch"] / (fold[2] / fold[0]), 3)
+            if pfold else None,
             "note": "conv1 launches that also form the previous block output (bn3 + residual "
                     "+ ReLU, DESIGN.md 2.20); not in achieved / frac / launches above"},
     }
@@ -335,6 +348,8 @@ def main():
     ap.add_argument("--sonar", type=int, default=256)
     ap.add_argument("--infer-batch", type=int, default=256)
     ap.add_argument("--infer-mc", type=int, default=100)
+    ap.add_argument("--infer-batches", type=int, default=3,
+                    help="distinct batches each inference leg times (main.py's shape: 32)")
     ap.add_argument("--no-infer", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -607,10 +622,12 @@ def main():
         progress("inference leg")
         from mauv.predict import multimodal_predict_and_save
         opt.zero_grad(set_to_none=True)
-        xi, bi, si, _ = synthetic_batch(args.infer_batch, args.optical, args.sonar, dev, 99)
+        nib = max(1, args.infer_batches)
+        loader = []
+        for j in range(nib):
+            xi, bi, si, _ = synthetic_batch(args.infer_batch, args.optical, args.sonar, dev, 99 + j)
+            loader.append((xi, bi, si, [f"tile{j}_{i}" for i in range(args.infer_batch)]))
         group = dist.group.WORLD if world > 1 else None
-        names = [f"tile{i}" for i in range(args.infer_batch)]
-        loader = [(xi, bi, si, names)]
         pred_csv = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mauv_bench_pred_r{rank}.csv")
         hw = [(args.optical, args.optical), (args.sonar, args.sonar), (args.sonar, args.sonar)]
 
@@ -627,13 +644,13 @@ def main():
         # its own torch.amp.autocast (predictors.py:55 -> f16 trunks), MC samples sharded
         # across ranks under DistributedMC, fused statistics, CSV rows written
         chunk = warm(torch.float16)
-        multimodal_predict_and_save(model, loader, dev, pred_csv,
+        multimodal_predict_and_save(model, loader[:1], dev, pred_csv,
                                     num_mc_samples=max(world, 2) * chunk)
         di = timed(lambda: multimodal_predict_and_save(model, loader, dev, pred_csv,
                                                        num_mc_samples=args.infer_mc), 1)
-        infer = {"value": round(args.infer_mc * args.infer_batch / di, 2),
+        infer = {"value": round(args.infer_mc * args.infer_batch * nib / di, 2),
                  "unit": "MC-samples/s", "batch": args.infer_batch, "num_mc": args.infer_mc,
-                 "ms_per_batch": round(di * 1e3, 1), "mc_chunk": chunk,
+                 "batches": nib, "ms_per_batch": round(di / nib * 1e3, 1), "mc_chunk": chunk,
                  "sharding": "mc" if world > 1 else "none",
                  "path": "Multimodal_AUV.inference.predictors.multimodal_predict_and_save",
                  "dtype": "f16 trunks (the predictor's own torch.amp.autocast, predictors.py:55)"}
@@ -641,11 +658,12 @@ def main():
             # fp32 trunks: the same MC statistics with autocast off
             chunk32 = warm(torch.float32)
             with torch.no_grad():
-                mc_statistics(model, xi, bi, si, max(world, 2) * chunk32, group=group)
-                d32 = timed(lambda: mc_statistics(model, xi, bi, si, args.infer_mc,
-                                                  group=group), 1)
-            infer["fp32"] = {"value": round(args.infer_mc * args.infer_batch / d32, 2),
-                             "unit": "MC-samples/s", "ms_per_batch": round(d32 * 1e3, 1),
+                mc_statistics(model, *loader[0][:3], max(world, 2) * chunk32, group=group)
+                d32 = timed(lambda: [mc_statistics(model, *lb[:3], args.infer_mc, group=group)
+                                     for lb in loader], 1)
+            infer["fp32"] = {"value": round(args.infer_mc * args.infer_batch * nib / d32, 2),
+                             "unit": "MC-samples/s", "batches": nib,
+                             "ms_per_batch": round(d32 / nib * 1e3, 1),
                              "mc_chunk": chunk32,
                              "dtype": "fp32 trunks (split-fp32 convs), autocast off",
                              "path": "mauv.predict.mc_statistics"}
@@ -658,8 +676,8 @@ def main():
         # :310) over 32 batches — both through the drop-in multimodal_predict_and_save under
         # its own f16 autocast
         infer_sweep = {}
-        legs = [(f"sonar{S}", args.infer_sweep_batch, S, args.infer_sweep_mc, 1)
-                for S in (128, 512)]
+        legs = [(f"sonar{S}", args.infer_sweep_batch, S, args.infer_sweep_mc,
+                 max(1, args.infer_batches)) for S in (128, 512)]
         legs.append(("main_py_b8_mc12", 8, args.sonar, 12, 32))
         for name, Bi, S, Ni, nb in legs:
             progress(f"infer_sweep {name}")

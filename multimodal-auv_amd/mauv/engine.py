@@ -61,7 +61,9 @@ BWD_PARTIALS_F32 = True
 # spread |y - mean| instead of |y|: the largest of the path's rounding points (DESIGN.md
 # §2.31).  Exact in real arithmetic; c changes only when refreshed, so a forward's result stays
 # a function of the weights, samples and inputs between refreshes.  Test hook like FOLD.
-CENTRE_Y = True
+CENTRE_Y = os.environ.get("MAUV_CENTRE_Y", "1") == "1"
+# a channel is centred where |running mean| > this many running standard deviations
+CENTRE_MIN_Z = float(os.environ.get("MAUV_CENTRE_MIN_Z", "1"))
 _STREAMS = {}
 
 
@@ -156,7 +158,10 @@ class RootState:
         self._centre_views = {}
 
     def refresh_centres(self):
-        """Copy every tracked BatchNorm's running mean into the centre buffer (one launch)."""
+        """Every tracked BatchNorm's centre from its running statistics: the running mean where
+        it exceeds CENTRE_MIN_Z running standard deviations, else 0 — centring pays where a
+        channel's mean dominates its spread (the stored magnitude |y| ~ |mean| + std falls to
+        ~std) and only adds the running mean's staleness elsewhere."""
         if not self.bns:
             return
         dev = self.bns[0].running_mean.device
@@ -170,8 +175,11 @@ class RootState:
                 off += c
             self._centre_views = views
         with torch.no_grad():
-            torch._foreach_copy_([self._centre_views[id(bn)] for bn in self.bns],
-                                 [bn.running_mean.detach() for bn in self.bns])
+            rm = torch.cat([bn.running_mean.detach().float() for bn in self.bns])
+            rv = torch.cat([bn.running_var.detach().float() if bn.running_var is not None
+                            else torch.zeros_like(bn.running_mean) for bn in self.bns])
+            keep = rm.abs() > CENTRE_MIN_Z * rv.clamp(min=0).sqrt()
+            torch.where(keep, rm, torch.zeros_like(rm), out=self._centre_buf)
 
     def centre(self, bn):
         """bn's centre (the first call builds the buffer from the current running means)."""

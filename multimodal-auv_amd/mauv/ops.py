@@ -279,8 +279,17 @@ def conv2d_bwd_data(dy, w, dx, G, B, H, W, Cin, Cout, R, stride, pad, addend=Non
     fl = 2.0 * G * B * Ho * Wo * Cout * R * R * Cin
     nb = w.element_size() * (G * B * Ho * Wo * Cout + G * Cout * R * R * Cin +
                              G * B * H * W * Cin * (1 + (addend is not None) + bool(accumulate)))
+    # kernel launches: one per output-parity class with pixels, except the tapless classes of an
+    # accumulating call without addend or partials (they add nothing and are not launched:
+    # the stride-2 1x1 downsample's 3 of 4, conv_gemm.hip / conv_gemm16.hip)
+    skip_tapless = bool(accumulate) and addend is None and bn is None
+
+    def taps(p):
+        r0 = (p + pad) % stride
+        return (R - r0 + stride - 1) // stride if r0 < R else 0
     nl = sum(1 for ph in range(stride) for pw in range(stride)
-             if (H - ph + stride - 1) // stride > 0 and (W - pw + stride - 1) // stride > 0)
+             if (H - ph + stride - 1) // stride > 0 and (W - pw + stride - 1) // stride > 0
+             and not (skip_tapless and taps(ph) * taps(pw) == 0))
     if w.dtype in H16:
         _h16(w.dtype, dy, w, dx, addend, b.get("y"), b.get("out"))
         _f32(b.get("scale"), b.get("shift"), b.get("mean"), b.get("invstd"), b.get("p1"),

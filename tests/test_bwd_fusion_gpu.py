@@ -55,8 +55,10 @@ def test_fp32_bn_partials_from_data_gradient_epilogue(S, B, monkeypatch):
     """engine.BWD_PARTIALS_F32: in the fp32 step the BN-backward partial sums
     of bn2 / bn1 and of the previous block's bn3 come from the LDS-staged epilogue of the data
     gradient that produces their output gradient instead of a pass over (y, dout).  The same
-    fp32 terms summed in another order: logits identical, every gradient tensor at cosine >=
-    0.9999 with the pass form and the whole arena at >= 0.99999."""
+    fp32 terms summed in another order: logits identical; every gradient tensor within 1e-4 of
+    the pass form's norm (relative L2; ADVICE r5: a cosine bar would pass a partial tile that was
+    never written in a few channels — tests/test_kernels16_gpu.py fills the partials with NaN for
+    that at the kernel level), the whole arena at cosine >= 0.99999."""
     from mauv import engine
     _, m = build_pair()
     x, b, s, y = _batch(B, S)
@@ -65,16 +67,19 @@ def test_fp32_bn_partials_from_data_gradient_epilogue(S, B, monkeypatch):
     monkeypatch.setattr(engine, "BWD_PARTIALS_F32", True)
     lg1, g1 = _step(m, x, b, s, y, 2)
     assert torch.equal(lg0, lg1)
-    worst = (1.0, None)
+    worst, worst_rel = (1.0, None), (0.0, None)
     for n in g0:
         a, c = g0[n].double().flatten(), g1[n].double().flatten()
         if a.norm().item() == 0.0:
             assert c.norm().item() == 0.0, n
             continue
+        assert torch.isfinite(c).all(), n
         cos = (a @ c).item() / (a.norm() * c.norm()).item()
         worst = min(worst, (cos, n))
+        worst_rel = max(worst_rel, ((c - a).norm().item() / a.norm().item(), n))
     A = torch.cat([g0[n].double().flatten() for n in g0])
     C = torch.cat([g1[n].double().flatten() for n in g0])
     gcos = (A @ C).item() / (A.norm() * C.norm()).item()
-    print(f"fp32 {S} px B={B}: whole arena cosine {gcos:.9f}, worst tensor {worst}")
-    assert gcos >= 0.99999 and worst[0] >= 0.9999, (gcos, worst)
+    print(f"fp32 {S} px B={B}: whole arena cosine {gcos:.9f}, worst tensor cosine {worst}, "
+          f"worst relative L2 difference {worst_rel}")
+    assert gcos >= 0.99999 and worst_rel[0] <= 1e-4, (gcos, worst, worst_rel)

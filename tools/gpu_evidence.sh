@@ -1,7 +1,8 @@
 # One gpurun call that produces a round's evidence on one box, in order:
 #   the full GPU suite (-rP: the parity tests' printed deviations are kept) and smoke(),
 #   PMC traffic of both conv families on this library (copied where bench.py reads it),
-#   the default bench line, serial kernel statistics of one fp32 and one bf16 step, and
+#   the default bench line, serial kernel statistics of the steady fp32 and bf16 steps
+#   (tools/steady_stats.py: setup and the warm-up step excluded), and
 #   kernel statistics of the f16 inference leg.
 # usage (from the repo root, on the box):  bash tools/gpu_evidence.sh TAG [all|tests|rest]
 #   (a gpurun call is capped at 20 minutes: run "tests" and "rest" as two calls)
@@ -34,5 +35,8 @@ python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_bench.json'));print(
 C="--no-cpu-baseline --exact-steps 0 --no-roofline --no-sweep --no-infer --no-bf16"
 MAUV_TRUNK_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_st32 -o run -- python3 bench.py --steps 2 --warmup 1 $C > gpurun_out/${TAG}_st32.log 2>&1 || exit 1
 MAUV_TRUNK_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_st16 -o run -- python3 bench.py --dtype bf16 --steps 2 --warmup 1 $C > gpurun_out/${TAG}_st16.log 2>&1 || exit 1
+# per-kernel statistics of the steady steps only (setup and the warm-up step excluded)
+python3 tools/steady_stats.py gpurun_out/${TAG}_st32 gpurun_out/${TAG}_train_step_kernel_stats_steady.csv || exit 1
+python3 tools/steady_stats.py gpurun_out/${TAG}_st16 gpurun_out/${TAG}_bf16_train_step_kernel_stats_steady.csv || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_inf -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --exact-steps 0 --no-roofline --no-sweep --no-infer-sweep --no-bf16 --no-infer-fp32 > gpurun_out/${TAG}_inf.log 2>&1 || exit 1
 echo done

@@ -14,9 +14,20 @@ import sys
 from collections import defaultdict
 
 
+def template_args(name):
+    """The template arguments of a demangled kernel name: 'void f<1, 256, true, 2>(...)' ->
+    ['1', '256', 'true', '2']."""
+    head = name.split("(")[0]
+    if "<" not in head:
+        return []
+    return [s.strip() for s in head[head.index("<") + 1:head.rindex(">")].split(",")]
+
+
 def family(name):
-    if "conv_big16<" in name and name.split("(")[0].rstrip().endswith((", 1>", ", 2>")):
-        return "conv_fold16"     # conv1 forming the previous block output (its own family)
+    # conv_big16<DT, BM, BN, XBN, RES>: RES 1 / 2 = conv1 forming the previous block output
+    # (the fold, its own family beside the MFMA one; bench.py's roofline 'fold')
+    if "conv_big16<" in name and template_args(name)[4:5] in (["1"], ["2"]):
+        return "conv_fold16"
     if "conv_gemm_f32" in name or "conv_split_f32" in name:
         return "conv_f32"        # the fp32 conv family: split kernels + stems on conv_gemm_f32
     if any(k in name for k in ("conv_gemm_h16", "conv_pipe16", "conv_halo16", "conv_haloc16",

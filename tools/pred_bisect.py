@@ -58,7 +58,11 @@ def main():
     ap.add_argument("--N", type=int, default=8)
     ap.add_argument("--seeds", type=int, default=0,
                     help="light mode: K (data, epsilon) seeds, product vs autocast only")
+    ap.add_argument("--no-fit", action="store_true", help="random-init model (no fit_model)")
+    ap.add_argument("--centre", type=int, default=1, help="engine.CENTRE_Y (1 default)")
     a = ap.parse_args()
+    from mauv import engine as _engine
+    _engine.CENTRE_Y = bool(a.centre)
     if a.seeds:
         return sweep(a)
     from mauv import engine
@@ -168,9 +172,10 @@ def sweep(a):
         batch = make_batches(SEED_DATA + 1 + k, 1, B=B, S_opt=a.S_opt, S_son=a.S_son)[0]
         x, b, s = batch["main_image"], batch["bathy_image"], batch["sss_image"]
         cu = [t.cuda() for t in (x, b, s)]
-        fit_model(m, *cu, torch.randint(0, 7, (B,),
-                                        generator=torch.Generator().manual_seed(3 + k)).cuda())
-        o.load_state_dict({kk: v.cpu() for kk, v in m.state_dict().items()})
+        if not a.no_fit:
+            fit_model(m, *cu, torch.randint(0, 7, (B,),
+                                            generator=torch.Generator().manual_seed(3 + k)).cuda())
+            o.load_state_dict({kk: v.cpu() for kk, v in m.state_dict().items()})
         bridge = EpsBridge(o, m, 7 + 100 * k)
         with bridge, torch.no_grad():
             for _ in range(N):
@@ -189,19 +194,32 @@ def sweep(a):
         def pent(lg):
             pm = F.softmax(lg, -1).mean(0)
             return -(pm * torch.log(pm + 1e-8)).sum(-1)
-        ar, _ = stats(lg32)
-        aa, _ = stats(lgac)
+        ar, vr = stats(lg32)
+        aa, va_ = stats(lgac)
+        dvh = (st["var"].double().cpu() - vr).abs()
+        dva = (va_ - vr).abs()
+        print(f"seed {k}: variance |d| mean HIP {dvh.mean():.3e} autocast {dva.mean():.3e}, max "
+              f"HIP {dvh.max():.3e} autocast {dva.max():.3e} (|var| <= {vr.abs().max():.3e})")
         dah = (st["aleatoric"].double().cpu() - ar).abs()
         daa = (aa - ar).abs()
         dph = (st["predictive_entropy"].double().cpu() - pent(lg32)).abs()
         dpa = (pent(lgac) - pent(lg32)).abs()
+        root_state(m).eps_provider = bridge.provider
+        with torch.no_grad(), torch.autocast("cuda"):
+            lh = m.mc_forward(*cu, N).double().cpu()
+        bar = 5e-2 * lg32.abs().clamp(min=1)
+        vh = int(((lh - lg32).abs() > bar).sum())
+        va = int(((lgac - lg32).abs() > bar).sum())
         rows.append((dah.mean().item(), daa.mean().item(), dah.max().item(), daa.max().item(),
-                     dph.max().item(), dpa.max().item()))
+                     dph.max().item(), dpa.max().item(), vh, va, (lh - lg32).abs().max().item(),
+                     (lgac - lg32).abs().max().item(), dph.mean().item(), dpa.mean().item()))
         print(f"seed {k}: aleatoric |d| mean HIP {rows[-1][0]:.3e} autocast {rows[-1][1]:.3e} "
               f"(ratio {rows[-1][0] / rows[-1][1]:.2f}); max HIP {rows[-1][2]:.3e} autocast "
               f"{rows[-1][3]:.3e}; predictive entropy max HIP {rows[-1][4]:.3e} autocast "
-              f"{rows[-1][5]:.3e}; classes {len(set(F.softmax(lg32, -1).mean(0).argmax(-1).tolist()))}",
-              flush=True)
+              f"{rows[-1][5]:.3e} (mean {rows[-1][10]:.3e} / {rows[-1][11]:.3e}); logits over "
+              f"SURVEY's 5e-2 max(1,|ref|) HIP {vh} autocast {va} of {lg32.numel()} (max |d| "
+              f"{rows[-1][8]:.3e} / {rows[-1][9]:.3e}, |ref| <= {lg32.abs().max():.1f}); classes "
+              f"{len(set(F.softmax(lg32, -1).mean(0).argmax(-1).tolist()))}", flush=True)
         del o, m
         torch.cuda.empty_cache()
     import numpy as np
@@ -209,7 +227,10 @@ def sweep(a):
     print(f"over {len(rows)} seeds: mean-of-means HIP {r[:, 0].mean():.3e} autocast "
           f"{r[:, 1].mean():.3e} (ratio {r[:, 0].mean() / r[:, 1].mean():.2f}); ratio per seed "
           f"min {np.min(r[:, 0] / r[:, 1]):.2f} max {np.max(r[:, 0] / r[:, 1]):.2f}; worst item "
-          f"HIP {r[:, 2].max():.3e} autocast {r[:, 3].max():.3e}")
+          f"HIP {r[:, 2].max():.3e} autocast {r[:, 3].max():.3e}; predictive entropy mean "
+          f"HIP {r[:, 10].mean():.3e} autocast {r[:, 11].mean():.3e}, worst HIP {r[:, 4].max():.3e} "
+          f"autocast {r[:, 5].max():.3e}; logit bar violations HIP {int(r[:, 6].sum())} autocast "
+          f"{int(r[:, 7].sum())}")
 
 
 if __name__ == "__main__":
