@@ -56,11 +56,12 @@ BWD_PARTIALS_F32 = True
 # 16-bit trunks: a conv output consumed by a batch-statistics BatchNorm is stored centred,
 # y - c (ops.conv2d_fwd ysh; the finalize turns the statistics into those of the stored values
 # and updates the running mean with the true one), c = that BN's running mean as of the model's
-# last refresh_centres (the first 16-bit forward, and every multimodal_predict_and_save call /
-# training epoch).  The f16 / bf16 rounding error of the stored tensor then follows the batch
-# spread |y - mean| instead of |y|: the largest of the path's rounding points (DESIGN.md
-# §2.31).  Exact in real arithmetic; c changes only when refreshed, so a forward's result stays
-# a function of the weights, samples and inputs between refreshes.  Test hook like FOLD.
+# last refresh_centres (the model's first 16-bit forward, and the start of every training epoch
+# of the drop-in loops) where it dominates the channel's spread.  The f16 / bf16 rounding error
+# of the stored tensor then follows the batch spread |y - mean| instead of |y|: the largest of
+# the path's rounding points.  Exact in real arithmetic; c changes only when
+# refreshed, so predictions stay a function of the weights, samples and inputs (two predictor
+# calls on the same samples give the same rows).  Test hook like FOLD.
 CENTRE_Y = os.environ.get("MAUV_CENTRE_Y", "1") == "1"
 # a channel is centred where |running mean| > this many running standard deviations
 CENTRE_MIN_Z = float(os.environ.get("MAUV_CENTRE_MIN_Z", "1"))
@@ -231,7 +232,8 @@ def invalidate(root):
 
 def refresh_centres(root):
     """Take the 16-bit trunks' storage centres (CENTRE_Y) from the current BatchNorm running
-    means — the drop-in predictor does at every call, the training loops at every epoch."""
+    statistics — the drop-in training loops do at every epoch; the first 16-bit forward of a
+    model takes them on its own."""
     root_state(root).refresh_centres()
 
 

@@ -234,13 +234,12 @@ def multimodal_predict_and_save(multimodal_model, dataloader, device, csv_path,
                                 model_type="multimodal"):
     """inference/predictors.py:9-97 (model kept in .train(): BN uses batch statistics; MC
     passes under torch.amp.autocast as predictors.py:55 -> f16 trunks on a ROCm device)."""
-    from .train import loop_device, is_writer, _NullFile, _tile_to, refresh_centres_on_gpu
+    from .train import loop_device, is_writer, _NullFile, _tile_to
     device = torch.device(loop_device(multimodal_model, device))
     amp_device = "cuda" if device.type == "cuda" else "cpu"
     group = _shard_group(multimodal_model)
     writer = is_writer(multimodal_model)   # MC-sharded: every rank holds the same rows
     multimodal_model.train()
-    refresh_centres_on_gpu(multimodal_model)
     logging.info(f"CSV will be saved to: {csv_path}")
     with (open(csv_path, mode="w", newline="") if writer else _NullFile()) as fh:
         w = csv.writer(fh)

@@ -326,7 +326,7 @@ def _patch_tag(t, kind):
 
 def refresh_centres_on_gpu(model):
     """engine.refresh_centres for a model on a ROCm device (the 16-bit storage centres follow
-    the running means once per training epoch / predictor call)."""
+    the running statistics once per training epoch)."""
     from .engine import refresh_centres
     core = unwrap(model)
     p = next(core.parameters(), None)
