@@ -134,11 +134,14 @@ int mauv_conv2d_bwd_weight_f32(const float* x, const long long* x_strides, const
  * run as GEMMs over im2col rows, mauv_stem_*; their former 8-channel padded form remains
  * valid), dgrad needs Cout % 32 == 0; x strides
  * are channel-contiguous multiples of 8.  Statistics partials: mauv_conv2d_fwd_stat_blocks.
- * y_shift (nullable, [Cout] fp32): y is STORED centred, y[.., c] = round16(conv - y_shift[c]),
- * while the statistics partials stay those of the uncentred conv output; pass the consuming
- * BatchNorm's running mean here and to mauv_bn_stats_finalize — the 16-bit rounding error of the
+ * y_shift (nullable, [Cout] fp32): y is STORED centred, y[.., c] = round16(conv - y_shift[c]):
+ * the fp32 accumulators start at -y_shift[c], so the statistics partials are those of the stored
+ * values too; pass the consuming BatchNorm's centre (its running mean where that dominates the
+ * channel's spread, else 0) here and to mauv_bn_stats_finalize — the 16-bit rounding error of the
  * stored tensor then scales with the batch spread |y - mean| instead of |y|, the error the BN's
- * 1/std amplifies when a channel's mean is large. */
+ * 1/std amplifies when a channel's mean is large.  Every route (the
+ * implicit GEMM, 3x3 row images, LDS-DMA tiles, weight-stationary expansion) gives the same bits
+ * for the same y_shift. */
 int mauv_conv2d_fwd_h16(int dtype, const void* x, const long long* x_strides,
                         const float* x_scale, const float* x_shift, int x_relu, const void* w,
                         void* y, int G, int B, int H, int W, int Cin, int Cout, int R, int S,
@@ -295,10 +298,10 @@ int mauv_bn_fwd_train(const float* y, int G, long long M, int C, const float* ga
  * mean/invstd/scale/shift [G][C], sequential running-stat update (run_* nullable);
  * workspace: mauv_bn_stats_workspace_floats(G, nblk, C) floats (2*G*C when nblk <= 128*64;
  * larger partial counts are merged in segments).  y_shift (nullable, [C]): the centre the 16-bit
- * forward stored y with (mauv_conv2d_fwd_h16) — mean and shift then describe the stored values
- * (mean = mu - y_shift, shift = beta - mean*scale) for every consumer of that tensor, while the
- * running mean is updated with the true mu; y_shift may alias run_mean (it is read before the
- * update). */
+ * forward stored y with (mauv_conv2d_fwd_h16); the partials are then those of the stored values
+ * and mean / shift describe them (mean = mu_stored, shift = beta - mean*scale) for every
+ * consumer of that tensor, while the running mean is updated with the true mean
+ * mu_stored + y_shift; y_shift may alias run_mean (it is read before the update). */
 long long mauv_bn_stats_workspace_floats(int G, int nblk, int C);
 int mauv_bn_stats_finalize(int G, int nblk, int C, const float* pmean, const float* pm2,
                            const float* pcnt, const float* gamma, const float* beta,

@@ -113,11 +113,10 @@ __device__ __forceinline__ void chan_merge(double& nn, double& mu, double& mm, d
 // M2 = sum [M2_b + n_b*(mean_b - mean)^2] (double; no divisions in the loops).
 constexpr int FIN_L = 16;
 
-// The finalized statistics of channel c of group g.  With ysh (the centre the 16-bit forward
-// epilogue subtracted before storing y, ConvArgs::ysh) mean / shift describe the STORED values
-// y - ysh, which every consumer (BN on load, the BN backward's xhat) reads: mean_out = mu - ysh,
-// shift = beta - mean_out * scale; the running statistics take the true mean mu (uvar_out[G*C + ...],
-// bn_running_kernel).
+// The finalized statistics of channel c of group g from partials of the STORED values: with ysh
+// (the centre a 16-bit forward stored y around, ConvArgs::ysh) they are those of y - ysh, which
+// every consumer (BN on load, the BN backward's xhat) reads — mean / shift describe them as they
+// are; the running statistics take the true mean mu + ysh (ws[G*C + ...], bn_running_kernel).
 __device__ __forceinline__ void stats_out(int G, int g, int c, int C, double nn, double mu,
                                           double mm,
                                           const float* gamma, const float* beta, float eps,
@@ -126,13 +125,12 @@ __device__ __forceinline__ void stats_out(int G, int g, int c, int C, double nn,
   const double var = mm / nn;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const float sc = gamma[c] * invstd;
-  const float ms = (float)(ysh ? mu - (double)ysh[c] : mu);
-  mean_out[g * C + c] = ms;
+  mean_out[g * C + c] = (float)mu;
   invstd_out[g * C + c] = invstd;
   scale_out[g * C + c] = sc;
-  shift_out[g * C + c] = beta[c] - ms * sc;
-  ws[g * C + c] = (float)(nn > 1.0 ? mm / (nn - 1.0) : var);   // unbiased variance
-  ws[(long long)G * C + g * C + c] = (float)mu;                  // true mean (running stats)
+  shift_out[g * C + c] = beta[c] - (float)mu * sc;
+  ws[g * C + c] = (float)(nn > 1.0 ? mm / (nn - 1.0) : var);            // unbiased variance
+  ws[(long long)G * C + g * C + c] = (float)(ysh ? mu + (double)ysh[c] : mu);  // true mean
 }
 
 __device__ __forceinline__ double lane_sum16(double v, double (*red)[64], int tx, int ty) {

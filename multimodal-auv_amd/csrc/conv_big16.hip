@@ -155,15 +155,12 @@ __global__ __launch_bounds__(512, 2) void conv_big16(const ConvArgs a) {
       tp0[i] = m < a.M ? oh * a.stride - a.pad : -(1 << 28);
       tp1[i] = ow * a.stride - a.pad;
     }
-    for (int i = tid; i < a.Cin; i += NT) {
-      xbn[i] = a.xsc[g * a.Cin + i];
-      xbn[XS + i] = a.xsh[g * a.Cin + i];
-      if constexpr (RES == 2) {
-        xbn[2 * XS + i] = a.rs_sc[g * a.Cin + i];
-        xbn[3 * XS + i] = a.rs_sh[g * a.Cin + i];
-      }
-    }
   }
+  // the parameter tables: fetched here, put into LDS once the first tile's DMAs are issued
+  constexpr int XJ = XF ? (XS + NT - 1) / NT : 1;
+  float xv[XJ][2], rv[RES == 2 ? XJ : 1][2];
+  if constexpr (XF) xbn_fetch(xv, a.xsc + g * a.Cin, a.xsh + g * a.Cin, a.Cin, tid, NT);
+  if constexpr (RES == 2) xbn_fetch(rv, a.rs_sc + g * a.Cin, a.rs_sh + g * a.Cin, a.Cin, tid, NT);
   // fold: this thread's residual chunks (the rows / slots it transforms, 1x1: pixel = row) reach
   // registers one stage ahead, issued after the transform that frees them
   u32x4 rres[RES ? TCH : 1];
@@ -202,12 +199,8 @@ __global__ __launch_bounds__(512, 2) void conv_big16(const ConvArgs a) {
   };
 
   floatx16 acc[MI][NI];
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+  float cs[NI];  // the accumulators' start, loaded here and filled after the first DMAs
+  acc_shift16(cs, a, n0 + wn * WN, true);
 
   auto frag = [&](const unsigned char* img, int row, int chunk) -> u32x4 {
     return *(const u32x4*)(img + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
@@ -239,6 +232,9 @@ __global__ __launch_bounds__(512, 2) void conv_big16(const ConvArgs a) {
   int x_r = 0, x_s = 0, x_c = 0;  // k position of the stage being transformed
   issue(0);
   if constexpr (RES != 0) load_res(0);
+  acc_start16(acc, cs);
+  if constexpr (XF) xbn_put(xbn, xbn + XS, xv, a.Cin, tid, NT);
+  if constexpr (RES == 2) xbn_put(xbn + 2 * XS, xbn + 3 * XS, rv, a.Cin, tid, NT);
   if constexpr (XF) block_sync();  // xbn staged
   for (int t = 0; t < nt; ++t) {
     // tile t + 1 goes to the buffer tile t - 1 was read from (free since the barrier ending t - 1).

@@ -45,10 +45,11 @@ struct ConvArgs {
   // FWD epilogue BN statistics partials [G][st_nblk][N] (+ counts [G][st_nblk])
   float *st_mean, *st_m2, *st_cnt;
   int st_nblk, st_base;
-  // 16-bit FWD: the stored output is y - ysh[channel] (nullable, [N] or [cpg]; the consuming
-  // BatchNorm's running mean): the 16-bit rounding error then scales with |y - ysh| (the batch
-  // spread) instead of |y|, which the BN's 1/std amplifies when a channel's mean is large; the
-  // statistics partials stay those of y (mauv_bn_stats_finalize takes the same ysh)
+  // 16-bit FWD: the accumulators start at -ysh[channel] (nullable, [N] or [cpg]; the consuming
+  // BatchNorm's centre, conv_epi16.h acc_start16), so the stored output and its statistics
+  // partials are those of y - ysh: the 16-bit rounding error then scales with |y - ysh| (the
+  // batch spread) instead of |y|, which the BN's 1/std amplifies when a channel's mean is
+  // large (mauv_bn_stats_finalize takes the same ysh to add it back for the running mean)
   const float* ysh;
   // DGRAD epilogue BN-backward partials [G][bp_nblk][N]: sum dz, sum dz*xhat
   const float *bp_y, *bp_out, *bp_sc, *bp_sh, *bp_mean, *bp_invstd;

@@ -55,6 +55,76 @@ __device__ __forceinline__ u32x4 bn_relu8(u32x4 v, const floatx8& sc, const floa
   return o;
 }
 
+// The accumulators' starting value: 0, or - a FWD with centred storage (ConvArgs::ysh) - minus
+// the column's centre, so that they hold y - ysh[channel] from the first MFMA on: the stored
+// output AND the statistics partials are those of the centred values (mauv_bn_stats_finalize
+// adds the centre back for the running mean).  Every 16-bit forward kernel starts its
+// accumulators this way with the same C/D column map (lane l -> column col0 + 32 ni + (l & 31)),
+// so the kernels stay bit-identical to each other.  col0 = the wave's first output column.
+// Two halves, so that the centre's load overlaps the tile loads instead of stalling the block
+// (measured: a load-and-wait at the top cost 5-18 % on short-K forwards): acc_shift16 issues one
+// branch-free buffer load per column fragment at the top of the kernel (no centre, or a column
+// >= N: a zero-length / out-of-range descriptor access, which returns 0); acc_start16 fills the
+// accumulators after the prologue's tile loads are issued, where the wait for the centre (the
+// oldest load) costs nothing.  0 - c keeps +0 without a centre (the uncentred bits).
+template <int NI>
+__device__ __forceinline__ void acc_shift16(float (&c)[NI], const ConvArgs& a, int col0, bool fwd) {
+  const int li = threadIdx.x & 31;
+  const bool on = fwd && a.ysh;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.ysh, (short)0, on ? 4 * (a.cpg ? a.cpg : a.N) : 0, 0x00020000);
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    const int col = col0 + ni * 32 + li;
+    const int off = col < a.N ? 4 * (a.cpg ? col % a.cpg : col) : 0x7ffffff0;
+    c[ni] = on ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0)) : 0.f;
+  }
+}
+template <int MI, int NI>
+__device__ __forceinline__ void acc_start16(floatx16 (&acc)[MI][NI], const float (&c)[NI]) {
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    const float v = 0.f - c[ni];
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = v;
+  }
+}
+
+// A pending BatchNorm's per-channel scale / shift staged into LDS without stalling the block
+// (the same reasoning as acc_shift16: a staging loop at the top of the kernel waited for its
+// global loads before the first tile load was issued).  xbn_fetch issues branch-free buffer
+// loads of channels tid + NT j (beyond n: out of range, 0) into registers; xbn_put writes them to
+// LDS once the tile loads are in flight (before the barrier that publishes the staged values).
+template <int J>
+__device__ __forceinline__ void xbn_fetch(float (&v)[J][2], const float* sc, const float* sh,
+                                          int n, int tid, int nt) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sc, (short)0, 4 * n,
+                                                                      0x00020000);
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)sh, (short)0, 4 * n,
+                                                                      0x00020000);
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int i = tid + nt * j;
+    const int off = i < n ? 4 * i : 0x7ffffff0;
+    v[j][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+    v[j][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rh, off, 0, 0));
+  }
+}
+template <int J>
+__device__ __forceinline__ void xbn_put(float* dsc, float* dsh, const float (&v)[J][2], int n,
+                                        int tid, int nt) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int i = tid + nt * j;
+    if (i < n) {
+      dsc[i] = v[j][0];
+      dsh[i] = v[j][1];
+    }
+  }
+}
+
 // Chan et al.'s merge of two row sets' (count, mean, M2) into the first: the 16-bit forwards'
 // statistics partials combine their 64-row halves with exactly these operations
 __device__ __forceinline__ void stats_merge(float na, float ma, float qa, float nb, float mb,
@@ -262,12 +332,6 @@ __device__ __forceinline__ void epilogue16(const ConvArgs& a, floatx16 (&acc)[MI
 #pragma unroll
       for (int e = 0; e < 4; ++e) { f[e] = v0[e]; f[4 + e] = v1[e]; }
       const int kk = k % PFD;
-      if constexpr (MODE == FWD) {
-        if (a.ysh) {  // centred storage (ConvArgs::ysh): one fp32 subtraction, then the rounding
-          const int ch = a.cpg ? (n0 + 8 * cc) % a.cpg : n0 + 8 * cc;
-          f -= ldf8(a.ysh + ch);
-        }
-      }
       if constexpr (MODE == DGRAD) {
         if (addp) {
           floatx8 av = unpack8<DT>(PF ? pa[kk] : *(const u32x4*)(addp + o));

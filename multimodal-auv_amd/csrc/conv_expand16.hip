@@ -44,8 +44,12 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
   constexpr int CPW = BM * WN / 8 / 64;         // 16-byte output chunks per lane per tile
   static_assert(NVA >= 1 && NT % KQ == 0 && CPW >= 1 && MI == 2, "tile geometry");
   constexpr int XS = XBN ? 2 * K : 0;  // the pending BN's scale / shift (floats)
-  __shared__ __attribute__((aligned(16))) u16 smem[2 * A_SZ + NW * P_SZ + 2 * XS];
+  // + the accumulators' starting values of the block's NW * WN columns (acc_start16's: minus
+  // the centre of centred storage, else 0), staged once: the weight fragments leave no
+  // registers to hold them across the tile loop
+  __shared__ __attribute__((aligned(16))) u16 smem[2 * A_SZ + NW * P_SZ + 2 * XS + 2 * NW * WN];
   float* xbn = (float*)(smem + 2 * A_SZ + NW * P_SZ);
+  float* acc0 = (float*)(smem + 2 * A_SZ + NW * P_SZ + 2 * XS);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 31, lh = lane >> 5;
   const int g = blockIdx.y / ncg, cg = blockIdx.y - g * ncg;
@@ -70,8 +74,12 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
       xbn[c] = a.xsc[g * a.Cin + c];
       xbn[K + c] = a.xsh[g * a.Cin + c];
     }
-    __syncthreads();
   }
+  for (int c = tid; c < NW * WN; c += NT) {
+    const int col = cg * NW * WN + c;
+    acc0[c] = a.ysh && col < a.N ? -a.ysh[col] : 0.f;
+  }
+  __syncthreads();
   const unsigned rfloor = a.xrelu ? 0u : 0x80008000u;
 
   // tile i of this block: row pair blockIdx.x + (i / 2) * gridDim.x, half i % 2
@@ -115,11 +123,13 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
     const int t = tile_of(i), buf = i & 1;
     floatx16 acc[MI][NI];
 #pragma unroll
-    for (int mi = 0; mi < MI; ++mi)
+    for (int ni = 0; ni < NI; ++ni) {
+      const float v = acc0[((int)threadIdx.x >> 6) * WN + ni * 32 + ((int)threadIdx.x & 31)];
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[mi][ni][r] = v;
+    }
     const u16* As = smem + buf * A_SZ;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -233,11 +243,7 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
       }
     }
 
-    // ---- 16-bit output: park the wave's 64 x WN tile (centred by ysh: ConvArgs), store
-    // 16-byte rows ----
-    float ctr[NI];
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) ctr[ni] = a.ysh ? a.ysh[nw0 + ni * 32 + li] : 0.f;
+    // ---- 16-bit output: park the wave's 64 x WN tile, store 16-byte rows ----
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -245,7 +251,7 @@ void conv_expand16(const ConvArgs a, int npairs, int ncg) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           park[(mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * PLD + ni * 32 + li] =
-              H16<DT>::from_f(acc[mi][ni][r] - ctr[ni]);
+              H16<DT>::from_f(acc[mi][ni][r]);
     __syncthreads();  // parked tiles and the next A image visible; every wave done with `buf`
     u16* outp = (u16*)a.out + (long long)g * a.out_sg;
 #pragma unroll

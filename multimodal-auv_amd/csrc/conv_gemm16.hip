@@ -337,6 +337,17 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(const ConvArgs16 a) {
   }
 
   // ---------------- epilogue ----------------
+  if ((MODE == H_FWD) && a.ysh) {  // centred storage (conv_epi16.h acc_start16's semantics)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int col = n0 + wn * WN + ni * 32 + li;
+      const float c = col < a.N ? a.ysh[col] : 0.f;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mi][ni][r] -= c;
+    }
+  }
   // FWD statistics (from the fp32 accumulators, before any rounding)
   if ((MODE == H_FWD) && a.st_mean) {
     const int nvalid = min(BM, a.M - m0);
@@ -451,9 +462,6 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(const ConvArgs16 a) {
         if constexpr (MODE == H_DGRAD) {
           if (a.addend) f += unpack8<DT>(*(const u32x4*)(a.addend + o));
           if (a.accumulate) f += unpack8<DT>(*(const u32x4*)(outp + o));
-        }
-        if constexpr (MODE == H_FWD) {
-          if (a.ysh) f -= ldf8(a.ysh + col);
         }
         *(u32x4*)(outp + o) = pack8<DT>(f);
       }

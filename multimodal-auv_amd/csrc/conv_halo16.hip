@@ -77,14 +77,13 @@ void conv_halo16(const ConvArgs a) {
   const u16* wg = (const u16*)a.w + (long long)g * a.ws_g;
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)xg, (short)0, (int)(nin * 2), 0x00020000);
-  if constexpr (XBN) {
-    if (tid < C) {
-      xbn[tid] = a.xsc[g * C + tid];
-      xbn[C + tid] = a.xsh[g * C + tid];
-    }
-  }
+  // the pending BN: fetched here, put into LDS once the input rows' loads are issued
+  float xv[1][2];
+  if constexpr (XBN) xbn_fetch(xv, a.xsc + g * C, a.xsh + g * C, C, tid, NT);
 
   // ---- the input rows: chunk q = (LDS row hr, column iw, channel chunk cq), 8 per pixel ----
+  float cs[NI];  // the accumulators' start, loaded here and filled after the weight loads
+  acc_shift16(cs, a, n0 + wn * WN, MODE == FWD);
   const unsigned nch = (unsigned)(nhr * W * 8);
   u32x4 v[NCH];
 #pragma unroll
@@ -111,7 +110,17 @@ void conv_halo16(const ConvArgs a) {
   u32x4 wv[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) wv[t] = *(const u32x4*)(wrow + t * C);
-  if constexpr (XBN) __syncthreads();  // xbn staged
+  floatx16 acc[NI];
+  {
+    floatx16 a0[1][NI];
+    acc_start16(a0, cs);
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) acc[ni] = a0[0][ni];
+  }
+  if constexpr (XBN) {
+    xbn_put(xbn, xbn + C, xv, C, tid, NT);
+    __syncthreads();  // xbn staged
+  }
   const unsigned rfloor = a.xrelu ? 0u : 0x80008000u;
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
@@ -143,12 +152,6 @@ void conv_halo16(const ConvArgs a) {
   const int oh = gr_m - (gr_m / H) * H;
   const int hb = (gr_m - R0) * W2 + ow;                // LDS pixel of tap (0, 0)
   __syncthreads();
-
-  floatx16 acc[NI];
-#pragma unroll
-  for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[ni][r] = 0.f;
 
 #pragma unroll
   for (int t = 0; t < 9; ++t) {

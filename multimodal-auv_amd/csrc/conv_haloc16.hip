@@ -70,12 +70,10 @@ void conv_haloc16(const ConvArgs a) {
   const u16* wg = (const u16*)a.w + (long long)g * a.ws_g;
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)xg, (short)0, (int)(nin * 2), 0x00020000);
-  if constexpr (XBN) {
-    for (int i = tid; i < C; i += NT) {
-      xbn[i] = a.xsc[g * C + i];
-      xbn[kMaxHcC + i] = a.xsh[g * C + i];
-    }
-  }
+  // the pending BN: fetched here, put into LDS once the first chunk's loads are issued
+  constexpr int XJ = XBN ? (kMaxHcC + NT - 1) / NT : 1;
+  float xv[XJ][2];
+  if constexpr (XBN) xbn_fetch(xv, a.xsc + g * C, a.xsh + g * C, C, tid, NT);
   const unsigned rfloor = a.xrelu ? 0u : 0x80008000u;
 
   // ---- one 64-channel chunk of the input rows: chunk q = (LDS row hr, column iw, cq) ----
@@ -162,9 +160,16 @@ void conv_haloc16(const ConvArgs a) {
     const int hr = q >> 4, side = (q >> 3) & 1, cq = q & 7;
     *(u32x4*)(img + cslot(hr * W2 + side * (W + 1), cq)) = u32x4{0u, 0u, 0u, 0u};
   }
+  float cs[NI];  // the accumulators' start, loaded first and filled after the first tile loads
+  acc_shift16(cs, a, n0 + wn * WN, MODE == FWD);
   load_img(0);
   load_w(0, 0);
-  if constexpr (XBN) __syncthreads();  // xbn staged
+  floatx16 acc[MI][NI];
+  acc_start16(acc, cs);
+  if constexpr (XBN) {
+    xbn_put(xbn, xbn + kMaxHcC, xv, C, tid, NT);
+    __syncthreads();  // xbn staged
+  }
   store_img(0);
   store_w(0);
   const int nchunk = C / 64;
@@ -184,14 +189,6 @@ void conv_haloc16(const ConvArgs a) {
     hb[mi] = (gr_m - R0) * W2 + ow;  // LDS pixel of tap (0, 0)
   }
   __syncthreads();
-
-  floatx16 acc[MI][NI];
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
   int wb = 0;  // weight buffer of the current tap
   for (int cc = 0; cc < nchunk; ++cc) {

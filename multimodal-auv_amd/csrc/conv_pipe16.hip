@@ -179,12 +179,13 @@ void conv_pipe16(const ConvArgs a) {
       }
     }
   }
-  if constexpr (XBN && MODE == FWD) {
-    for (int i = tid; i < a.Cin; i += NT) {
-      xbn[i] = a.xsc[g * a.Cin + i];
-      xbn[kMaxXbn16 + i] = a.xsh[g * a.Cin + i];
-    }
-  }
+  // FWD pending BN: fetched here, put into LDS once the first tile loads are issued
+  constexpr int XJ = (XBN && MODE == FWD) ? (kMaxXbn16 + NT - 1) / NT : 1;
+  float xv[XJ][2];
+  if constexpr (XBN && MODE == FWD) xbn_fetch(xv, a.xsc + g * a.Cin, a.xsh + g * a.Cin, a.Cin, tid, NT);
+  auto xbn_stage = [&]() {
+    if constexpr (XBN && MODE == FWD) xbn_put(xbn, xbn + kMaxXbn16, xv, a.Cin, tid, NT);
+  };
 
   int t_r = 0, t_s = 0, t_c = 0;  // tile-uniform k position (FWD: r, s, cin; DGRAD: tr, ts, cout)
   typedef Stage16<NVA, NVB> St;
@@ -285,12 +286,8 @@ void conv_pipe16(const ConvArgs a) {
   };
 
   floatx16 acc[MI][NI];
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+  float cs[NI];  // the accumulators' start, loaded here and filled after the first tile loads
+  acc_shift16(cs, a, n0 + wn * WN, MODE == FWD);
 
   auto compute = [&](int buf) {
     const u16* As = smem + buf * STG;
@@ -318,6 +315,8 @@ void conv_pipe16(const ConvArgs a) {
   if constexpr (SHORT == 1) {  // nt == 1 (host-checked)
     St S0;
     load(S0, 0);
+    acc_start16(acc, cs);
+    xbn_stage();
     if constexpr (XBN && MODE == FWD) __syncthreads();  // xbn staged
     store(S0, 0);
     __syncthreads();
@@ -325,19 +324,39 @@ void conv_pipe16(const ConvArgs a) {
     __syncthreads();  // the epilogue reuses the operand buffer
   } else if constexpr (SHORT == 2) {  // short K: stages one after another through one buffer
     St S0;
-    if constexpr (XBN && MODE == FWD) __syncthreads();  // xbn staged
-    for (int t = 0; t < nt; ++t) {
-      load(S0, t);
+    auto stage = [&]() {
       store(S0, 0);
       __syncthreads();
       compute(0);
       __syncthreads();  // the next stage / the epilogue reuses the operand buffer
+    };
+    // (two loop shapes, each the one that fits the 80-VGPR budget of waves_per_eu(6) without a
+    // spill or a lower occupancy: checked with -Rpass-analysis=kernel-resource-usage)
+    if constexpr (XBN && MODE == FWD) {
+      // the pending BN staged before the first tile load: no room to hold it across the load
+      xbn_stage();
+      __syncthreads();  // xbn staged
+      for (int t = 0; t < nt; ++t) {
+        load(S0, t);
+        if (t == 0) acc_start16(acc, cs);
+        stage();
+      }
+    } else {
+      load(S0, 0);
+      acc_start16(acc, cs);
+      for (int t = 0;;) {
+        stage();
+        if (++t == nt) break;
+        load(S0, t);
+      }
     }
   } else {
   // ---- pipeline: buffer 0 <- tile 0, registers S1 <- tile 1 ----
   St S0, S1;
   load(S0, 0);
   load(S1, 1);
+  acc_start16(acc, cs);
+  xbn_stage();
   if constexpr (XBN && MODE == FWD) __syncthreads();  // xbn staged
   store(S0, 0);
   __syncthreads();

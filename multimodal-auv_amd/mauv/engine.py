@@ -54,8 +54,8 @@ FOLD_MIN_TILES = 512
 # into that dx afterwards).  Test hook like FOLD: the same sums in another fp32 order.
 BWD_PARTIALS_F32 = True
 # 16-bit trunks: a conv output consumed by a batch-statistics BatchNorm is stored centred,
-# y - c (ops.conv2d_fwd ysh; the finalize turns the statistics into those of the stored values
-# and updates the running mean with the true one), c = that BN's running mean as of the model's
+# y - c (ops.conv2d_fwd ysh: the accumulators start at -c, so the statistics partials are those
+# of the stored values; the finalize updates the running mean with the true one), c = that BN's running mean as of the model's
 # last refresh_centres (the model's first 16-bit forward, and the start of every training epoch
 # of the drop-in loops) where it dominates the channel's spread.  The f16 / bf16 rounding error
 # of the stored tensor then follows the batch spread |y - mean| instead of |y|: the largest of

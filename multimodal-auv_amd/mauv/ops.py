@@ -184,8 +184,9 @@ def conv2d_fwd(x, w, y, G, B, H, W, Cin, Cout, R, stride, pad, bias=None, x_stri
     """y[G][B*Ho*Wo][Cout] = conv(x'[g], w[g]) (+ bias[g]); w: [G][Cout][R][R][Cin].
     x_bn = (scale [G][Cin], shift [G][Cin], relu): x' = [relu](x*scale + shift) on load.
     stats = (mean, m2, cnt) partial buffers for the epilogue BN statistics (see
-    fwd_stat_blocks).  ysh ([Cout] fp32, 16-bit only): y is stored centred, y - ysh (the
-    consuming BN's running mean; bn_stats_finalize takes the same ysh)."""
+    fwd_stat_blocks).  ysh ([Cout] fp32, 16-bit only): y is stored centred, y - ysh, and the
+    statistics partials are those of the stored values (the accumulators start at -ysh; the
+    consuming BN's centre, bn_stats_finalize takes the same ysh)."""
     xs = None if x_strides is None else _LL5(*x_strides)
     sc, sh, rl = x_bn if x_bn is not None else (None, None, 0)
     sm, s2, sn = stats if stats is not None else (None, None, None)
@@ -462,8 +463,9 @@ def bn_stats_workspace_floats(G, nblk, C):
 
 def bn_stats_finalize(G, nblk, C, pmean, pm2, pcnt, gamma, beta, run_mean, run_var, momentum,
                       eps, ws, mean, invstd, scale, shift, ysh=None):
-    """ysh: the centre the 16-bit forward stored y with (conv2d_fwd): mean / shift then describe
-    the stored values, the running mean the true one."""
+    """ysh: the centre the 16-bit forward stored y with (conv2d_fwd; its partials are those of
+    the stored values): mean / shift describe the stored values, the running mean is updated
+    with the true one (stored mean + ysh)."""
     _f32(ysh)
     check(lib.mauv_bn_stats_finalize(G, nblk, C, _p(pmean), _p(pm2), _p(pcnt), _p(gamma),
                                      _p(beta), _p(run_mean), _p(run_var), momentum, eps, _p(ws),

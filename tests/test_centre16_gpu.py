@@ -2,17 +2,20 @@
 engine.CENTRE_Y) on every 16-bit forward route and in the statistics finalize.
 
 A conv output that feeds a batch-statistics BatchNorm is stored as round16(y - c), c = that BN's
-running mean, while the epilogue's statistics partials stay those of y.  Checked here:
+centre: every 16-bit forward kernel starts its fp32 accumulators at -c (conv_epi16.h
+acc_start16), so the stored values and the statistics partials are those of y - c.  Checked here:
 * every forward kernel (the implicit GEMM's one-stage, short-K and long-K forms, the 3x3 LDS row
   images over 64 and 128 channels, the 256-row LDS-DMA tiles, the weight-stationary expansions,
-  the stems over shared im2col rows, the fold): the statistics partials are BIT-identical to the
-  uncentred run's, the stored values are within 2 ulp of float64 (conv - c), and — inputs with a
-  large channel mean, c near it — the reconstructed y = stored + c is closer to float64 than the
-  uncentred store (the point of the change);
-* mauv_bn_stats_finalize with y_shift: scale and the running statistics BIT-identical to the
-  uncentred finalize (the running mean takes the true mean), mean = mu - c, shift such that
-  stored * scale + shift = y * scale + shift_uncentred, and y_shift aliasing run_mean gives the
-  same result as a copy of it (it is read before the update).
+  the stems over shared im2col rows, the fold): the stored values within 2 ulp of float64
+  (conv - c); the partial means those of the uncentred run minus c and the M2 partials equal,
+  to fp32 rounding; — inputs with a large channel mean, c near it — the reconstructed
+  y = stored + c closer to float64 than the uncentred store, in BatchNorm's units (the point of
+  the change); and every route that keeps the implicit GEMM's k order (all but the chunked
+  3x3 row image) BIT-identical to it with the same centre, outputs and statistics;
+* mauv_bn_stats_finalize with y_shift on the centred partials: scale that of the uncentred
+  finalize (to fp32 rounding of the merge), mean = the stored values' mean, shift such that stored * scale + shift =
+  y * scale + shift_uncentred, the running statistics those of the true mean, and y_shift
+  aliasing run_mean gives the same result as a copy of it (it is read before the update).
 Reference op: F.conv2d followed by F.batch_norm in training mode inside torchvision's
 Bottleneck / stem (models/base_models.py:74-90)."""
 import math
@@ -70,6 +73,16 @@ def _ref(x, w, st, pd):
                                  padding=pd).permute(0, 2, 3, 1) for g in range(w.shape[0])])
 
 
+def _check_stats(s0, s1, c):
+    """Statistics partials of the centred run (s1) against the uncentred run's (s0): counts
+    equal, means shifted by the centre, M2 equal — to fp32 rounding of the accumulations."""
+    (m0, q0, n0), (m1, q1, n1) = s0, s1
+    assert torch.equal(n0, n1)
+    cc = c.view(1, 1, -1)
+    assert torch.allclose(m1, m0 - cc, rtol=0, atol=1e-5 * max(1.0, m0.abs().max().item()))
+    assert torch.allclose(q1, q0, rtol=1e-4, atol=1e-4 * q0.abs().max().item())
+
+
 def _check_centred(y0, y1, c, ref, dt, tag):
     """y0 uncentred, y1 centred (stored y - c) against the float64 truth ref.  The error that
     matters is the one BatchNorm sees, relative to each channel's spread: the rms error of
@@ -114,9 +127,22 @@ def test_centred_store_every_forward_route(case, dt):
         ops.set_route(**prev)
     (y0, s0), (y1, s1) = outs
     assert not torch.isnan(y1).any()
-    for a, b in zip(s0, s1):
-        assert torch.equal(a, b)          # the statistics are those of y, untouched
+    _check_stats(s0, s1, c)
     ec, eu = _check_centred(y0, y1, c, ref, dt, route)
+    # the same centre through the implicit GEMM: bit-identical where the route keeps its k order
+    # (haloc16 runs 64-channel chunks outer, taps inner: fp32-summation close, checked above)
+    if route not in ("pipe16", "haloc16"):
+        prev = ops.set_route(**ROUTE_SET["pipe16"])
+        try:
+            yp = torch.full_like(y1, float("nan"))
+            sp = _stat_bufs(ops, G, B, H, Cin, Cout, R, st, pd)
+            ops.conv2d_fwd(xd, wd, yp, G, B, H, H, Cin, Cout, R, st, pd, stats=sp, ysh=c)
+            torch.cuda.synchronize()
+        finally:
+            ops.set_route(**prev)
+        assert torch.equal(yp, y1), route
+        for a_, b_ in zip(sp, s1):
+            assert torch.equal(a_, b_), route
     print(f"\n{route} {str(dt)[6:]} K={Cin * R * R} N={Cout}: rms error / channel std, centred "
           f"{ec:.3e} uncentred {eu:.3e}")
 
@@ -148,8 +174,7 @@ def test_centred_store_stem_and_fold(dt):
         torch.cuda.synchronize()
         outs.append((y, stats))
     (y0, s0), (y1, s1) = outs
-    for a, b in zip(s0, s1):
-        assert torch.equal(a, b)
+    _check_stats(s0, s1, c)
     _check_centred(y0, y1, c, ref, dt, "stem")
     # the fold: the block output it writes through is untouched by the centre; y1 centred
     Gf, Bf, Hf, Cin, Cout = 2, 2, 16, 256, 128
@@ -177,8 +202,7 @@ def test_centred_store_stem_and_fold(dt):
         outs.append((out, y1f, stats))
     (o0, f0, t0), (o1, f1, t1) = outs
     assert torch.equal(o0, o1)
-    for a, b in zip(t0, t1):
-        assert torch.equal(a, b)
+    _check_stats(t0, t1, cf.to(dev))
     _check_centred(f0, f1, cf, reff, dt, "fold")
 
 
@@ -187,7 +211,7 @@ def test_finalize_with_centre(nblk):
     from mauv import ops
     G, C = 3, 96
     g = torch.Generator().manual_seed(11)
-    pm = (torch.randn(G, nblk, C, generator=g) * 0.1 + 40.0).to(dev)
+    pm = (torch.randn(G, nblk, C, generator=g) * 0.1 + 40.0).to(dev)   # partial means of y
     p2 = (torch.rand(G, nblk, C, generator=g) * 5 + 1).to(dev)
     pc = torch.full((G, nblk), 128.0, device=dev)
     gamma = (torch.rand(C, generator=g) + 0.5).to(dev)
@@ -200,18 +224,21 @@ def test_finalize_with_centre(nblk):
         ws = torch.empty(ops.bn_stats_workspace_floats(G, nblk, C), device=dev)
         out = [torch.empty(G, C, device=dev) for _ in range(4)]
         ysh = None if ysh_kind is None else (rm if ysh_kind == "alias" else rm0.clone())
-        ops.bn_stats_finalize(G, nblk, C, pm, p2, pc, gamma, beta, rm, rv, 0.1, 1e-5, ws, *out,
+        # a centred forward's partials are those of the stored values y - c
+        pmx = pm if ysh_kind is None else pm - rm0.view(1, 1, -1)
+        ops.bn_stats_finalize(G, nblk, C, pmx, p2, pc, gamma, beta, rm, rv, 0.1, 1e-5, ws, *out,
                               ysh=ysh)
         torch.cuda.synchronize()
         return out, rm, rv
     (m0, i0, s0, h0), rm_a, rv_a = run(None)
     (m1, i1, s1, h1), rm_b, rv_b = run("copy")
     (m2, i2, s2, h2), rm_c, rv_c = run("alias")
-    assert torch.equal(i0, i1) and torch.equal(s0, s1)
-    assert torch.equal(rm_a, rm_b) and torch.equal(rv_a, rv_b)       # true mean in running stats
+    # the spread does not move (the merge of shifted partial means rounds differently)
+    assert torch.allclose(i1, i0, rtol=1e-5, atol=0) and torch.allclose(s1, s0, rtol=1e-5, atol=0)
     assert torch.equal(m1, m2) and torch.equal(h1, h2) and torch.equal(rm_b, rm_c) and \
-        torch.equal(rv_b, rv_c)                                        # aliasing run_mean is safe
-    assert torch.allclose(m1, m0 - rm0, atol=1e-5, rtol=0)
+        torch.equal(rv_b, rv_c)                                # aliasing run_mean is safe
+    assert torch.allclose(m1, m0 - rm0, atol=1e-5, rtol=0)    # the stored values' mean
+    assert torch.allclose(rm_b, rm_a, atol=1e-5, rtol=0) and torch.allclose(rv_b, rv_a, rtol=1e-5)
     # a stored value v = y - c maps to the same normalised output as y did
     y = torch.randn(G, C, device=dev) * 2 + 40
     assert torch.allclose((y - rm0) * s1 + h1, y * s0 + h0, atol=1e-4, rtol=2e-6)
