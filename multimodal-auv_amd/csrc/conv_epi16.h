@@ -92,39 +92,6 @@ __device__ __forceinline__ void acc_start16(floatx16 (&acc)[MI][NI], const float
   }
 }
 
-// A pending BatchNorm's per-channel scale / shift staged into LDS without stalling the block
-// (the same reasoning as acc_shift16: a staging loop at the top of the kernel waited for its
-// global loads before the first tile load was issued).  xbn_fetch issues branch-free buffer
-// loads of channels tid + NT j (beyond n: out of range, 0) into registers; xbn_put writes them to
-// LDS once the tile loads are in flight (before the barrier that publishes the staged values).
-template <int J>
-__device__ __forceinline__ void xbn_fetch(float (&v)[J][2], const float* sc, const float* sh,
-                                          int n, int tid, int nt) {
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sc, (short)0, 4 * n,
-                                                                      0x00020000);
-  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)sh, (short)0, 4 * n,
-                                                                      0x00020000);
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int i = tid + nt * j;
-    const int off = i < n ? 4 * i : 0x7ffffff0;
-    v[j][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-    v[j][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rh, off, 0, 0));
-  }
-}
-template <int J>
-__device__ __forceinline__ void xbn_put(float* dsc, float* dsh, const float (&v)[J][2], int n,
-                                        int tid, int nt) {
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int i = tid + nt * j;
-    if (i < n) {
-      dsc[i] = v[j][0];
-      dsh[i] = v[j][1];
-    }
-  }
-}
-
 // Chan et al.'s merge of two row sets' (count, mean, M2) into the first: the 16-bit forwards'
 // statistics partials combine their 64-row halves with exactly these operations
 __device__ __forceinline__ void stats_merge(float na, float ma, float qa, float nb, float mb,
