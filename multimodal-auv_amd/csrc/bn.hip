@@ -11,6 +11,7 @@
 // Statistics: per-thread Welford over a row slab, Chan merges across threads and blocks
 // (double in the final merge) — no E[x^2]-E[x]^2 cancellation.
 #include <cstdlib>
+#include <type_traits>
 
 #include "h16.h"
 
@@ -364,24 +365,50 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const typename S::T* __res
   floatx8 s1 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2 = s1;
   if (t_r < rp) {
     const floatx8 mu = ldf8(mean + gc), is = ldf8(invstd + gc);
-    floatx8 sc, sh;
+    floatx8 sc = s1, sh = s1;
     if (relu && !out && !mask) { sc = ldf8(scale + gc); sh = ldf8(shift + gc); }
-    for (long long r = r0 + t_r; r < r1; r += rp) {
-      const long long o = go + r * C + c0;
-      const floatx8 yv = S::ld8(y + o);
-      floatx8 dz = S::ld8(dout + o);
-      if (mask) {  // ReLU mask bits written by the forward's bn_apply (one byte per 8 channels)
-        const unsigned m = mask[(go + r * C + c0) >> 3];
+    // RU rows per thread per step: every row's loads issued before the first is consumed (one
+    // row at a time, with the ReLU-source branches inside the loop, left two 16-byte loads in
+    // flight per lane: latency-bound); rows past r1 add zeros, so the sums keep their row order.
+    // The ReLU source is chosen once, outside the row loop.
+    constexpr int RU = 4;
+    const floatx8 z8 = s1;
+    auto rows = [&](auto src) {
+      constexpr int SRC = decltype(src)::value;  // 0 none, 1 mask bits, 2 out, 3 y*scale+shift
+      for (long long r = r0 + t_r; r < r1; r += RU * rp) {
+        typename S::R8 yr[RU], dr[RU], pr[RU];
+        unsigned m[RU];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) dz[e] = (m >> e) & 1u ? dz[e] : 0.f;
-      } else if (relu) {
-        const floatx8 pre = out ? S::ld8(out + o) : yv * sc + sh;
+        for (int u = 0; u < RU; ++u) {
+          // rows past r1 re-read row r (unconditional loads, no branch to wait inside)
+          const long long rr = r + (long long)u * rp;
+          const long long o = go + (rr < r1 ? rr : r) * C + c0;
+          yr[u] = S::raw8(y + o);
+          dr[u] = S::raw8(dout + o);
+          if constexpr (SRC == 1) m[u] = mask[o >> 3];
+          if constexpr (SRC == 2) pr[u] = S::raw8(out + o);
+        }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) dz[e] = pre[e] > 0.f ? dz[e] : 0.f;
+        for (int u = 0; u < RU; ++u) {
+          const floatx8 yv = S::cvt8(yr[u]);
+          floatx8 dz = r + (long long)u * rp < r1 ? S::cvt8(dr[u]) : z8;
+          if constexpr (SRC == 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dz[e] = (m[u] >> e) & 1u ? dz[e] : 0.f;
+          } else if constexpr (SRC >= 2) {
+            const floatx8 p = SRC == 2 ? S::cvt8(pr[u]) : yv * sc + sh;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dz[e] = p[e] > 0.f ? dz[e] : 0.f;
+          }
+          s1 += dz;
+          s2 += dz * (yv - mu) * is;
+        }
       }
-      s1 += dz;
-      s2 += dz * (yv - mu) * is;
-    }
+    };
+    if (mask) rows(std::integral_constant<int, 1>());
+    else if (!relu) rows(std::integral_constant<int, 0>());
+    else if (out) rows(std::integral_constant<int, 2>());
+    else rows(std::integral_constant<int, 3>());
   }
   __shared__ float sh1[2048], sh2[2048];  // [rp][C], rp * C = 8 * 256
   if (t_r < rp) {
@@ -619,24 +646,50 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rows(const typename S::T* __
   floatx8 sh = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (relu && !out && !mask) sh = ldf8(shift + gc);
   const long long base = (long long)g * M * C + c0;
-#pragma unroll 2
-  for (long long r = r0 + t_r; r < r1; r += rp) {
-    const long long o = base + r * C;
-    floatx8 dz = S::ld8(dout + o);
-    const floatx8 yv = S::ld8(y + o);
-    if (mask) {
-      const unsigned m = mask[o >> 3];
+  // RU rows per step with every load (dz, y, the mask byte / out) issued before the first use
+  // and the ReLU source chosen outside the loop: in one loop body with the branches inside,
+  // each row waited for dz and y, then for its mask byte, then stored — three latencies a row
+  constexpr int RU = 2;
+  auto rows = [&](auto src) {
+    constexpr int SRC = decltype(src)::value;  // 0 none, 1 mask bits, 2 out, 3 y*scale+shift
+    for (long long r = r0 + t_r; r < r1; r += RU * rp) {
+      typename S::R8 yr[RU], dr[RU], pr[RU];
+      unsigned m[RU];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) dz[e] = (m >> e) & 1u ? dz[e] : 0.f;
-    } else if (relu) {
-      const floatx8 pre = out ? S::ld8(out + o) : yv * sc + sh;
+      for (int u = 0; u < RU; ++u) {
+        const long long rr = r + (long long)u * rp;
+        const long long o = base + (rr < r1 ? rr : r) * C;   // past r1: row r again, not stored
+        dr[u] = S::raw8(dout + o);
+        yr[u] = S::raw8(y + o);
+        if constexpr (SRC == 1) m[u] = mask[o >> 3];
+        if constexpr (SRC == 2) pr[u] = S::raw8(out + o);
+      }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) dz[e] = pre[e] > 0.f ? dz[e] : 0.f;
+      for (int u = 0; u < RU; ++u) {
+        const long long rr = r + (long long)u * rp;
+        const floatx8 yv = S::cvt8(yr[u]);
+        floatx8 dz = S::cvt8(dr[u]);
+        if constexpr (SRC == 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dz[e] = (m[u] >> e) & 1u ? dz[e] : 0.f;
+        } else if constexpr (SRC >= 2) {
+          const floatx8 p = SRC == 2 ? S::cvt8(pr[u]) : yv * sc + sh;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dz[e] = p[e] > 0.f ? dz[e] : 0.f;
+        }
+        if (rr < r1) {
+          const long long o = base + rr * C;
+          const floatx8 xh = (yv - mu) * is;
+          S::st8(dy + o, sc * (dz - a1 - xh * a2));
+          if (dres) S::st8(dres + o, dz);
+        }
+      }
     }
-    const floatx8 xh = (yv - mu) * is;
-    S::st8(dy + o, sc * (dz - a1 - xh * a2));
-    if (dres) S::st8(dres + o, dz);
-  }
+  };
+  if (mask) rows(std::integral_constant<int, 1>());
+  else if (!relu) rows(std::integral_constant<int, 0>());
+  else if (out) rows(std::integral_constant<int, 2>());
+  else rows(std::integral_constant<int, 3>());
 }
 
 // Row-walk geometry: <= 2 rows per thread (measured 2 vs 4 vs 8 vs 16: inference 10.40-10.43k vs 10.32-10.35k vs 10.16-10.19k vs 10.12k

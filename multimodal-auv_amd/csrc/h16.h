@@ -143,6 +143,11 @@ struct SF32 {
     *(floatx4*)p = a;
     *(floatx4*)(p + 4) = b;
   }
+  // 8 elements as loaded (R8) and converted at their use (cvt8): keeps a batch of rows in
+  // flight in as few registers as the storage format needs
+  typedef floatx8 R8;
+  static __device__ __forceinline__ R8 raw8(const T* p) { return ld8(p); }
+  static __device__ __forceinline__ floatx8 cvt8(const R8& r) { return r; }
 };
 
 template <int DT>
@@ -167,6 +172,9 @@ struct S16 {
   }
   static __device__ __forceinline__ floatx8 ld8(const T* p) { return unpack8<DT>(*(const u32x4*)p); }
   static __device__ __forceinline__ void st8(T* p, floatx8 v) { *(u32x4*)p = pack8<DT>(v); }
+  typedef u32x4 R8;
+  static __device__ __forceinline__ R8 raw8(const T* p) { return *(const u32x4*)p; }
+  static __device__ __forceinline__ floatx8 cvt8(const R8& r) { return unpack8<DT>(r); }
 };
 
 }  // namespace mauv
