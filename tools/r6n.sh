@@ -8,9 +8,9 @@ timeout -k 10 600 python -u -m pytest -x -v -rP --timeout 300 --timeout-method t
   tests/test_kernels_gpu.py tests/test_kernels16_gpu.py tests/test_bwd_fusion_gpu.py \
   > $O/r6n_tests.log 2>&1; r=$?; tail -2 $O/r6n_tests.log; [ $r -eq 0 ] || { grep -E "FAILED|Error" $O/r6n_tests.log | head -20; exit 1; }
 for d in bf16 fp32; do
-  MAUV_LIB=$HL MAUV_CENTRE_Y=0 timeout -k 10 300 python -u tools/lib_bitcmp.py save $O/bc_head_$d.pt $d || exit 1
-  MAUV_CENTRE_Y=0 timeout -k 10 300 python -u tools/lib_bitcmp.py save $O/bc_new_$d.pt $d || exit 1
-  python tools/lib_bitcmp.py cmp $O/bc_head_$d.pt $O/bc_new_$d.pt | tee -a $O/r6n_bitcmp.txt
+  MAUV_LIB=$HL MAUV_CENTRE_Y=0 timeout -k 10 300 python -u tools/lib_bitcmp.py save /tmp/bc_head_$d.pt $d || exit 1
+  MAUV_CENTRE_Y=0 timeout -k 10 300 python -u tools/lib_bitcmp.py save /tmp/bc_new_$d.pt $d || exit 1
+  python tools/lib_bitcmp.py cmp /tmp/bc_head_$d.pt /tmp/bc_new_$d.pt | tee -a $O/r6n_bitcmp.txt
 done
 C="--steps 2 --warmup 1 --no-cpu-baseline --exact-steps 0 --no-roofline --no-sweep --no-infer"
 MAUV_TRUNK_STREAMS=0 MAUV_LIB=$HL MAUV_CENTRE_Y=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/b16h -o run -- python3 bench.py $C --dtype bf16 --no-bf16 > $O/b16h.log 2>&1 || exit 1
