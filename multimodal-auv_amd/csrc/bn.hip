@@ -593,30 +593,51 @@ __global__ __launch_bounds__(256) void bn_apply_rows(const typename S::T* __rest
   floatx8 rsc, rsh;
   if (res_scale) { rsc = ldf8(res_scale + gc); rsh = ldf8(res_shift + gc); }
   const long long base = (long long)g * M * C + c0;
-#pragma unroll 2
-  for (long long r = r0 + t_r; r < r1; r += rp) {
-    const long long o = base + r * C;
-    floatx8 v = S::ld8(y + o) * sc + sh;
-    if (res) {
-      floatx8 rv = S::ld8(res + o);
-      if (res_scale) rv = rv * rsc + rsh;
-      v += rv;
-    }
-    if (relu) {
+  // RU rows per step, every row's loads (y, the residual) issued before the first is used, the
+  // residual's form chosen outside the loop (bn_bwd_apply_rows' reasoning)
+  constexpr int RU = 2;
+  auto rows = [&](auto rk) {
+    constexpr int RES = decltype(rk)::value;  // 0 none, 1 res, 2 res * res_scale + res_shift
+    for (long long r = r0 + t_r; r < r1; r += RU * rp) {
+      typename S::R8 yr[RU], rr_[RU];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
-    }
-    S::st8(out + o, v);
-    if (mask) {  // bit e = (stored out > 0): the value as rounded to the storage type
-      alignas(16) typename S::T tmp[8];
-      S::st8(tmp, v);
-      const floatx8 q = S::ld8(tmp);
-      unsigned m = 0;
+      for (int u = 0; u < RU; ++u) {
+        const long long rr = r + (long long)u * rp;
+        const long long o = base + (rr < r1 ? rr : r) * C;   // past r1: row r again, not stored
+        yr[u] = S::raw8(y + o);
+        if constexpr (RES != 0) rr_[u] = S::raw8(res + o);
+      }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) m |= (q[e] > 0.f ? 1u : 0u) << e;
-      mask[o >> 3] = (unsigned char)m;
+      for (int u = 0; u < RU; ++u) {
+        const long long rr = r + (long long)u * rp;
+        floatx8 v = S::cvt8(yr[u]) * sc + sh;
+        if constexpr (RES != 0) {
+          floatx8 rv = S::cvt8(rr_[u]);
+          if constexpr (RES == 2) rv = rv * rsc + rsh;
+          v += rv;
+        }
+        if (relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        }
+        if (rr >= r1) continue;
+        const long long o = base + rr * C;
+        S::st8(out + o, v);
+        if (mask) {  // bit e = (stored out > 0): the value as rounded to the storage type
+          alignas(16) typename S::T tmp[8];
+          S::st8(tmp, v);
+          const floatx8 q = S::ld8(tmp);
+          unsigned m = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m |= (q[e] > 0.f ? 1u : 0u) << e;
+          mask[o >> 3] = (unsigned char)m;
+        }
+      }
     }
-  }
+  };
+  if (!res) rows(std::integral_constant<int, 0>());
+  else if (!res_scale) rows(std::integral_constant<int, 1>());
+  else rows(std::integral_constant<int, 2>());
 }
 
 template <class S>
