@@ -52,7 +52,7 @@ int mauv_abi_version(void);
  *   big16, big16_min_k  16-bit forwards on 256-row LDS-DMA tiles (conv_big16.hip): 1 (default)
  *                   the shapes where they measured faster (1x1, no pending BN, K >= 512,
  *                   N >= 256, >= 512 tiles), 2 every covered forward with K >= big16_min_k
- *                   (default 512), 0 none.
+ *                   (default and minimum 512: the K range its tests cover), 0 none.
  *   haloc16         16-bit 3x3 / stride-1 forwards and data gradients over 128-512 channels
  *                   through the chunked LDS row image (conv_haloc16.hip): 1 (default) with
  *                   32 x 64 wave tiles, 2 with 64 x 64 wave tiles, 3 the forwards only, 0 none.

@@ -59,7 +59,7 @@ MAUV_API int mauv_set_route(const MauvRoute* in) {
     bad = "f32_math must be 0 (exact), 3 (split3), 5 (split1) or 6 (split)";
   else if (r.halo3 != 0 && r.halo3 != 1) bad = "halo3 must be 0 or 1";
   else if (r.big16 < 0 || r.big16 > 2) bad = "big16 must be 0, 1 or 2";
-  else if (r.big16_min_k < 64) bad = "big16_min_k must be >= 64";
+  else if (r.big16_min_k < 512) bad = "big16_min_k must be >= 512 (the K range conv_big16 is tested on)";
   else if (r.haloc16 < 0 || r.haloc16 > 3) bad = "haloc16 must be 0..3";
   else if (r.expand16 < 0 || r.expand16 > 3) bad = "expand16 must be 0..3";
   else if (r.reparam_kernels < 0 || r.reparam_kernels > 3) bad = "reparam_kernels must be 0..3";

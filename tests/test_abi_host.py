@@ -74,7 +74,9 @@ def test_route_host_record():
             ops.set_route(halo3=0, haloc16=9)   # rejected as a whole: halo3 stays 1
         assert ops.route()["halo3"] == 1 and ops.f32_math() == "split3"
         assert ops.set_expand16(3) == 1 and ops.set_expand16(None) == 3
-        assert ops.set_big16(True, 256) == 1 and ops.route()["big16_min_k"] == 256
+        assert ops.set_big16(True, 1024) == 1 and ops.route()["big16_min_k"] == 1024
+        with pytest.raises(RuntimeError, match="big16_min_k"):
+            ops.set_big16(True, 256)    # below the K range conv_big16 is tested on
         with pytest.raises(ValueError):
             ops.set_route(dma16=1)
         bad = MauvRoute()

@@ -7,7 +7,7 @@ has it (conv2, conv3) and the statistics epilogue; and, for the 1x1 / stride-1 s
 GEMM on the same operands ("bmm": torch.bmm [G, M, K] x [G, K, N] through --blas, without the
 BN transform or the statistics the conv kernels also do).
 
-    python tools/fwd_ab.py [--dtype bf16|f16] [--G 5] [--B 64] [--min-k 512] [--rounds 3]
+    python tools/fwd_ab.py [--dtype bf16|f16] [--G 5] [--B 64] [--min-k 512 (the minimum)] [--rounds 3]
                            [--blas hipblaslt|rocblas] [--only1x1]
 """
 import argparse
