@@ -360,7 +360,27 @@ void conv_split_f32(const ConvArgs a) {
       }
   };
 
-  if constexpr (SEQ) {
+  // SEQ with the BN-partials epilogue (BP): its register budget is the pipelined kernel's (four
+  // waves per SIMD), so the next stage's loads go out before this stage's MFMAs — one LDS buffer,
+  // two register stages — instead of each stage waiting for its own loads
+  constexpr bool SEQ_PF = SEQ && BP;
+  if constexpr (SEQ_PF) {
+    St S0, S1;
+    load(S0, 0);
+    for (int t = 0; t < nt; t += 2) {
+      split_store(S0, 0);
+      __syncthreads();
+      if (t + 1 < nt) load(S1, t + 1);
+      compute(0);
+      __syncthreads();  // the next stage / the epilogue scratch reuses the buffer
+      if (t + 1 >= nt) break;
+      split_store(S1, 0);
+      __syncthreads();
+      if (t + 2 < nt) load(S0, t + 2);
+      compute(0);
+      __syncthreads();
+    }
+  } else if constexpr (SEQ) {
     St S0;
     if constexpr (XBN && MODE == FWD) __syncthreads();  // xbn staged
     for (int t = 0; t < nt; ++t) {
