@@ -340,28 +340,31 @@ __device__ __forceinline__ void staged_epilogue_f32(const ConvArgs& a, floatx16 
       bsh = *(const floatx4*)(a.bp_sh + (long long)g * a.N + bcol);
     }
   }
+  // The prefetch only issues loads: the mask bytes are kept as loaded (shifted at the chunk's
+  // use) and the ReLU test on y*scale + shift is made there too — an operation on a loaded value
+  // inside the prefetch made every prefetch wait for its own loads (one chunk in flight, not two)
   auto prefetch = [&](int pass, int k) {
     const int q = k % PFD;
     long long o = 0;
     pa[q] = pd[q] = py[q] = floatx4{0.f, 0.f, 0.f, 0.f};
-    pm[q] = 0xfu;
-    pr[q] = 0xfu;
+    pm[q] = 0xfffu;   // (all four bits set after any in-byte shift)
+    pr[q] = 0xfffu;
     if (MODE == DGRAD && k < CPT && chunk(pass, tid + k * NT, o)) {
       if (a.addend) {
         pa[q] = *(const floatx4*)(a.addend + o);
-        if (a.add_mask) pm[q] = (unsigned)(a.add_mask[o >> 3] >> (o & 7));
+        if (a.add_mask) pm[q] = a.add_mask[o >> 3];
       }
       if (a.accumulate) pd[q] = *(const floatx4*)(outp + o);
       if (bst) {
         py[q] = *(const floatx4*)(a.bp_y + o);
         if (a.bp_relu) {
           if (a.bp_mask) {
-            pr[q] = (unsigned)(a.bp_mask[o >> 3] >> (o & 7));
-          } else {
-            const floatx4 pre = a.bp_out ? *(const floatx4*)(a.bp_out + o) : py[q] * bsc + bsh;
+            pr[q] = a.bp_mask[o >> 3];
+          } else if (a.bp_out) {  // (the BN's materialised output: rare) tested here
+            const floatx4 pre = *(const floatx4*)(a.bp_out + o);
             pr[q] = 0u;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) pr[q] |= (pre[e] > 0.f ? 1u : 0u) << e;
+            for (int e = 0; e < 4; ++e) pr[q] |= (pre[e] > 0.f ? 1u : 0u) << (e + (o & 7));
           }
         }
       }
@@ -390,15 +393,24 @@ __device__ __forceinline__ void staged_epilogue_f32(const ConvArgs& a, floatx16 
         const int rl = c / CPR, cc = c - rl * CPR;
         floatx4 v = *(const floatx4*)(stile + rl * SLD + 4 * cc);
         if constexpr (MODE == DGRAD) {
+          const unsigned sh = (unsigned)(o & 7);   // this chunk's first bit in its mask byte
+          const unsigned am = pm[q] >> sh;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            if ((pm[q] >> e) & 1u) v[e] += pa[q][e];
+            if ((am >> e) & 1u) v[e] += pa[q][e];
             v[e] += pd[q][e];
           }
           if (bst) {
+            unsigned rm = pr[q] >> sh;
+            if (a.bp_relu && !a.bp_mask && !a.bp_out) {
+              const floatx4 pre = py[q] * bsc + bsh;
+              rm = 0u;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) rm |= (pre[e] > 0.f ? 1u : 0u) << e;
+            }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float dz = (pr[q] >> e) & 1u ? v[e] : 0.f;
+              const float dz = (rm >> e) & 1u ? v[e] : 0.f;
               b1[e] += dz;
               b2[e] += dz * (py[q][e] - bmu[e]) * bis[e];
             }
